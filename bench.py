@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""bench.py -- programmable bootstraps/sec at PARAM_MESSAGE_2_CARRY_2 on 1/2/4/8 MI355X.
+
+BASELINE.json metric "programmable bootstraps/sec (PARAM_MESSAGE_2_CARRY_2) at 1/2/4/8 MI355X",
+workload = BASELINE config 2: a batch of 4096 independent classic PBS per GPU, identity LUT
+(PARAM_MESSAGE_2_CARRY_2_KS_PBS: n=742, k=1, N=2048, L=1, base 2^23).  One step = one PBS
+launch over the GPU's batch (blind rotation + sample extraction), inputs resident in HBM.
+
+Multi-GPU (weak scaling): one process per GPU launched by torch.distributed.run; the standard
+BSK is generated once on rank 0 and broadcast ONCE over RCCL (xGMI), each rank converts it to
+the Fourier domain on its own GPU, then each rank bootstraps its own batch -- no collective in
+the timed loop except the bracketing barriers.  value = sum of PBS over ranks / max wall time.
+
+Also printed: roofline of the dominant kernel (pbs_classic_kernel) -- BSK-streaming HBM model
+ with the FP64 fraction beside it -- and the CPU baseline (oracle C restatement,
+1 PBS per thread, rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "tfhe-rs-odd_amd"))
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
+FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 vector (= matrix) spec, SURVEY.md 8d
+
+
+def pbs_algorithmic_bytes(p) -> int:
+    """SURVEY.md 8d BSK-streaming model: |BSK_fourier| + 8(n+1) + 8(kN+1) + 8(k+1)N."""
+    M = p.polynomial_size // 2
+    k1 = p.glwe_dimension + 1
+    fbsk = p.lwe_dimension * p.pbs_level * k1 * k1 * M * 16
+    return fbsk + 8 * (p.lwe_dimension + 1) + 8 * (p.glwe_dimension * p.polynomial_size + 1) + 8 * k1 * p.polynomial_size
+
+
+def pbs_flops(p) -> float:
+    """per CMUX ((k+1)L + (k+1)) (5 M log2 M + 6 M) + (k+1)^2 L M 8, times n."""
+    M = p.polynomial_size // 2
+    k1 = p.glwe_dimension + 1
+    per = (k1 * p.pbs_level + k1) * (5 * M * math.log2(M) + 6 * M) + k1 * k1 * p.pbs_level * M * 8
+    return per * p.lwe_dimension
+
+
+def load_pmc_traffic(batch: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json,
+    FETCH_SIZE doubled per MI355X_MICROARCH.md 'HBM' + WRITE_SIZE), scaled to this batch."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+        return float(d["hbm_bytes_per_pbs"]) * batch
+    except Exception:
+        return None
+
+
+def cpu_baseline(params, bsk, cts, acc, threads: int):
+    """Oracle (C restatement of the reference fft64 PBS) on the host cores, one PBS per thread,
+    as the reference's pbs_throughput bench (benches/core_crypto/pbs_bench.rs:430-549)."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+
+    O.build()
+    fb = O.FourierBsk(bsk, params.lwe_dimension, params.glwe_dimension, params.polynomial_size,
+                      params.pbs_base_log, params.pbs_level)
+    t = time.perf_counter()
+    fb.pbs(cts[:1], acc, threads=1)
+    t1 = time.perf_counter() - t
+    count = max(threads, int(round(15.0 / max(t1, 1e-3))))
+    count = min(((count + threads - 1) // threads) * threads, cts.shape[0])
+    t = time.perf_counter()
+    fb.pbs(cts[:count], acc, threads=threads)
+    wall = time.perf_counter() - t
+    return {
+        "value": count / wall,
+        "unit": "PBS/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"{count} PBS of the same PARAM_MESSAGE_2_CARRY_2 batch, oracle C restatement of the "
+                   f"reference fft64 PBS, 1 PBS per thread on {threads} threads ({wall:.1f} s wall); "
+                   f"single-thread latency {t1 * 1e3:.1f} ms/PBS (reference published 16.6 ms KS+PBS "
+                   f"on Xeon 8375C AVX-512, benchmarks.md:42)"),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=4096, help="ciphertexts per GPU per step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--seed", type=int, default=1)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from tfhe_mi355 import Engine, client, fill_accumulator
+    from tfhe_mi355.distributed import broadcast_u64, env_rank_world
+    from tfhe_mi355.parameters import PARAM_MESSAGE_2_CARRY_2_KS_PBS as P
+
+    rank, world, local = env_rank_world()
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    def barrier():
+        if world > 1:
+            t = torch.ones(1, device=device)
+            dist.all_reduce(t)
+        torch.cuda.synchronize()
+
+    B = args.batch
+    eng = Engine(P, local)
+    # secret keys: derived from the seed on every rank (cheap); the BSK once on rank 0
+    lwe_sk = client.gen_binary_key(args.seed, 1, P.lwe_dimension)
+    glwe_sk = client.gen_binary_key(args.seed, 2, P.big_lwe_dimension)
+    bsk_len = P.lwe_dimension * P.pbs_level * (P.glwe_dimension + 1) ** 2 * P.polynomial_size
+    bsk = None
+    t_key = time.perf_counter()
+    if rank == 0:
+        bsk = client.gen_bootstrap_key(args.seed + 100, lwe_sk, glwe_sk, P.glwe_dimension, P.polynomial_size,
+                                       P.pbs_base_log, P.pbs_level, P.glwe_modular_std_dev)
+    t_gen = time.perf_counter() - t_key
+    t_bc = time.perf_counter()
+    d_bsk = broadcast_u64(bsk, bsk_len, 0, device)  # one RCCL broadcast of 48.6 MB
+    torch.cuda.synchronize()
+    t_bc = time.perf_counter() - t_bc
+    eng.convert_bootstrap_key_device(d_bsk, bsk_len)
+    torch.cuda.synchronize()
+    del d_bsk
+
+    rng = np.random.default_rng(args.seed * 1000 + rank)
+    msgs = rng.integers(0, 16, B).astype(np.uint64)
+    cts = client.lwe_encrypt(args.seed * 1000 + rank, lwe_sk, msgs * np.uint64(P.delta), P.lwe_modular_std_dev)
+    acc = fill_accumulator(P, lambda x: x)
+    d_in = torch.from_numpy(cts.view(np.int64)).to(device)
+    d_out = torch.zeros((B, P.big_lwe_dimension + 1), dtype=torch.int64, device=device)
+    d_lut = torch.from_numpy(acc.view(np.int64)).to(device)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        eng.programmable_bootstrap_async(d_in, d_out, d_lut, 1, B, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for s, e in evs:
+        s.record(stream)
+        step()
+        e.record(stream)
+    barrier()
+    wall = time.perf_counter() - t0
+    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
+    tt = torch.tensor([wall], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    wall_max = float(tt.item())
+
+    # correctness of this rank's outputs (decrypt with the big key)
+    out = d_out.cpu().numpy().view(np.uint64)
+    dec = client.decode(client.lwe_decrypt(glwe_sk, out), P.delta) % np.uint64(16)
+    ok = int(np.count_nonzero(dec == msgs))
+    okt = torch.tensor([ok, B], dtype=torch.int64, device=device)
+    if world > 1:
+        dist.all_reduce(okt)
+
+    if rank == 0:
+        total = world * B * args.steps
+        value = total / wall_max
+        per_launch_bytes = pbs_algorithmic_bytes(P) * B
+        achieved = per_launch_bytes / (kernel_ms * 1e-3) / 1e9
+        flops = pbs_flops(P) * B / (kernel_ms * 1e-3) / 1e12
+        line = {
+            "metric": "programmable bootstraps/sec (PARAM_MESSAGE_2_CARRY_2) at 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "PBS/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": wall_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded LWE encryptions of uniform 4-bit messages; keys from the engine's client-side keygen)",
+            "config": {
+                "workload": "BASELINE config 2: batch of 4096 independent classic PBS per GPU, identity LUT",
+                "parameters": "PARAM_MESSAGE_2_CARRY_2_KS_PBS (n=742, k=1, N=2048, pbs 2^23 x 1)",
+                "batch_per_gpu": B,
+                "global_batch": world * B,
+                "parallelism": f"dp{world} (batch shards, BSK replicated by one RCCL broadcast)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "model": "BSK-streaming (SURVEY.md 8d): 48,682,816 B per PBS; frac > 1 would mean reuse beyond streaming",
+                "kernel": "pbs_classic_kernel<2048,1,1>",
+                "kernel_ms": kernel_ms,
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": load_pmc_traffic(B),
+                "fp64": {"achieved": flops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": flops / FP64_PEAK_TFLOPS,
+                         "flop_per_pbs": pbs_flops(P)},
+            },
+            "check": {"decrypted_ok": int(okt[0].item()), "of": int(okt[1].item())},
+            "setup": {"bsk_keygen_s": t_gen, "bsk_broadcast_s": t_bc},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            line["cpu_baseline"] = cpu_baseline(P, bsk, cts, acc, threads)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

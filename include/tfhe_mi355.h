@@ -1,0 +1,163 @@
+/*
+ * tfhe_mi355.h -- C ABI of the MI355X programmable-bootstrap engine.
+ *
+ * This is the drop-in boundary for the reference's PBS hot path (tfhe-rs-odd = tfhe 0.5.0
+ * fork, CPU-only Rust).  Each entry point names the reference interface it replaces.  The
+ * Rust-side binding a maintainer would add (a `ShortintBootstrappingKey::Gpu` arm calling
+ * these functions through `extern "C"`) is shown in INTEGRATION.md.
+ *
+ * Conventions (mirroring tfhe/src/c_api/utils.rs:3-73 and c_api/core_crypto/mod.rs:37-121):
+ *   - every function returns int: 0 = success, 1 = failure; the failure text is returned by
+ *     tfhe_mi355_last_error() (thread-local);
+ *   - out-params of handle type are nulled first (c_api/shortint/server_key/pbs.rs:25-28);
+ *   - buffers are plain uint64_t arrays in the reference's entity layouts:
+ *       LWE ciphertext   = mask[0..n) || body                      (lwe_ciphertext.rs:598-599)
+ *       GLWE ciphertext  = k mask polys || body poly, N coeffs each (glwe_ciphertext.rs:423-425)
+ *       standard BSK     = [n][L][k+1 rows][k+1 polys][N]          (ggsw_ciphertext.rs:185-216)
+ *       multi-bit BSK    = [n/g][2^g][L][k+1][k+1][N]              (lwe_multi_bit_bootstrap_key.rs)
+ *       KSK              = [in_dim][L_ks][out_dim+1], levels stored L..1
+ *                          (lwe_keyswitch_key.rs:102-108, lwe_keyswitch_key_generation.rs:109);
+ *   - "_async" entry points take DEVICE pointers and a hipStream_t (as void*), enqueue the work
+ *     and return immediately; the others take HOST pointers and return after the outputs are
+ *     written (synchronous);
+ *   - a context is bound to one GPU; calls on one context are serialised by an internal mutex,
+ *     so rayon-style concurrent callers sharing a key are safe (SURVEY.md 8b "Threading").
+ */
+#ifndef TFHE_MI355_H
+#define TFHE_MI355_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TFHE_MI355_OK 0
+#define TFHE_MI355_ERROR 1
+
+typedef struct TfheMi355Context TfheMi355Context;
+
+/* Parameter set.  Mirrors shortint ClassicPBSParameters / MultiBitPBSParameters
+ * (shortint/parameters/mod.rs:60-75, multi_bit.rs:173-190). grouping_factor = 0: classic PBS. */
+typedef struct {
+    uint32_t lwe_dimension;   /* n: small LWE dimension (PBS input)            */
+    uint32_t glwe_dimension;  /* k                                             */
+    uint32_t polynomial_size; /* N                                             */
+    uint32_t pbs_base_log;
+    uint32_t pbs_level;
+    uint32_t ks_base_log;
+    uint32_t ks_level;
+    uint32_t message_modulus;
+    uint32_t carry_modulus;
+    uint32_t grouping_factor; /* 0 = classic; 2, 3, 4 = multi-bit              */
+} TfheMi355Parameters;
+
+/* Thread-local text of the last failure ("" if none). */
+const char *tfhe_mi355_last_error(void);
+
+/* Number of visible GPUs. */
+int tfhe_mi355_device_count(int *out_count);
+
+/* Create / destroy an engine context on `device`.
+ * Replaces Fft::new + the shortint engine's thread-local buffers
+ * (fft64/math/fft/mod.rs:146-193, shortint/engine/mod.rs:23-70,163-235). */
+int tfhe_mi355_context_create(const TfheMi355Parameters *params, int device,
+                              TfheMi355Context **out_ctx);
+int tfhe_mi355_context_destroy(TfheMi355Context *ctx);
+
+/* Upload a standard-domain (u64) bootstrapping key and convert it to the engine's Fourier
+ * layout on the GPU.  Replaces convert_standard_lwe_bootstrap_key_to_fourier /
+ * par_convert_standard_lwe_bootstrap_key_to_fourier (lwe_bootstrap_key_conversion.rs:21-151)
+ * and, for grouping_factor > 0, par_convert_standard_lwe_multi_bit_bootstrap_key_to_fourier
+ * (lwe_multi_bit_bootstrap_key_conversion.rs).  `len` is in u64 words. */
+int tfhe_mi355_bootstrap_key_upload(TfheMi355Context *ctx, const uint64_t *standard_bsk, size_t len);
+
+/* Device-pointer form of the above (standard BSK already in this context's GPU memory). */
+int tfhe_mi355_bootstrap_key_convert_async(TfheMi355Context *ctx, const uint64_t *d_standard_bsk,
+                                           size_t len, void *stream);
+
+/* Fourier BSK held by the context: device pointer and byte size, for RCCL broadcast of the
+ * converted key to the other GPUs of the node. */
+int tfhe_mi355_bootstrap_key_fourier(TfheMi355Context *ctx, void **d_ptr, size_t *bytes);
+/* Mark the Fourier BSK as valid after it was filled externally (e.g. by a broadcast into the
+ * buffer returned above). */
+int tfhe_mi355_bootstrap_key_fourier_set_ready(TfheMi355Context *ctx);
+
+/* Upload a keyswitching key (big LWE key -> small LWE key).  `len` in u64 words. */
+int tfhe_mi355_keyswitch_key_upload(TfheMi355Context *ctx, const uint64_t *ksk, size_t len);
+/* Device-pointer form of the KSK upload (device-to-device copy on `stream`). */
+int tfhe_mi355_keyswitch_key_upload_async(TfheMi355Context *ctx, const uint64_t *d_ksk, size_t len,
+                                          void *stream);
+int tfhe_mi355_keyswitch_key_device(TfheMi355Context *ctx, void **d_ptr, size_t *bytes);
+int tfhe_mi355_keyswitch_key_set_ready(TfheMi355Context *ctx);
+
+/* Batched programmable bootstrap: for c < count,
+ *   lwe_out[c] = PBS(lwe_in[c], luts[lut_indexes ? lut_indexes[c] : 0]).
+ * lwe_in: count x (n+1); lwe_out: count x (k*N+1); luts: lut_count x (k+1)*N (GLWE accumulators,
+ * e.g. from shortint generate_lookup_table).
+ * Replaces programmable_bootstrap_lwe_ciphertext[_mem_optimized]
+ * (lwe_programmable_bootstrapping.rs:1017-1111) = FourierLweBootstrapKeyView::bootstrap
+ * (fft64/crypto/bootstrap.rs:346-380) and, for grouping_factor > 0,
+ * multi_bit_programmable_bootstrap_lwe_ciphertext (lwe_multi_bit_programmable_bootstrapping.rs:1035). */
+int tfhe_mi355_programmable_bootstrap(TfheMi355Context *ctx, const uint64_t *lwe_in, uint64_t *lwe_out,
+                                      const uint64_t *luts, size_t lut_count,
+                                      const uint32_t *lut_indexes, size_t count);
+int tfhe_mi355_programmable_bootstrap_async(TfheMi355Context *ctx, const uint64_t *d_lwe_in,
+                                            uint64_t *d_lwe_out, const uint64_t *d_luts,
+                                            size_t lut_count, const uint32_t *d_lut_indexes,
+                                            size_t count, void *stream);
+
+/* Batched LWE keyswitch (big key -> small key): lwe_in count x (k*N+1) -> lwe_out count x (n+1).
+ * Replaces keyswitch_lwe_ciphertext (lwe_keyswitch.rs:96-170). */
+int tfhe_mi355_keyswitch(TfheMi355Context *ctx, const uint64_t *lwe_in, uint64_t *lwe_out, size_t count);
+int tfhe_mi355_keyswitch_async(TfheMi355Context *ctx, const uint64_t *d_lwe_in, uint64_t *d_lwe_out,
+                               size_t count, void *stream);
+
+/* shortint KS -> PBS (PBSOrder::KeyswitchBootstrap): lwe_in/out count x (k*N+1).
+ * Replaces ServerKey::keyswitch_programmable_bootstrap_assign (shortint/server_key/mod.rs:783-857). */
+int tfhe_mi355_keyswitch_programmable_bootstrap(TfheMi355Context *ctx, const uint64_t *lwe_in,
+                                                uint64_t *lwe_out, const uint64_t *luts, size_t lut_count,
+                                                const uint32_t *lut_indexes, size_t count);
+int tfhe_mi355_keyswitch_programmable_bootstrap_async(TfheMi355Context *ctx, const uint64_t *d_lwe_in,
+                                                      uint64_t *d_lwe_out, const uint64_t *d_luts,
+                                                      size_t lut_count, const uint32_t *d_lut_indexes,
+                                                      size_t count, void *d_scratch, void *stream);
+/* Device scratch (bytes) needed by the async KS->PBS for `count` ciphertexts. */
+int tfhe_mi355_keyswitch_programmable_bootstrap_scratch(TfheMi355Context *ctx, size_t count,
+                                                        size_t *bytes);
+
+/* shortint PBS -> KS (PBSOrder::BootstrapKeyswitch): lwe_in/out count x (n+1).
+ * Replaces ServerKey::programmable_bootstrap_keyswitch_assign (shortint/server_key/mod.rs:859-932). */
+int tfhe_mi355_programmable_bootstrap_keyswitch(TfheMi355Context *ctx, const uint64_t *lwe_in,
+                                                uint64_t *lwe_out, const uint64_t *luts, size_t lut_count,
+                                                const uint32_t *lut_indexes, size_t count);
+
+/* Fill a shortint lookup table (GLWE accumulator, (k+1)*N words) from f(i), i < msg*carry.
+ * Replaces shortint fill_accumulator (shortint/engine/mod.rs:72-128). */
+int tfhe_mi355_fill_accumulator(const TfheMi355Parameters *params, const uint64_t *f_values,
+                                uint64_t *accumulator);
+
+/* ---- client-side helpers (not on the PBS path; seeded, deterministic per (seed, index)) ----
+ * Binary secret keys, Gaussian noise (commons/math/random/gaussian.rs:15-52), GGSW/BSK
+ * (ggsw_encryption.rs:116-150,300-331), KSK (lwe_keyswitch_key_generation.rs:60-135),
+ * LWE encryption/decryption (lwe_encryption.rs).  The randomness is a seeded xoshiro256**,
+ * not the reference's AES-CTR CSPRNG: use the Rust client for production keys. */
+int tfhe_mi355_client_gen_binary_key(uint64_t seed, uint64_t stream, uint64_t *key, size_t len);
+int tfhe_mi355_client_gen_bootstrap_key(uint64_t seed, const uint64_t *lwe_sk, uint32_t n,
+                                        const uint64_t *glwe_sk, uint32_t k, uint32_t N,
+                                        uint32_t base_log, uint32_t level, double std_dev,
+                                        uint64_t *bsk, uint32_t threads);
+int tfhe_mi355_client_gen_keyswitch_key(uint64_t seed, const uint64_t *in_sk, uint32_t in_dim,
+                                        const uint64_t *out_sk, uint32_t out_dim, uint32_t base_log,
+                                        uint32_t level, double std_dev, uint64_t *ksk);
+int tfhe_mi355_client_lwe_encrypt(uint64_t seed, const uint64_t *sk, uint32_t n, const uint64_t *plaintexts,
+                                  size_t count, double std_dev, uint64_t *cts);
+int tfhe_mi355_client_lwe_decrypt(const uint64_t *sk, uint32_t n, const uint64_t *cts, size_t count,
+                                  uint64_t *plaintexts);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TFHE_MI355_H */

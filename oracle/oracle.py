@@ -1,0 +1,230 @@
+"""ctypes wrapper over liboracle_pbs.so -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module,
+and only as the checker (or the timed CPU baseline).  The product path never imports it.
+
+Every function follows a reference function; the file:line citations are in pbs_oracle.c.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle_pbs.so")
+_lib = None
+
+u64p = ctypes.POINTER(ctypes.c_uint64)
+u32p = ctypes.POINTER(ctypes.c_uint32)
+f64p = ctypes.POINTER(ctypes.c_double)
+
+
+def build(force: bool = False) -> str:
+    """Compile the oracle with its own Makefile (gcc)."""
+    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < max(
+        os.path.getmtime(os.path.join(_HERE, f))
+        for f in os.listdir(_HERE)
+        if f.endswith(".c")
+    ):
+        subprocess.run(["make", "-C", _HERE, "-B"], check=True, capture_output=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.orc_closest_representable.restype = ctypes.c_uint64
+        L.orc_closest_representable.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
+        L.orc_decompose.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, u64p]
+        L.orc_f64_to_i64.restype = ctypes.c_int64
+        L.orc_f64_to_i64.argtypes = [ctypes.c_double]
+        L.orc_pbs_modulus_switch.restype = ctypes.c_uint64
+        L.orc_pbs_modulus_switch.argtypes = [ctypes.c_uint64, ctypes.c_int]
+        L.orc_fft_supported.argtypes = [ctypes.c_int]
+        L.orc_fft_product.argtypes = [ctypes.c_int, u64p, u64p, u64p]
+        L.orc_fft_roundtrip.argtypes = [ctypes.c_int, u64p, u64p]
+        L.orc_fft_complex.argtypes = [ctypes.c_int, f64p, f64p, ctypes.c_int]
+        L.orc_negacyclic_mul_u64.argtypes = [ctypes.c_int, u64p, u64p, u64p]
+        L.orc_gen_binary_key.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, u64p]
+        L.orc_gen_bsk.argtypes = [ctypes.c_uint64, u64p, ctypes.c_int, u64p, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                  u64p, ctypes.c_int]
+        L.orc_gen_ksk.argtypes = [ctypes.c_uint64, u64p, ctypes.c_int, u64p, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_int, ctypes.c_double, u64p]
+        L.orc_lwe_encrypt_batch.argtypes = [ctypes.c_uint64, u64p, ctypes.c_int, u64p,
+                                            ctypes.c_size_t, ctypes.c_double, u64p]
+        L.orc_lwe_decrypt_batch.argtypes = [u64p, ctypes.c_int, u64p, ctypes.c_size_t, u64p]
+        L.orc_fill_accumulator.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           u64p, u64p]
+        L.orc_fbsk_create.restype = ctypes.c_void_p
+        L.orc_fbsk_create.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_int, ctypes.c_int]
+        L.orc_fbsk_destroy.argtypes = [ctypes.c_void_p]
+        L.orc_fbsk_copy.argtypes = [ctypes.c_void_p, f64p]
+        L.orc_pbs_batch.argtypes = [ctypes.c_void_p, u64p, u64p, u64p, u32p, ctypes.c_size_t,
+                                    ctypes.c_int]
+        L.orc_keyswitch_batch.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, u64p, u64p, ctypes.c_size_t]
+        if hasattr(L, "orc_mb_pbs_batch"):
+            L.orc_mb_fbsk_create.restype = ctypes.c_void_p
+            L.orc_mb_fbsk_create.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_int, ctypes.c_int]
+            L.orc_mb_fbsk_destroy.argtypes = [ctypes.c_void_p]
+            L.orc_mb_pbs_batch.argtypes = [ctypes.c_void_p, u64p, u64p, u64p, u32p,
+                                           ctypes.c_size_t, ctypes.c_int]
+            L.orc_gen_mb_bsk.argtypes = [ctypes.c_uint64, u64p, ctypes.c_int, u64p, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_double, u64p, ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray, t=u64p):
+    return a.ctypes.data_as(t)
+
+
+def _u64(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.uint64)
+
+
+# ---- scalar helpers ----------------------------------------------------------------------
+def closest_representable(x: int, base_log: int, level: int) -> int:
+    return lib().orc_closest_representable(x, base_log, level)
+
+
+def decompose(x: int, base_log: int, level: int) -> list[int]:
+    out = np.zeros(level, dtype=np.uint64)
+    lib().orc_decompose(x, base_log, level, _p(out))
+    return [int(v) for v in out]
+
+
+def f64_to_i64(x: float) -> int:
+    return lib().orc_f64_to_i64(x)
+
+
+def pbs_modulus_switch(x: int, log2n: int) -> int:
+    return lib().orc_pbs_modulus_switch(x, log2n)
+
+
+# ---- FFT hooks ---------------------------------------------------------------------------
+def fft_product(a_torus: np.ndarray, b_int: np.ndarray) -> np.ndarray:
+    a, b = _u64(a_torus), _u64(b_int)
+    out = np.zeros_like(a)
+    assert lib().orc_fft_product(len(a), _p(a), _p(b), _p(out)) == 0
+    return out
+
+
+def fft_roundtrip(a: np.ndarray) -> np.ndarray:
+    a = _u64(a)
+    out = np.zeros_like(a)
+    assert lib().orc_fft_roundtrip(len(a), _p(a), _p(out)) == 0
+    return out
+
+
+def fft_complex(z: np.ndarray, inverse: bool = False) -> np.ndarray:
+    zin = np.ascontiguousarray(z, dtype=np.complex128)
+    out = np.zeros_like(zin)
+    assert lib().orc_fft_complex(len(zin), zin.ctypes.data_as(f64p), out.ctypes.data_as(f64p),
+                                 int(inverse)) == 0
+    return out
+
+
+def negacyclic_mul(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    a, b = _u64(a), _u64(b)
+    out = np.zeros_like(a)
+    lib().orc_negacyclic_mul_u64(len(a), _p(a), _p(b), _p(out))
+    return out
+
+
+# ---- keys / encryption -------------------------------------------------------------------
+def binary_key(seed: int, stream: int, length: int) -> np.ndarray:
+    k = np.zeros(length, dtype=np.uint64)
+    lib().orc_gen_binary_key(seed, stream, length, _p(k))
+    return k
+
+
+def gen_bsk(seed, lwe_sk, glwe_sk, k, N, base_log, level, std, threads=8) -> np.ndarray:
+    n = len(lwe_sk)
+    bsk = np.zeros(n * level * (k + 1) * (k + 1) * N, dtype=np.uint64)
+    lib().orc_gen_bsk(seed, _p(_u64(lwe_sk)), n, _p(_u64(glwe_sk)), k, N, base_log, level,
+                      std, _p(bsk), threads)
+    return bsk
+
+
+def gen_ksk(seed, in_sk, out_sk, base_log, level, std) -> np.ndarray:
+    ksk = np.zeros(len(in_sk) * level * (len(out_sk) + 1), dtype=np.uint64)
+    lib().orc_gen_ksk(seed, _p(_u64(in_sk)), len(in_sk), _p(_u64(out_sk)), len(out_sk),
+                      base_log, level, std, _p(ksk))
+    return ksk
+
+
+def lwe_encrypt(seed, sk, plaintexts, std) -> np.ndarray:
+    pts = _u64(plaintexts)
+    n = len(sk)
+    cts = np.zeros((len(pts), n + 1), dtype=np.uint64)
+    lib().orc_lwe_encrypt_batch(seed, _p(_u64(sk)), n, _p(pts), len(pts), std, _p(cts))
+    return cts
+
+
+def lwe_decrypt(sk, cts) -> np.ndarray:
+    cts = _u64(cts)
+    n = len(sk)
+    cts2 = cts.reshape(-1, n + 1)
+    pts = np.zeros(cts2.shape[0], dtype=np.uint64)
+    lib().orc_lwe_decrypt_batch(_p(_u64(sk)), n, _p(cts2), cts2.shape[0], _p(pts))
+    return pts
+
+
+def fill_accumulator(N, k, msg_mod, carry_mod, f) -> np.ndarray:
+    p = msg_mod * carry_mod
+    fv = _u64([f(i) for i in range(p)])
+    acc = np.zeros((k + 1) * N, dtype=np.uint64)
+    lib().orc_fill_accumulator(N, k, msg_mod, carry_mod, _p(fv), _p(acc))
+    return acc
+
+
+# ---- PBS / KS ----------------------------------------------------------------------------
+class FourierBsk:
+    """fbsk = Fourier BSK built with the oracle FFT (lwe_bootstrap_key_conversion.rs)."""
+
+    def __init__(self, bsk, n, k, N, base_log, level):
+        self.n, self.k, self.N, self.base_log, self.level = n, k, N, base_log, level
+        self._bsk = _u64(bsk)
+        self.h = lib().orc_fbsk_create(_p(self._bsk), n, k, N, base_log, level)
+        assert self.h
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_fbsk_destroy(self.h)
+            self.h = None
+
+    def fourier(self) -> np.ndarray:
+        out = np.zeros(self.n * self.level * (self.k + 1) ** 2 * self.N // 2, dtype=np.complex128)
+        lib().orc_fbsk_copy(self.h, out.ctypes.data_as(f64p))
+        return out
+
+    def pbs(self, lwe_in, luts, lut_idx=None, threads=8) -> np.ndarray:
+        lwe_in = _u64(lwe_in).reshape(-1, self.n + 1)
+        luts = _u64(luts)
+        cnt = lwe_in.shape[0]
+        out = np.zeros((cnt, self.k * self.N + 1), dtype=np.uint64)
+        idx = None
+        if lut_idx is not None:
+            idx = np.ascontiguousarray(lut_idx, dtype=np.uint32)
+        lib().orc_pbs_batch(self.h, _p(lwe_in), _p(out), _p(luts),
+                            idx.ctypes.data_as(u32p) if idx is not None else None, cnt, threads)
+        return out
+
+
+def keyswitch(ksk, in_dim, out_dim, base_log, level, lwe_in) -> np.ndarray:
+    lwe_in = _u64(lwe_in).reshape(-1, in_dim + 1)
+    out = np.zeros((lwe_in.shape[0], out_dim + 1), dtype=np.uint64)
+    lib().orc_keyswitch_batch(_p(_u64(ksk)), in_dim, out_dim, base_log, level, _p(lwe_in),
+                              _p(out), lwe_in.shape[0])
+    return out

@@ -1,0 +1,505 @@
+// capi.cpp -- C ABI implementation (include/tfhe_mi355.h).  Host-side runtime of the engine:
+// context = device + parameter set + key material + FFT tables, guarded by a mutex so that
+// concurrent callers (the reference's rayon workers, shortint/engine/mod.rs:23-25) can share one
+// key.  Error convention: 0/1 return + thread-local message (tfhe/src/c_api/utils.rs:3-73).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/tfhe_mi355.h"
+#include "engine.h"
+#include "errors.h"
+
+using namespace tfhe_mi355;
+
+namespace {
+
+struct Failure : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+[[noreturn]] void fail(const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    throw Failure(buf);
+}
+
+void check(hipError_t e, const char *what) {
+    if (e != hipSuccess) fail("%s: %s", what, hipGetErrorString(e));
+}
+
+template <class F>
+int guarded(F &&f) {
+    try {
+        f();
+        last_error_text().clear();
+        return TFHE_MI355_OK;
+    } catch (const std::exception &ex) {
+        last_error_text() = ex.what();
+        return TFHE_MI355_ERROR;
+    } catch (...) {
+        last_error_text() = "unknown failure";
+        return TFHE_MI355_ERROR;
+    }
+}
+
+struct DeviceBuffer {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+    void reserve(size_t b) {
+        if (b <= bytes) return;
+        if (ptr) check(hipFree(ptr), "hipFree");
+        ptr = nullptr;
+        bytes = 0;
+        check(hipMalloc(&ptr, b), "hipMalloc");
+        bytes = b;
+    }
+    void release() {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+};
+
+bool is_pow2(uint32_t x) { return x && !(x & (x - 1)); }
+}  // namespace
+
+struct TfheMi355Context {
+    TfheMi355Parameters p{};
+    int device = 0;
+    std::mutex mu;
+    hipStream_t stream = nullptr;
+    FftTables tables;
+    DeviceBuffer fbsk, ksk, std_staging;
+    DeviceBuffer io_in, io_out, io_luts, io_idx, io_tmp;
+    bool fbsk_ready = false, ksk_ready = false;
+
+    size_t n() const { return p.lwe_dimension; }
+    size_t k() const { return p.glwe_dimension; }
+    size_t N() const { return p.polynomial_size; }
+    size_t big_dim() const { return k() * N(); }
+    size_t glwe_len() const { return (k() + 1) * N(); }
+    size_t std_bsk_len() const {
+        return n() * p.pbs_level * (k() + 1) * (k() + 1) * N();
+    }
+    size_t fourier_bsk_bytes() const {
+        return n() * p.pbs_level * (k() + 1) * (k() + 1) * (N() / 2) * sizeof(double2);
+    }
+    size_t ksk_len() const { return big_dim() * p.ks_level * (n() + 1); }
+};
+
+namespace {
+
+void build_tables(TfheMi355Context *c) {
+    const int N = c->p.polynomial_size, M = N / 2;
+    // W[t] = exp(-2 pi i t / M); twist w_j = exp(i pi j / N) as fft/mod.rs:58-69
+    std::vector<double2> W(M), tw(M), twi(M);
+    for (int t = 0; t < M; t++) {
+        double ang = 2.0 * M_PI * (double)t / (double)M;
+        W[t] = make_double2(std::cos(ang), -std::sin(ang));
+    }
+    double unit = M_PI / (2.0 * (double)M);
+    double norm = 1.0 / (double)M;
+    for (int j = 0; j < M; j++) {
+        double a = (double)j * unit;
+        tw[j] = make_double2(std::cos(a), std::sin(a));
+        twi[j] = make_double2(norm * tw[j].x, norm * tw[j].y);
+    }
+    size_t bytes = sizeof(double2) * M;
+    check(hipMalloc(&c->tables.W, bytes), "hipMalloc(W)");
+    check(hipMalloc(&c->tables.twist, bytes), "hipMalloc(twist)");
+    check(hipMalloc(&c->tables.twist_inv, bytes), "hipMalloc(twist_inv)");
+    check(hipMemcpy(c->tables.W, W.data(), bytes, hipMemcpyHostToDevice), "upload W");
+    check(hipMemcpy(c->tables.twist, tw.data(), bytes, hipMemcpyHostToDevice), "upload twist");
+    check(hipMemcpy(c->tables.twist_inv, twi.data(), bytes, hipMemcpyHostToDevice), "upload twist_inv");
+    c->tables.N = N;
+}
+
+void require_fbsk(TfheMi355Context *c) {
+    if (!c->fbsk_ready) fail("bootstrapping key not uploaded");
+}
+void require_ksk(TfheMi355Context *c) {
+    if (!c->ksk_ready) fail("keyswitching key not uploaded");
+}
+
+void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, const uint64_t *d_luts,
+                    size_t lut_count, const uint32_t *d_idx, size_t count, hipStream_t s) {
+    require_fbsk(c);
+    if (lut_count == 0) fail("lut_count must be >= 1");
+    if (count > 0x7fffffff) fail("batch too large");
+    ClassicPbsLaunch a;
+    a.lwe_in = d_in;
+    a.lwe_out = d_out;
+    a.luts = d_luts;
+    a.lut_indexes = d_idx;
+    a.fbsk = reinterpret_cast<const double2 *>(c->fbsk.ptr);
+    a.W = c->tables.W;
+    a.twist = c->tables.twist;
+    a.twist_inv = c->tables.twist_inv;
+    a.n = (int)c->n();
+    a.base_log = (int)c->p.pbs_base_log;
+    a.count = (int)count;
+    check(launch_classic_pbs((int)c->N(), (int)c->k(), (int)c->p.pbs_level, a, s), "launch pbs");
+}
+
+void launch_ks_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, size_t count, hipStream_t s) {
+    require_ksk(c);
+    KeyswitchLaunch a;
+    a.lwe_in = d_in;
+    a.lwe_out = d_out;
+    a.ksk = reinterpret_cast<const uint64_t *>(c->ksk.ptr);
+    a.in_dim = (int)c->big_dim();
+    a.out_dim = (int)c->n();
+    a.base_log = (int)c->p.ks_base_log;
+    a.level = (int)c->p.ks_level;
+    a.count = (int)count;
+    check(launch_keyswitch(a, s), "launch keyswitch");
+}
+
+void validate_lut_indexes(const uint32_t *idx, size_t count, size_t lut_count) {
+    if (!idx) return;
+    for (size_t i = 0; i < count; i++)
+        if (idx[i] >= lut_count) fail("lut_indexes[%zu] = %u out of range (lut_count %zu)", i, idx[i], lut_count);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *tfhe_mi355_last_error(void) { return last_error_text().c_str(); }
+
+int tfhe_mi355_device_count(int *out_count) {
+    return guarded([&] {
+        if (!out_count) fail("null out_count");
+        *out_count = 0;
+        int n = 0;
+        check(hipGetDeviceCount(&n), "hipGetDeviceCount");
+        *out_count = n;
+    });
+}
+
+int tfhe_mi355_context_create(const TfheMi355Parameters *params, int device, TfheMi355Context **out_ctx) {
+    return guarded([&] {
+        if (!out_ctx) fail("null out_ctx");
+        *out_ctx = nullptr;
+        if (!params) fail("null params");
+        const TfheMi355Parameters &p = *params;
+        if (!is_pow2(p.polynomial_size)) fail("polynomial_size must be a power of two");
+        if (p.grouping_factor != 0) fail("multi-bit PBS (grouping_factor %u) is not available in this build", p.grouping_factor);
+        if (!classic_pbs_supported((int)p.polynomial_size, (int)p.glwe_dimension, (int)p.pbs_level))
+            fail("no kernel for N=%u k=%u pbs_level=%u", p.polynomial_size, p.glwe_dimension, p.pbs_level);
+        if (p.pbs_base_log == 0 || p.pbs_base_log * p.pbs_level >= 64) fail("invalid pbs decomposition");
+        if (p.ks_level && (p.ks_base_log == 0 || p.ks_base_log * p.ks_level >= 64)) fail("invalid ks decomposition");
+        if (p.lwe_dimension == 0) fail("lwe_dimension must be > 0");
+        check(hipSetDevice(device), "hipSetDevice");
+        auto *c = new TfheMi355Context();
+        c->p = p;
+        c->device = device;
+        try {
+            check(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+            build_tables(c);
+        } catch (...) {
+            tfhe_mi355_context_destroy(c);
+            throw;
+        }
+        *out_ctx = c;
+    });
+}
+
+int tfhe_mi355_context_destroy(TfheMi355Context *ctx) {
+    return guarded([&] {
+        if (!ctx) return;
+        (void)hipSetDevice(ctx->device);
+        if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+        for (DeviceBuffer *b : {&ctx->fbsk, &ctx->ksk, &ctx->std_staging, &ctx->io_in, &ctx->io_out,
+                                &ctx->io_luts, &ctx->io_idx, &ctx->io_tmp})
+            b->release();
+        if (ctx->tables.W) (void)hipFree(ctx->tables.W);
+        if (ctx->tables.twist) (void)hipFree(ctx->tables.twist);
+        if (ctx->tables.twist_inv) (void)hipFree(ctx->tables.twist_inv);
+        if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+        delete ctx;
+    });
+}
+
+int tfhe_mi355_bootstrap_key_upload(TfheMi355Context *ctx, const uint64_t *bsk, size_t len) {
+    return guarded([&] {
+        if (!ctx || !bsk) fail("null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        if (len != ctx->std_bsk_len()) fail("bootstrapping key has %zu words, expected %zu", len, ctx->std_bsk_len());
+        ctx->std_staging.reserve(len * sizeof(uint64_t));
+        check(hipMemcpyAsync(ctx->std_staging.ptr, bsk, len * sizeof(uint64_t), hipMemcpyHostToDevice,
+                             ctx->stream), "upload bsk");
+        ctx->fbsk.reserve(ctx->fourier_bsk_bytes());
+        check(launch_bsk_to_fourier((int)ctx->N(), (const uint64_t *)ctx->std_staging.ptr,
+                                    (double2 *)ctx->fbsk.ptr, len / ctx->N(), ctx->tables, ctx->stream),
+              "bsk conversion");
+        check(hipStreamSynchronize(ctx->stream), "bsk conversion sync");
+        ctx->std_staging.release();
+        ctx->fbsk_ready = true;
+    });
+}
+
+int tfhe_mi355_bootstrap_key_convert_async(TfheMi355Context *ctx, const uint64_t *d_bsk, size_t len,
+                                           void *stream) {
+    return guarded([&] {
+        if (!ctx || !d_bsk) fail("null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        if (len != ctx->std_bsk_len()) fail("bootstrapping key has %zu words, expected %zu", len, ctx->std_bsk_len());
+        ctx->fbsk.reserve(ctx->fourier_bsk_bytes());
+        check(launch_bsk_to_fourier((int)ctx->N(), d_bsk, (double2 *)ctx->fbsk.ptr, len / ctx->N(), ctx->tables,
+                                    (hipStream_t)stream),
+              "bsk conversion");
+        ctx->fbsk_ready = true;
+    });
+}
+
+int tfhe_mi355_bootstrap_key_fourier(TfheMi355Context *ctx, void **d_ptr, size_t *bytes) {
+    return guarded([&] {
+        if (!ctx || !d_ptr || !bytes) fail("null argument");
+        *d_ptr = nullptr;
+        *bytes = 0;
+        std::lock_guard<std::mutex> g(ctx->mu);
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        ctx->fbsk.reserve(ctx->fourier_bsk_bytes());
+        *d_ptr = ctx->fbsk.ptr;
+        *bytes = ctx->fourier_bsk_bytes();
+    });
+}
+
+int tfhe_mi355_bootstrap_key_fourier_set_ready(TfheMi355Context *ctx) {
+    return guarded([&] {
+        if (!ctx) fail("null ctx");
+        if (!ctx->fbsk.ptr) fail("no Fourier key buffer");
+        ctx->fbsk_ready = true;
+    });
+}
+
+int tfhe_mi355_keyswitch_key_upload(TfheMi355Context *ctx, const uint64_t *ksk, size_t len) {
+    return guarded([&] {
+        if (!ctx || !ksk) fail("null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        if (len != ctx->ksk_len()) fail("keyswitching key has %zu words, expected %zu", len, ctx->ksk_len());
+        ctx->ksk.reserve(len * sizeof(uint64_t));
+        check(hipMemcpy(ctx->ksk.ptr, ksk, len * sizeof(uint64_t), hipMemcpyHostToDevice), "upload ksk");
+        ctx->ksk_ready = true;
+    });
+}
+
+int tfhe_mi355_keyswitch_key_upload_async(TfheMi355Context *ctx, const uint64_t *d_ksk, size_t len,
+                                          void *stream) {
+    return guarded([&] {
+        if (!ctx || !d_ksk) fail("null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        if (len != ctx->ksk_len()) fail("keyswitching key has %zu words, expected %zu", len, ctx->ksk_len());
+        ctx->ksk.reserve(len * sizeof(uint64_t));
+        check(hipMemcpyAsync(ctx->ksk.ptr, d_ksk, len * sizeof(uint64_t), hipMemcpyDeviceToDevice,
+                             (hipStream_t)stream), "copy ksk");
+        ctx->ksk_ready = true;
+    });
+}
+
+int tfhe_mi355_keyswitch_key_device(TfheMi355Context *ctx, void **d_ptr, size_t *bytes) {
+    return guarded([&] {
+        if (!ctx || !d_ptr || !bytes) fail("null argument");
+        *d_ptr = nullptr;
+        *bytes = 0;
+        std::lock_guard<std::mutex> g(ctx->mu);
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        ctx->ksk.reserve(ctx->ksk_len() * sizeof(uint64_t));
+        *d_ptr = ctx->ksk.ptr;
+        *bytes = ctx->ksk_len() * sizeof(uint64_t);
+    });
+}
+
+int tfhe_mi355_keyswitch_key_set_ready(TfheMi355Context *ctx) {
+    return guarded([&] {
+        if (!ctx) fail("null ctx");
+        if (!ctx->ksk.ptr) fail("no keyswitching key buffer");
+        ctx->ksk_ready = true;
+    });
+}
+
+int tfhe_mi355_programmable_bootstrap(TfheMi355Context *ctx, const uint64_t *lwe_in, uint64_t *lwe_out,
+                                      const uint64_t *luts, size_t lut_count, const uint32_t *lut_indexes,
+                                      size_t count) {
+    return guarded([&] {
+        if (!ctx || (!lwe_in && count) || (!lwe_out && count) || !luts) fail("null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        require_fbsk(ctx);
+        if (count == 0) return;
+        validate_lut_indexes(lut_indexes, count, lut_count);
+        const size_t in_b = count * (ctx->n() + 1) * 8, out_b = count * (ctx->big_dim() + 1) * 8;
+        const size_t lut_b = lut_count * ctx->glwe_len() * 8;
+        ctx->io_in.reserve(in_b);
+        ctx->io_out.reserve(out_b);
+        ctx->io_luts.reserve(lut_b);
+        if (lut_indexes) ctx->io_idx.reserve(count * 4);
+        hipStream_t s = ctx->stream;
+        check(hipMemcpyAsync(ctx->io_in.ptr, lwe_in, in_b, hipMemcpyHostToDevice, s), "H2D in");
+        check(hipMemcpyAsync(ctx->io_luts.ptr, luts, lut_b, hipMemcpyHostToDevice, s), "H2D luts");
+        if (lut_indexes)
+            check(hipMemcpyAsync(ctx->io_idx.ptr, lut_indexes, count * 4, hipMemcpyHostToDevice, s), "H2D idx");
+        launch_pbs_dev(ctx, (const uint64_t *)ctx->io_in.ptr, (uint64_t *)ctx->io_out.ptr,
+                       (const uint64_t *)ctx->io_luts.ptr, lut_count,
+                       lut_indexes ? (const uint32_t *)ctx->io_idx.ptr : nullptr, count, s);
+        check(hipMemcpyAsync(lwe_out, ctx->io_out.ptr, out_b, hipMemcpyDeviceToHost, s), "D2H out");
+        check(hipStreamSynchronize(s), "pbs sync");
+    });
+}
+
+int tfhe_mi355_programmable_bootstrap_async(TfheMi355Context *ctx, const uint64_t *d_in, uint64_t *d_out,
+                                            const uint64_t *d_luts, size_t lut_count,
+                                            const uint32_t *d_idx, size_t count, void *stream) {
+    return guarded([&] {
+        if (!ctx || (!d_in && count) || (!d_out && count) || !d_luts) fail("null argument");
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        launch_pbs_dev(ctx, d_in, d_out, d_luts, lut_count, d_idx, count, (hipStream_t)stream);
+    });
+}
+
+int tfhe_mi355_keyswitch(TfheMi355Context *ctx, const uint64_t *lwe_in, uint64_t *lwe_out, size_t count) {
+    return guarded([&] {
+        if (!ctx || (!lwe_in && count) || (!lwe_out && count)) fail("null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        require_ksk(ctx);
+        if (count == 0) return;
+        const size_t in_b = count * (ctx->big_dim() + 1) * 8, out_b = count * (ctx->n() + 1) * 8;
+        ctx->io_in.reserve(in_b);
+        ctx->io_out.reserve(out_b);
+        hipStream_t s = ctx->stream;
+        check(hipMemcpyAsync(ctx->io_in.ptr, lwe_in, in_b, hipMemcpyHostToDevice, s), "H2D in");
+        launch_ks_dev(ctx, (const uint64_t *)ctx->io_in.ptr, (uint64_t *)ctx->io_out.ptr, count, s);
+        check(hipMemcpyAsync(lwe_out, ctx->io_out.ptr, out_b, hipMemcpyDeviceToHost, s), "D2H out");
+        check(hipStreamSynchronize(s), "ks sync");
+    });
+}
+
+int tfhe_mi355_keyswitch_async(TfheMi355Context *ctx, const uint64_t *d_in, uint64_t *d_out, size_t count,
+                               void *stream) {
+    return guarded([&] {
+        if (!ctx || (!d_in && count) || (!d_out && count)) fail("null argument");
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        launch_ks_dev(ctx, d_in, d_out, count, (hipStream_t)stream);
+    });
+}
+
+int tfhe_mi355_keyswitch_programmable_bootstrap_scratch(TfheMi355Context *ctx, size_t count, size_t *bytes) {
+    return guarded([&] {
+        if (!ctx || !bytes) fail("null argument");
+        *bytes = count * (ctx->n() + 1) * 8;
+    });
+}
+
+int tfhe_mi355_keyswitch_programmable_bootstrap_async(TfheMi355Context *ctx, const uint64_t *d_in,
+                                                      uint64_t *d_out, const uint64_t *d_luts, size_t lut_count,
+                                                      const uint32_t *d_idx, size_t count, void *d_scratch,
+                                                      void *stream) {
+    return guarded([&] {
+        if (!ctx || (!d_in && count) || (!d_out && count) || !d_luts || (!d_scratch && count))
+            fail("null argument");
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        launch_ks_dev(ctx, d_in, (uint64_t *)d_scratch, count, (hipStream_t)stream);
+        launch_pbs_dev(ctx, (const uint64_t *)d_scratch, d_out, d_luts, lut_count, d_idx, count,
+                       (hipStream_t)stream);
+    });
+}
+
+int tfhe_mi355_keyswitch_programmable_bootstrap(TfheMi355Context *ctx, const uint64_t *lwe_in,
+                                                uint64_t *lwe_out, const uint64_t *luts, size_t lut_count,
+                                                const uint32_t *lut_indexes, size_t count) {
+    return guarded([&] {
+        if (!ctx || (!lwe_in && count) || (!lwe_out && count) || !luts) fail("null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        require_fbsk(ctx);
+        require_ksk(ctx);
+        if (count == 0) return;
+        validate_lut_indexes(lut_indexes, count, lut_count);
+        const size_t big_b = count * (ctx->big_dim() + 1) * 8, small_b = count * (ctx->n() + 1) * 8;
+        const size_t lut_b = lut_count * ctx->glwe_len() * 8;
+        ctx->io_in.reserve(big_b);
+        ctx->io_out.reserve(big_b);
+        ctx->io_tmp.reserve(small_b);
+        ctx->io_luts.reserve(lut_b);
+        if (lut_indexes) ctx->io_idx.reserve(count * 4);
+        hipStream_t s = ctx->stream;
+        check(hipMemcpyAsync(ctx->io_in.ptr, lwe_in, big_b, hipMemcpyHostToDevice, s), "H2D in");
+        check(hipMemcpyAsync(ctx->io_luts.ptr, luts, lut_b, hipMemcpyHostToDevice, s), "H2D luts");
+        if (lut_indexes)
+            check(hipMemcpyAsync(ctx->io_idx.ptr, lut_indexes, count * 4, hipMemcpyHostToDevice, s), "H2D idx");
+        launch_ks_dev(ctx, (const uint64_t *)ctx->io_in.ptr, (uint64_t *)ctx->io_tmp.ptr, count, s);
+        launch_pbs_dev(ctx, (const uint64_t *)ctx->io_tmp.ptr, (uint64_t *)ctx->io_out.ptr,
+                       (const uint64_t *)ctx->io_luts.ptr, lut_count,
+                       lut_indexes ? (const uint32_t *)ctx->io_idx.ptr : nullptr, count, s);
+        check(hipMemcpyAsync(lwe_out, ctx->io_out.ptr, big_b, hipMemcpyDeviceToHost, s), "D2H out");
+        check(hipStreamSynchronize(s), "ks-pbs sync");
+    });
+}
+
+int tfhe_mi355_programmable_bootstrap_keyswitch(TfheMi355Context *ctx, const uint64_t *lwe_in,
+                                                uint64_t *lwe_out, const uint64_t *luts, size_t lut_count,
+                                                const uint32_t *lut_indexes, size_t count) {
+    return guarded([&] {
+        if (!ctx || (!lwe_in && count) || (!lwe_out && count) || !luts) fail("null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        require_fbsk(ctx);
+        require_ksk(ctx);
+        if (count == 0) return;
+        validate_lut_indexes(lut_indexes, count, lut_count);
+        const size_t big_b = count * (ctx->big_dim() + 1) * 8, small_b = count * (ctx->n() + 1) * 8;
+        const size_t lut_b = lut_count * ctx->glwe_len() * 8;
+        ctx->io_in.reserve(small_b);
+        ctx->io_out.reserve(small_b);
+        ctx->io_tmp.reserve(big_b);
+        ctx->io_luts.reserve(lut_b);
+        if (lut_indexes) ctx->io_idx.reserve(count * 4);
+        hipStream_t s = ctx->stream;
+        check(hipMemcpyAsync(ctx->io_in.ptr, lwe_in, small_b, hipMemcpyHostToDevice, s), "H2D in");
+        check(hipMemcpyAsync(ctx->io_luts.ptr, luts, lut_b, hipMemcpyHostToDevice, s), "H2D luts");
+        if (lut_indexes)
+            check(hipMemcpyAsync(ctx->io_idx.ptr, lut_indexes, count * 4, hipMemcpyHostToDevice, s), "H2D idx");
+        launch_pbs_dev(ctx, (const uint64_t *)ctx->io_in.ptr, (uint64_t *)ctx->io_tmp.ptr,
+                       (const uint64_t *)ctx->io_luts.ptr, lut_count,
+                       lut_indexes ? (const uint32_t *)ctx->io_idx.ptr : nullptr, count, s);
+        launch_ks_dev(ctx, (const uint64_t *)ctx->io_tmp.ptr, (uint64_t *)ctx->io_out.ptr, count, s);
+        check(hipMemcpyAsync(lwe_out, ctx->io_out.ptr, small_b, hipMemcpyDeviceToHost, s), "D2H out");
+        check(hipStreamSynchronize(s), "pbs-ks sync");
+    });
+}
+
+int tfhe_mi355_fill_accumulator(const TfheMi355Parameters *params, const uint64_t *f_values, uint64_t *acc) {
+    return guarded([&] {
+        if (!params || !f_values || !acc) fail("null argument");
+        const size_t N = params->polynomial_size, k = params->glwe_dimension;
+        const size_t p = (size_t)params->message_modulus * params->carry_modulus;
+        if (p == 0 || N % p) fail("polynomial_size must be a multiple of message_modulus*carry_modulus");
+        const size_t box = N / p, half = box / 2;
+        const uint64_t delta = (1ULL << 63) / p;
+        std::vector<uint64_t> body(N);
+        for (size_t i = 0; i < p; i++)
+            for (size_t j = 0; j < box; j++) body[i * box + j] = f_values[i] * delta;
+        for (size_t j = 0; j < half; j++) body[j] = 0 - body[j];
+        std::memset(acc, 0, sizeof(uint64_t) * k * N);
+        for (size_t j = 0; j < N; j++) acc[k * N + j] = body[(j + half) % N];
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,187 @@
+// client.cpp -- client-side helpers of the engine (key generation, LWE encryption/decryption).
+// Not on the PBS hot path; they let a standalone user (and bench.py) build valid server keys
+// without the Rust client.  They follow the reference's rules:
+//   binary secret keys                  (LweSecretKey::generate_new_binary)
+//   Gaussian noise, Marsaglia polar      (commons/math/random/gaussian.rs:15-52) + from_torus
+//                                         (commons/math/torus/mod.rs:71-78)
+//   GGSW rows of the BSK                 (algorithms/ggsw_encryption.rs:116-150, 300-331)
+//   KSK levels stored L..1               (algorithms/lwe_keyswitch_key_generation.rs:60-135)
+// The randomness source is a seeded xoshiro256** (the reference's AES-CTR CSPRNG is not part of
+// the GPU path); keys are deterministic per (seed, index) whatever the thread count.
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+#include <atomic>
+
+#include "../../include/tfhe_mi355.h"
+#include "errors.h"
+
+namespace {
+
+struct Rng {
+    uint64_t s[4];
+    static uint64_t splitmix(uint64_t &x) {
+        uint64_t z = (x += 0x9E3779B97F4A7C15ULL);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        return z ^ (z >> 31);
+    }
+    Rng(uint64_t seed, uint64_t stream) {
+        uint64_t x = seed ^ (stream * 0xD1B54A32D192ED03ULL) ^ 0xA5A5A5A5F00DF00DULL;
+        for (auto &v : s) v = splitmix(x);
+    }
+    static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+    uint64_t next() {
+        uint64_t r = rotl(s[1] * 5, 7) * 9, t = s[1] << 17;
+        s[2] ^= s[0];
+        s[3] ^= s[1];
+        s[1] ^= s[2];
+        s[0] ^= s[3];
+        s[2] ^= t;
+        s[3] = rotl(s[3], 45);
+        return r;
+    }
+    uint64_t gaussian_torus(double std) {
+        for (;;) {
+            double u = (double)(int64_t)next() * 0x1p-63;
+            double v = (double)(int64_t)next() * 0x1p-63;
+            double s2 = u * u + v * v;
+            if (s2 > 0.0 && s2 < 1.0) {
+                double x = u * std * std::sqrt(-2.0 * std::log(s2) / s2);
+                double fract = x - std::round(x);
+                fract = std::round(fract * 18446744073709551616.0);
+                if (fract >= 9223372036854775808.0) return 0x8000000000000000ULL;
+                return (uint64_t)(int64_t)fract;
+            }
+        }
+    }
+};
+
+template <class F>
+int guard(F &&f) {
+    try {
+        f();
+        tfhe_mi355::last_error_text().clear();
+        return TFHE_MI355_OK;
+    } catch (const std::exception &e) {
+        tfhe_mi355::last_error_text() = e.what();
+        return TFHE_MI355_ERROR;
+    }
+}
+
+void negacyclic_binary_add(uint64_t *body, const uint64_t *a, const uint64_t *s, int N) {
+    for (int i = 0; i < N; i++) {
+        if (!s[i]) continue;
+        for (int j = 0; j < i; j++) body[j] -= a[j - i + N];
+        for (int j = i; j < N; j++) body[j] += a[j - i];
+    }
+}
+
+void glwe_encrypt_assign(Rng &r, uint64_t *glwe, const uint64_t *key, int k, int N, double std) {
+    uint64_t *body = glwe + (size_t)k * N;
+    for (size_t i = 0; i < (size_t)k * N; i++) glwe[i] = r.next();
+    for (int j = 0; j < N; j++) body[j] += r.gaussian_torus(std);
+    for (int p = 0; p < k; p++) negacyclic_binary_add(body, glwe + (size_t)p * N, key + (size_t)p * N, N);
+}
+
+void lwe_encrypt(Rng &r, const uint64_t *sk, int n, uint64_t pt, double std, uint64_t *ct) {
+    uint64_t b = pt + r.gaussian_torus(std);
+    for (int i = 0; i < n; i++) {
+        ct[i] = r.next();
+        b += ct[i] * sk[i];
+    }
+    ct[n] = b;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tfhe_mi355_client_gen_binary_key(uint64_t seed, uint64_t stream, uint64_t *key, size_t len) {
+    return guard([&] {
+        if (!key) throw std::invalid_argument("null key");
+        Rng r(seed, stream);
+        for (size_t i = 0; i < len; i++) key[i] = r.next() >> 63;
+    });
+}
+
+int tfhe_mi355_client_gen_bootstrap_key(uint64_t seed, const uint64_t *lwe_sk, uint32_t n,
+                                        const uint64_t *glwe_sk, uint32_t k, uint32_t N, uint32_t base_log,
+                                        uint32_t level, double std, uint64_t *bsk, uint32_t threads) {
+    return guard([&] {
+        if (!lwe_sk || !glwe_sk || !bsk) throw std::invalid_argument("null argument");
+        const size_t glwe_len = (size_t)(k + 1) * N, ggsw_len = (size_t)level * (k + 1) * glwe_len;
+        std::atomic<uint32_t> next{0};
+        auto work = [&] {
+            for (;;) {
+                uint32_t i = next++;
+                if (i >= n) break;
+                Rng r(seed, 0x1000000ULL + i);
+                uint64_t m = lwe_sk[i];
+                uint64_t *ggsw = bsk + (size_t)i * ggsw_len;
+                for (uint32_t lvl = 1; lvl <= level; lvl++) {
+                    uint64_t factor = (0 - m) * (1ULL << (64 - base_log * lvl));
+                    for (uint32_t row = 0; row <= k; row++) {
+                        uint64_t *g = ggsw + ((size_t)(lvl - 1) * (k + 1) + row) * glwe_len;
+                        uint64_t *body = g + (size_t)k * N;
+                        if (row < k) {
+                            for (uint32_t j = 0; j < N; j++) body[j] = glwe_sk[(size_t)row * N + j] * factor;
+                        } else {
+                            std::memset(body, 0, sizeof(uint64_t) * N);
+                            body[0] = 0 - factor;
+                        }
+                        glwe_encrypt_assign(r, g, glwe_sk, (int)k, (int)N, std);
+                    }
+                }
+            }
+        };
+        uint32_t nt = threads ? threads : std::max(1u, std::thread::hardware_concurrency());
+        std::vector<std::thread> th;
+        for (uint32_t t = 1; t < nt; t++) th.emplace_back(work);
+        work();
+        for (auto &t : th) t.join();
+    });
+}
+
+int tfhe_mi355_client_gen_keyswitch_key(uint64_t seed, const uint64_t *in_sk, uint32_t in_dim,
+                                        const uint64_t *out_sk, uint32_t out_dim, uint32_t base_log,
+                                        uint32_t level, double std, uint64_t *ksk) {
+    return guard([&] {
+        if (!in_sk || !out_sk || !ksk) throw std::invalid_argument("null argument");
+        Rng r(seed, 0x2000000ULL);
+        for (uint32_t i = 0; i < in_dim; i++)
+            for (uint32_t l = 0; l < level; l++) {
+                uint32_t lvl = level - l;
+                uint64_t msg = in_sk[i] << (64 - base_log * lvl);
+                lwe_encrypt(r, out_sk, (int)out_dim, msg, std, ksk + ((size_t)i * level + l) * (out_dim + 1));
+            }
+    });
+}
+
+int tfhe_mi355_client_lwe_encrypt(uint64_t seed, const uint64_t *sk, uint32_t n, const uint64_t *pts,
+                                  size_t count, double std, uint64_t *cts) {
+    return guard([&] {
+        if (!sk || (!pts && count) || (!cts && count)) throw std::invalid_argument("null argument");
+        Rng r(seed, 0x3000000ULL);
+        for (size_t c = 0; c < count; c++) lwe_encrypt(r, sk, (int)n, pts[c], std, cts + c * (n + 1));
+    });
+}
+
+int tfhe_mi355_client_lwe_decrypt(const uint64_t *sk, uint32_t n, const uint64_t *cts, size_t count,
+                                  uint64_t *pts) {
+    return guard([&] {
+        if (!sk || (!pts && count) || (!cts && count)) throw std::invalid_argument("null argument");
+        for (size_t c = 0; c < count; c++) {
+            const uint64_t *ct = cts + c * (n + 1);
+            uint64_t b = ct[n];
+            for (uint32_t i = 0; i < n; i++) b -= ct[i] * sk[i];
+            pts[c] = b;
+        }
+    });
+}
+
+}  // extern "C"

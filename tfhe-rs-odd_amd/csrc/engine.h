@@ -1,0 +1,46 @@
+// engine.h -- internal launchers of the MI355X PBS engine (host side, no torch types).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace tfhe_mi355 {
+
+struct FftTables {
+    // device tables, M entries each (M = N/2)
+    double2 *W = nullptr;          // exp(-2 pi i t / M)
+    double2 *twist = nullptr;      // exp(i pi j / N)            (fft/mod.rs:58-69)
+    double2 *twist_inv = nullptr;  // twist / M (backward, x86.rs:823-874)
+    int N = 0;
+};
+
+struct ClassicPbsLaunch {
+    const uint64_t *lwe_in;      // [count][n+1]
+    uint64_t *lwe_out;           // [count][k*N+1]
+    const uint64_t *luts;        // [lut_count][(k+1)*N]
+    const uint32_t *lut_indexes; // [count] or null
+    const double2 *fbsk;         // engine Fourier layout
+    const double2 *W, *twist, *twist_inv;
+    int n;
+    int base_log;
+    int count;
+};
+
+// Returns false if (N, k, L) has no compiled specialisation.
+bool classic_pbs_supported(int N, int k, int L);
+hipError_t launch_classic_pbs(int N, int k, int L, const ClassicPbsLaunch &a, hipStream_t s);
+
+// standard BSK polys (npoly x N u64) -> Fourier (npoly x M double2, engine layout)
+hipError_t launch_bsk_to_fourier(int N, const uint64_t *std_polys, double2 *fourier, size_t npoly,
+                                 const FftTables &t, hipStream_t s);
+
+struct KeyswitchLaunch {
+    const uint64_t *lwe_in;  // [count][in_dim+1]
+    uint64_t *lwe_out;       // [count][out_dim+1]
+    const uint64_t *ksk;     // [in_dim][level][out_dim+1]
+    int in_dim, out_dim, base_log, level;
+    int count;
+};
+hipError_t launch_keyswitch(const KeyswitchLaunch &a, hipStream_t s);
+
+}  // namespace tfhe_mi355

@@ -1,0 +1,70 @@
+"""Client-side helpers (key generation, LWE encryption/decryption) through the C ABI.
+
+They follow the reference's rules (binary keys, Marsaglia-polar Gaussian noise, GGSW rows of
+ggsw_encryption.rs:116-150, KSK levels L..1 of lwe_keyswitch_key_generation.rs:109) with a seeded
+xoshiro256** stream instead of the reference's AES-CTR CSPRNG.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+from . import _lib
+from ._lib import u64p
+
+
+def _ptr(a):
+    return a.ctypes.data_as(u64p)
+
+
+def gen_binary_key(seed: int, stream: int, length: int) -> np.ndarray:
+    k = np.zeros(length, dtype=np.uint64)
+    _lib.call("tfhe_mi355_client_gen_binary_key", seed, stream, _ptr(k), length)
+    return k
+
+
+def gen_bootstrap_key(seed, lwe_sk, glwe_sk, glwe_dimension, polynomial_size, base_log, level, std_dev,
+                      threads: int = 0) -> np.ndarray:
+    lwe_sk = np.ascontiguousarray(lwe_sk, dtype=np.uint64)
+    glwe_sk = np.ascontiguousarray(glwe_sk, dtype=np.uint64)
+    k, N = glwe_dimension, polynomial_size
+    bsk = np.empty(len(lwe_sk) * level * (k + 1) * (k + 1) * N, dtype=np.uint64)
+    if threads <= 0:
+        threads = min(16, os.cpu_count() or 1)
+    _lib.call("tfhe_mi355_client_gen_bootstrap_key", seed, _ptr(lwe_sk), len(lwe_sk), _ptr(glwe_sk), k, N,
+              base_log, level, std_dev, _ptr(bsk), threads)
+    return bsk
+
+
+def gen_keyswitch_key(seed, in_sk, out_sk, base_log, level, std_dev) -> np.ndarray:
+    in_sk = np.ascontiguousarray(in_sk, dtype=np.uint64)
+    out_sk = np.ascontiguousarray(out_sk, dtype=np.uint64)
+    ksk = np.empty(len(in_sk) * level * (len(out_sk) + 1), dtype=np.uint64)
+    _lib.call("tfhe_mi355_client_gen_keyswitch_key", seed, _ptr(in_sk), len(in_sk), _ptr(out_sk), len(out_sk),
+              base_log, level, std_dev, _ptr(ksk))
+    return ksk
+
+
+def lwe_encrypt(seed, sk, plaintexts, std_dev) -> np.ndarray:
+    sk = np.ascontiguousarray(sk, dtype=np.uint64)
+    pts = np.ascontiguousarray(plaintexts, dtype=np.uint64).ravel()
+    cts = np.empty((len(pts), len(sk) + 1), dtype=np.uint64)
+    _lib.call("tfhe_mi355_client_lwe_encrypt", seed, _ptr(sk), len(sk), _ptr(pts), len(pts), std_dev, _ptr(cts))
+    return cts
+
+
+def lwe_decrypt(sk, cts) -> np.ndarray:
+    sk = np.ascontiguousarray(sk, dtype=np.uint64)
+    cts = np.ascontiguousarray(cts, dtype=np.uint64).reshape(-1, len(sk) + 1)
+    pts = np.empty(cts.shape[0], dtype=np.uint64)
+    _lib.call("tfhe_mi355_client_lwe_decrypt", _ptr(sk), len(sk), _ptr(cts), cts.shape[0], _ptr(pts))
+    return pts
+
+
+def decode(plaintexts, delta: int) -> np.ndarray:
+    """shortint decrypt_message_and_carry rounding (shortint/client_key/mod.rs:281-302)."""
+    d = np.asarray(plaintexts, dtype=np.uint64)
+    rb = np.uint64(delta >> 1)
+    rounding = (d & rb) << np.uint64(1)
+    return (d + rounding) // np.uint64(delta)

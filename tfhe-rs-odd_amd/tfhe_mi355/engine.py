@@ -1,0 +1,206 @@
+"""Engine = one C-ABI context on one GPU (include/tfhe_mi355.h), numpy in/out or torch device
+tensors in/out.  This is the object a reference `ShortintBootstrappingKey::Gpu{handle}` arm would
+hold (SURVEY.md 8b seam 1).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import TfheMi355Parameters, u32p, u64p, vp
+from .parameters import ClassicPBSParameters
+
+
+def _u64(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.uint64)
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(u64p)
+
+
+def _dev_ptr(t) -> int:
+    """Device pointer of a torch tensor (or a raw int)."""
+    if t is None:
+        return None
+    if isinstance(t, int):
+        return t
+    if not t.is_contiguous():
+        raise ValueError("device tensors must be contiguous")
+    return t.data_ptr()
+
+
+def _stream_ptr(stream) -> int:
+    if stream is None:
+        import torch
+
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+def c_params(p: ClassicPBSParameters) -> TfheMi355Parameters:
+    return TfheMi355Parameters(p.lwe_dimension, p.glwe_dimension, p.polynomial_size, p.pbs_base_log,
+                               p.pbs_level, p.ks_base_log, p.ks_level, p.message_modulus,
+                               p.carry_modulus, p.grouping_factor)
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    _lib.call("tfhe_mi355_device_count", ctypes.byref(n))
+    return n.value
+
+
+class Engine:
+    """MI355X PBS engine context bound to `device`."""
+
+    def __init__(self, params: ClassicPBSParameters, device: int = 0):
+        self.params = params
+        self.device = device
+        self._cp = c_params(params)
+        h = vp()
+        _lib.call("tfhe_mi355_context_create", ctypes.byref(self._cp), device, ctypes.byref(h))
+        self._h = h
+
+    # -- lifetime ---------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            _lib.call("tfhe_mi355_context_destroy", self._h)
+            self._h = vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- sizes --------------------------------------------------------------------------
+    @property
+    def n(self):
+        return self.params.lwe_dimension
+
+    @property
+    def big_dim(self):
+        return self.params.glwe_dimension * self.params.polynomial_size
+
+    @property
+    def glwe_len(self):
+        return (self.params.glwe_dimension + 1) * self.params.polynomial_size
+
+    # -- keys ---------------------------------------------------------------------------
+    def upload_bootstrap_key(self, standard_bsk: np.ndarray) -> None:
+        b = _u64(standard_bsk).ravel()
+        _lib.call("tfhe_mi355_bootstrap_key_upload", self._h, _ptr(b), b.size)
+
+    def convert_bootstrap_key_device(self, d_standard_bsk, numel: int, stream=None) -> None:
+        _lib.call("tfhe_mi355_bootstrap_key_convert_async", self._h, _dev_ptr(d_standard_bsk), numel,
+                  _stream_ptr(stream))
+
+    def fourier_bootstrap_key(self):
+        """(device pointer, bytes) of the Fourier BSK buffer (for RCCL broadcast)."""
+        p, b = vp(), ctypes.c_size_t()
+        _lib.call("tfhe_mi355_bootstrap_key_fourier", self._h, ctypes.byref(p), ctypes.byref(b))
+        return p.value, b.value
+
+    def fourier_bootstrap_key_set_ready(self):
+        _lib.call("tfhe_mi355_bootstrap_key_fourier_set_ready", self._h)
+
+    def upload_keyswitch_key(self, ksk: np.ndarray) -> None:
+        k = _u64(ksk).ravel()
+        _lib.call("tfhe_mi355_keyswitch_key_upload", self._h, _ptr(k), k.size)
+
+    def upload_keyswitch_key_device(self, d_ksk, numel: int, stream=None) -> None:
+        _lib.call("tfhe_mi355_keyswitch_key_upload_async", self._h, _dev_ptr(d_ksk), numel, _stream_ptr(stream))
+
+    def keyswitch_key_device(self):
+        p, b = vp(), ctypes.c_size_t()
+        _lib.call("tfhe_mi355_keyswitch_key_device", self._h, ctypes.byref(p), ctypes.byref(b))
+        return p.value, b.value
+
+    def keyswitch_key_set_ready(self):
+        _lib.call("tfhe_mi355_keyswitch_key_set_ready", self._h)
+
+    # -- host (numpy) batched ops ---------------------------------------------------------
+    def _luts(self, luts):
+        luts = _u64(luts)
+        if luts.ndim == 1:
+            luts = luts.reshape(1, -1)
+        if luts.shape[1] != self.glwe_len:
+            raise ValueError(f"lookup table has {luts.shape[1]} words, expected {self.glwe_len}")
+        return luts
+
+    @staticmethod
+    def _idx(lut_indexes, count, lut_count):
+        if lut_indexes is None:
+            return None, None
+        idx = np.ascontiguousarray(lut_indexes, dtype=np.uint32)
+        if idx.shape != (count,):
+            raise ValueError("lut_indexes must have one entry per ciphertext")
+        return idx, idx.ctypes.data_as(u32p)
+
+    def programmable_bootstrap(self, lwe_in, luts, lut_indexes=None) -> np.ndarray:
+        x = _u64(lwe_in).reshape(-1, self.n + 1)
+        L = self._luts(luts)
+        idx, idxp = self._idx(lut_indexes, x.shape[0], L.shape[0])
+        out = np.empty((x.shape[0], self.big_dim + 1), dtype=np.uint64)
+        _lib.call("tfhe_mi355_programmable_bootstrap", self._h, _ptr(x), _ptr(out), _ptr(L), L.shape[0],
+                  idxp, x.shape[0])
+        return out
+
+    def keyswitch(self, lwe_in) -> np.ndarray:
+        x = _u64(lwe_in).reshape(-1, self.big_dim + 1)
+        out = np.empty((x.shape[0], self.n + 1), dtype=np.uint64)
+        _lib.call("tfhe_mi355_keyswitch", self._h, _ptr(x), _ptr(out), x.shape[0])
+        return out
+
+    def keyswitch_programmable_bootstrap(self, lwe_in, luts, lut_indexes=None) -> np.ndarray:
+        x = _u64(lwe_in).reshape(-1, self.big_dim + 1)
+        L = self._luts(luts)
+        idx, idxp = self._idx(lut_indexes, x.shape[0], L.shape[0])
+        out = np.empty((x.shape[0], self.big_dim + 1), dtype=np.uint64)
+        _lib.call("tfhe_mi355_keyswitch_programmable_bootstrap", self._h, _ptr(x), _ptr(out), _ptr(L),
+                  L.shape[0], idxp, x.shape[0])
+        return out
+
+    def programmable_bootstrap_keyswitch(self, lwe_in, luts, lut_indexes=None) -> np.ndarray:
+        x = _u64(lwe_in).reshape(-1, self.n + 1)
+        L = self._luts(luts)
+        idx, idxp = self._idx(lut_indexes, x.shape[0], L.shape[0])
+        out = np.empty((x.shape[0], self.n + 1), dtype=np.uint64)
+        _lib.call("tfhe_mi355_programmable_bootstrap_keyswitch", self._h, _ptr(x), _ptr(out), _ptr(L),
+                  L.shape[0], idxp, x.shape[0])
+        return out
+
+    # -- device (torch) async ops -------------------------------------------------------
+    def programmable_bootstrap_async(self, d_in, d_out, d_luts, lut_count: int, count: int,
+                                     d_lut_indexes=None, stream=None) -> None:
+        _lib.call("tfhe_mi355_programmable_bootstrap_async", self._h, _dev_ptr(d_in), _dev_ptr(d_out),
+                  _dev_ptr(d_luts), lut_count, _dev_ptr(d_lut_indexes), count, _stream_ptr(stream))
+
+    def keyswitch_async(self, d_in, d_out, count: int, stream=None) -> None:
+        _lib.call("tfhe_mi355_keyswitch_async", self._h, _dev_ptr(d_in), _dev_ptr(d_out), count,
+                  _stream_ptr(stream))
+
+    def keyswitch_programmable_bootstrap_async(self, d_in, d_out, d_luts, lut_count: int, count: int,
+                                               d_scratch, d_lut_indexes=None, stream=None) -> None:
+        _lib.call("tfhe_mi355_keyswitch_programmable_bootstrap_async", self._h, _dev_ptr(d_in),
+                  _dev_ptr(d_out), _dev_ptr(d_luts), lut_count, _dev_ptr(d_lut_indexes), count,
+                  _dev_ptr(d_scratch), _stream_ptr(stream))
+
+    def ks_pbs_scratch_bytes(self, count: int) -> int:
+        b = ctypes.c_size_t()
+        _lib.call("tfhe_mi355_keyswitch_programmable_bootstrap_scratch", self._h, count, ctypes.byref(b))
+        return b.value
+
+
+def fill_accumulator(params: ClassicPBSParameters, f) -> np.ndarray:
+    """shortint fill_accumulator (shortint/engine/mod.rs:72-128) through the C ABI."""
+    p = params.message_modulus * params.carry_modulus
+    fv = _u64([int(f(i)) & 0xFFFFFFFFFFFFFFFF for i in range(p)])
+    acc = np.zeros((params.glwe_dimension + 1) * params.polynomial_size, dtype=np.uint64)
+    cp = c_params(params)
+    _lib.call("tfhe_mi355_fill_accumulator", ctypes.byref(cp), _ptr(fv), _ptr(acc))
+    return acc
