@@ -1,0 +1,25 @@
+#!/bin/bash
+# One GPU-box session: GPU parity tests, smoke, bench, rocprofv3 kernel-trace summary.
+# Each GPU step has its own time limit; a crash/timeout (rc not 0/1) stops the script.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # step NAME TIMEOUT CMD...
+  local name=$1 to=$2; shift 2
+  echo "== $name"; timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?; echo "== $name rc=$rc"; tail -5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+STAGES=${STAGES:-"tests smoke bench prof"}
+for s in $STAGES; do
+  case $s in
+    tests) step gpu_tests 600 python -m pytest tests -m gpu -x -q ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py --steps 5 --warmup 1 ;;
+    prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+    pmc1)  step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc1 -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pmc2)  step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc2 -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pmc3)  step pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD -d gpurun_out/pmc3 -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+  esac
+done
