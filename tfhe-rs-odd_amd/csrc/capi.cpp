@@ -198,7 +198,8 @@ int tfhe_mi355_context_create(const TfheMi355Parameters *params, int device, Tfh
         if (p.grouping_factor != 0) fail("multi-bit PBS (grouping_factor %u) is not available in this build", p.grouping_factor);
         if (!classic_pbs_supported((int)p.polynomial_size, (int)p.glwe_dimension, (int)p.pbs_level))
             fail("no kernel for N=%u k=%u pbs_level=%u", p.polynomial_size, p.glwe_dimension, p.pbs_level);
-        if (p.pbs_base_log == 0 || p.pbs_base_log * p.pbs_level >= 64) fail("invalid pbs decomposition");
+        if (p.pbs_base_log < 2 || p.pbs_base_log * p.pbs_level > 30)
+            fail("pbs decomposition base_log*level must be in [2, 30] (got %u x %u)", p.pbs_base_log, p.pbs_level);
         if (p.ks_level && (p.ks_base_log == 0 || p.ks_base_log * p.ks_level >= 64)) fail("invalid ks decomposition");
         if (p.lwe_dimension == 0) fail("lwe_dimension must be > 0");
         check(hipSetDevice(device), "hipSetDevice");

@@ -194,103 +194,170 @@ __device__ __forceinline__ cx gld(const double2 *__restrict__ p) {
     return {t.x, t.y};
 }
 
+// ---- twiddle sources ---------------------------------------------------------------------
+// Stage-1 twiddle of lane a, output c:   W_M[a c]           (c = 1..R1-1)
+// Stage-2 twiddle of row a1, output c2:  W_M[(M/64) a1 c2]  (c2 = 1..R2-1)
+// with W_M[t] = exp(-2 pi i t / M).  t == 0 multiplies by W[0] = (1, -0): value-identical to
+// skipping it (only the sign of a zero can change, which no later rounding observes), so the
+// multiply is unconditional (branch-free).
+template <int M>
+struct GlobalTwiddles {  // straight from the M-entry table in global memory (L1/L2)
+    const double2 *__restrict__ W;
+    __device__ __forceinline__ cx s1(int c, int lane) const { return gld(W + lane * c); }
+    __device__ __forceinline__ cx s2(int c2, int a1) const { return gld(W + (M / 64) * a1 * c2); }
+};
+// LDS copies laid out for conflict-free reads: s1 table [c-1][lane] (R1-1 x 64 entries),
+// s2 table [c2-1][a1] (R2-1 x A1 entries).
+template <int R1, int R2, int A1>
+struct LdsTwiddles {
+    const double2 *t1, *t2;
+    __device__ __forceinline__ cx s1(int c, int lane) const {
+        double2 t = t1[(c - 1) * 64 + lane];
+        return {t.x, t.y};
+    }
+    __device__ __forceinline__ cx s2(int c2, int a1) const {
+        double2 t = t2[(c2 - 1) * A1 + a1];
+        return {t.x, t.y};
+    }
+    static constexpr int s1_len = (R1 - 1) * 64;
+    static constexpr int s2_len = (R2 - 1) * A1;
+    // cooperative fill from the global W table by `nthreads` threads
+    template <int M>
+    __device__ static void fill(double2 *t1, double2 *t2, const double2 *__restrict__ W, int tid,
+                                int nthreads) {
+        for (int e = tid; e < s1_len; e += nthreads) t1[e] = W[(e & 63) * ((e >> 6) + 1)];
+        for (int e = tid; e < s2_len; e += nthreads) t2[e] = W[(M / 64) * (e % A1) * (e / A1 + 1)];
+    }
+};
+
 template <int M>
 struct WaveFft;
+
+// ---- cross-lane 4x4 transposes on gfx950 (v_permlane32_swap / v_permlane16_swap) --------
+// permlane32_swap(A, B): A <- [A.lo32, B.lo32], B <- [A.hi32, B.hi32]   (lanes 0-31 / 32-63)
+// permlane16_swap(A, B): A <- [A.r0, B.r0, A.r2, B.r2], B <- [A.r1, B.r1, A.r3, B.r3]
+__device__ __forceinline__ void pl32_swap(double &a, double &b) {
+    uint64_t ua = __double_as_longlong(a), ub = __double_as_longlong(b);
+    auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)ua, (uint32_t)ub, false, false);
+    auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(ua >> 32), (uint32_t)(ub >> 32), false, false);
+    a = __longlong_as_double(((uint64_t)hi[0] << 32) | lo[0]);
+    b = __longlong_as_double(((uint64_t)hi[1] << 32) | lo[1]);
+}
+__device__ __forceinline__ void pl16_swap(double &a, double &b) {
+    uint64_t ua = __double_as_longlong(a), ub = __double_as_longlong(b);
+    auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)ua, (uint32_t)ub, false, false);
+    auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(ua >> 32), (uint32_t)(ub >> 32), false, false);
+    a = __longlong_as_double(((uint64_t)hi[0] << 32) | lo[0]);
+    b = __longlong_as_double(((uint64_t)hi[1] << 32) | lo[1]);
+}
+__device__ __forceinline__ void pl32_swap(cx &a, cx &b) {
+    pl32_swap(a.re, b.re);
+    pl32_swap(a.im, b.im);
+}
+__device__ __forceinline__ void pl16_swap(cx &a, cx &b) {
+    pl16_swap(a.re, b.re);
+    pl16_swap(a.im, b.im);
+}
+// (register r, row-of-16 w) 4x4 transpose: R_r[w] <- R_w[r]
+__device__ __forceinline__ void transpose_rows4(cx &r0, cx &r1, cx &r2, cx &r3) {
+    pl32_swap(r0, r2);
+    pl32_swap(r1, r3);
+    pl16_swap(r0, r1);
+    pl16_swap(r2, r3);
+}
 
 // ---------------------------------------------------------------------------------------
 // M = 1024 (N = 2048): radices [16, 16, 4]; 64 lanes x 16 values.
 //   natural layout  : lane a, slot b  <->  position a + 64 b
 //   fourier layout  : lane L, slot s  <->  position 64 (L & 15) + 16 (L >> 4) + s
-// W = exp(-2 pi i t / 1024) table (t < 1024).  `sync()` orders the wave's LDS accesses.
+// stage 1 -> stage 2 goes through the wave's LDS buffer; stage 2 -> stage 3 is a register
+// transpose across the four 16-lane rows (lanes L, L+16, L+32, L+48 share cc = L & 15).
+// `sync()` orders the wave's LDS accesses.
 // ---------------------------------------------------------------------------------------
 template <>
 struct WaveFft<1024> {
     static constexpr int M = 1024;
     static constexpr int V = 16;
+    using Lds = LdsTwiddles<16, 16, 4>;
 
-    template <class Sync>
-    __device__ __forceinline__ static void forward(cx *v, cx *xb, const double2 *__restrict__ W,
-                                                   int lane, Sync sync) {
+    template <class TW, class Sync>
+    __device__ __forceinline__ static void forward(cx *v, cx *xb, const TW &tw, int lane, Sync sync) {
         // stage 1: L=1024, R=16, m=64, a = lane
         dft16_fwd(v);
 #pragma unroll
         for (int c = 1; c < 16; c++) {
-            int t = lane * c;
-            if (t) {
-                cx w = gld(W + t);
-                v[c] = cmulw(v[c], w.re, w.im);
-            }
+            cx w = tw.s1(c, lane);
+            v[c] = cmulw(v[c], w.re, w.im);
         }
+        sync();  // previous readers of xb done
 #pragma unroll
         for (int c = 0; c < 16; c++) lds_st(xb, lane + 64 * c, v[c]);
         sync();
-        // stage 2: blocks of 64 (cc), R=16, m=4 (a1)
+        // stage 2: blocks of 64 (cc), R=16, m=4 (a1 = row)
         const int cc = lane & 15, a1 = lane >> 4;
 #pragma unroll
         for (int b = 0; b < 16; b++) v[b] = lds_ld(xb, 64 * cc + a1 + 4 * b);
         dft16_fwd(v);
 #pragma unroll
         for (int c2 = 1; c2 < 16; c2++) {
-            int t = a1 * c2;
-            if (t) {
-                cx w = gld(W + 16 * t);
-                v[c2] = cmulw(v[c2], w.re, w.im);
-            }
+            cx w = tw.s2(c2, a1);
+            v[c2] = cmulw(v[c2], w.re, w.im);
         }
-        sync();
+        // lane (cc, a1) holds positions 64cc + a1 + 4 c2 -> lane (cc, j) slot 4q+b holds
+        // 64cc + 16j + 4q + b (from row b, register 4j + q)
 #pragma unroll
-        for (int c2 = 0; c2 < 16; c2++) lds_st(xb, 64 * cc + a1 + 4 * c2, v[c2]);
-        sync();
-        // stage 3: blocks of 4, R=4, m=1 -- lane (cc, j) takes positions 64cc + 16j + [0,16)
-        const int j = lane >> 4;
+        for (int q = 0; q < 4; q++) transpose_rows4(v[q], v[4 + q], v[8 + q], v[12 + q]);
+        cx t[16];
 #pragma unroll
-        for (int s = 0; s < 16; s++) v[s] = lds_ld(xb, 64 * cc + 16 * j + s);
+        for (int q = 0; q < 4; q++)
 #pragma unroll
-        for (int q = 0; q < 4; q++) r4_fwd(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-        sync();  // xb free again
+            for (int b = 0; b < 4; b++) t[4 * q + b] = v[4 * b + q];
+        // stage 3: blocks of 4, R=4, m=1
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            r4_fwd(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
+#pragma unroll
+            for (int b = 0; b < 4; b++) v[4 * q + b] = t[4 * q + b];
+        }
     }
 
-    template <class Sync>
-    __device__ __forceinline__ static void inverse(cx *v, cx *xb, const double2 *__restrict__ W,
-                                                   int lane, Sync sync) {
-        const int cc = lane & 15, j = lane >> 4, a1 = lane >> 4;
+    template <class TW, class Sync>
+    __device__ __forceinline__ static void inverse(cx *v, cx *xb, const TW &tw, int lane, Sync sync) {
+        const int cc = lane & 15, a1 = lane >> 4;
+        cx t[16];
 #pragma unroll
-        for (int q = 0; q < 4; q++) r4_inv(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+        for (int q = 0; q < 4; q++) {
+            r4_inv(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
 #pragma unroll
-        for (int s = 0; s < 16; s++) lds_st(xb, 64 * cc + 16 * j + s, v[s]);
-        sync();
+            for (int b = 0; b < 4; b++) t[4 * b + q] = v[4 * q + b];
+        }
+        // inverse of the row transpose: register 4j+q of row a1 <- slot 4q+a1 of row j
 #pragma unroll
-        for (int c2 = 0; c2 < 16; c2++) {
-            cx y = lds_ld(xb, 64 * cc + a1 + 4 * c2);
-            int t = a1 * c2;
-            if (t) {
-                cx w = gld(W + 16 * t);
-                y = cmulw(y, w.re, -w.im);
-            }
-            v[c2] = y;
+        for (int q = 0; q < 4; q++) transpose_rows4(t[q], t[4 + q], t[8 + q], t[12 + q]);
+        v[0] = t[0];
+#pragma unroll
+        for (int c2 = 1; c2 < 16; c2++) {
+            cx w = tw.s2(c2, a1);
+            v[c2] = cmulw(t[c2], w.re, -w.im);
         }
         dft16_inv(v);
-        sync();
+        sync();  // previous readers of xb done
 #pragma unroll
         for (int b = 0; b < 16; b++) lds_st(xb, 64 * cc + a1 + 4 * b, v[b]);
         sync();
+        v[0] = lds_ld(xb, lane);
 #pragma unroll
-        for (int c = 0; c < 16; c++) {
+        for (int c = 1; c < 16; c++) {
             cx y = lds_ld(xb, lane + 64 * c);
-            int t = lane * c;
-            if (t) {
-                cx w = gld(W + t);
-                y = cmulw(y, w.re, -w.im);
-            }
-            v[c] = y;
+            cx w = tw.s1(c, lane);
+            v[c] = cmulw(y, w.re, -w.im);
         }
         dft16_inv(v);
-        sync();  // xb free again
     }
 };
 
 // ---------------------------------------------------------------------------------------
-// M = 512 (N = 1024): radices [8, 8, 8]; 64 lanes x 8 values.
+// M = 512 (N = 1024): radices [8, 8, 8]; 64 lanes x 8 values, both exchanges through LDS.
 //   natural layout  : lane a, slot b  <->  position a + 64 b
 //   fourier layout  : lane L, slot s  <->  position 64 (L & 7) + 8 (L >> 3) + s
 // ---------------------------------------------------------------------------------------
@@ -298,19 +365,17 @@ template <>
 struct WaveFft<512> {
     static constexpr int M = 512;
     static constexpr int V = 8;
+    using Lds = LdsTwiddles<8, 8, 8>;
 
-    template <class Sync>
-    __device__ __forceinline__ static void forward(cx *v, cx *xb, const double2 *__restrict__ W,
-                                                   int lane, Sync sync) {
+    template <class TW, class Sync>
+    __device__ __forceinline__ static void forward(cx *v, cx *xb, const TW &tw, int lane, Sync sync) {
         dft8_fwd(v);
 #pragma unroll
         for (int c = 1; c < 8; c++) {
-            int t = lane * c;
-            if (t) {
-                cx w = gld(W + t);
-                v[c] = cmulw(v[c], w.re, w.im);
-            }
+            cx w = tw.s1(c, lane);
+            v[c] = cmulw(v[c], w.re, w.im);
         }
+        sync();
 #pragma unroll
         for (int c = 0; c < 8; c++) lds_st(xb, lane + 64 * c, v[c]);
         sync();
@@ -320,11 +385,8 @@ struct WaveFft<512> {
         dft8_fwd(v);
 #pragma unroll
         for (int c2 = 1; c2 < 8; c2++) {
-            int t = a1 * c2;
-            if (t) {
-                cx w = gld(W + 8 * t);
-                v[c2] = cmulw(v[c2], w.re, w.im);
-            }
+            cx w = tw.s2(c2, a1);
+            v[c2] = cmulw(v[c2], w.re, w.im);
         }
         sync();
 #pragma unroll
@@ -334,69 +396,57 @@ struct WaveFft<512> {
 #pragma unroll
         for (int s = 0; s < 8; s++) v[s] = lds_ld(xb, 64 * cc + 8 * j + s);
         dft8_fwd(v);
-        sync();
     }
 
-    template <class Sync>
-    __device__ __forceinline__ static void inverse(cx *v, cx *xb, const double2 *__restrict__ W,
-                                                   int lane, Sync sync) {
+    template <class TW, class Sync>
+    __device__ __forceinline__ static void inverse(cx *v, cx *xb, const TW &tw, int lane, Sync sync) {
         const int cc = lane & 7, j = lane >> 3, a1 = lane >> 3;
         dft8_inv(v);
+        sync();
 #pragma unroll
         for (int s = 0; s < 8; s++) lds_st(xb, 64 * cc + 8 * j + s, v[s]);
         sync();
+        v[0] = lds_ld(xb, 64 * cc + a1);
 #pragma unroll
-        for (int c2 = 0; c2 < 8; c2++) {
+        for (int c2 = 1; c2 < 8; c2++) {
             cx y = lds_ld(xb, 64 * cc + a1 + 8 * c2);
-            int t = a1 * c2;
-            if (t) {
-                cx w = gld(W + 8 * t);
-                y = cmulw(y, w.re, -w.im);
-            }
-            v[c2] = y;
+            cx w = tw.s2(c2, a1);
+            v[c2] = cmulw(y, w.re, -w.im);
         }
         dft8_inv(v);
         sync();
 #pragma unroll
         for (int b = 0; b < 8; b++) lds_st(xb, 64 * cc + a1 + 8 * b, v[b]);
         sync();
+        v[0] = lds_ld(xb, lane);
 #pragma unroll
-        for (int c = 0; c < 8; c++) {
+        for (int c = 1; c < 8; c++) {
             cx y = lds_ld(xb, lane + 64 * c);
-            int t = lane * c;
-            if (t) {
-                cx w = gld(W + t);
-                y = cmulw(y, w.re, -w.im);
-            }
-            v[c] = y;
+            cx w = tw.s1(c, lane);
+            v[c] = cmulw(y, w.re, -w.im);
         }
         dft8_inv(v);
-        sync();
     }
 };
 
-// f64 -> i64 by bit twiddling (exact for integral |x| < 2^64; 2^63 wraps), as
-// fft/math/fft/x86.rs:28-81.
-__device__ __forceinline__ uint64_t f64_to_u64_wrap(double x) {
-    uint64_t bits = __double_as_longlong(x);
-    uint64_t mant = (bits & 0xFFFFFFFFFFFFFULL) | 0x10000000000000ULL;
-    uint64_t biased_exp = (bits >> 52) & 0x7FF;
-    uint64_t lshift = mant << 11;
-    uint64_t rs = 1086 - biased_exp;
-    uint64_t v = rs < 64 ? (lshift >> rs) : 0;
-    v = biased_exp == 0 ? 0 : v;
-    return (bits >> 63) ? (0 - v) : v;
+// exact u64 (mod 2^64) of an integral double |v| <= 2^63: v = hi * 2^32 + lo with hi, lo
+// exact in f64; same value as the reference's f64 -> i64 bit twiddle (x86.rs:28-81).
+__device__ __forceinline__ uint64_t f64_int_to_u64(double v) {
+    double hi = floor(v * 0x1p-32);
+    double lo = fma(hi, -0x1p32, v);
+    double hu = hi < 0.0 ? hi + 0x1p32 : hi;
+    return ((uint64_t)(uint32_t)hu << 32) | (uint64_t)(uint32_t)lo;
 }
 
-// backward conversion of one complex value (x86.rs:823-874 + 961-1044): returns the two
-// torus increments for coefficients j (re) and j+M (im).
-__device__ __forceinline__ void backward_convert(cx z, cx w_scaled, uint64_t &dre, uint64_t &dim) {
-    double mr = fma(z.re, w_scaled.re, z.im * w_scaled.im);
-    double mi = fma(-z.re, w_scaled.im, z.im * w_scaled.re);
+// backward conversion (x86.rs:823-874 + 961-1044): with ws = twist / M,
+// torus increments for coefficient j (re) and j + M (im).
+__device__ __forceinline__ void backward_convert(cx z, cx ws, uint64_t &dre, uint64_t &dim) {
+    double mr = fma(z.re, ws.re, z.im * ws.im);
+    double mi = fma(-z.re, ws.im, z.im * ws.re);
     double fr = mr - rint(mr);
     double fi = mi - rint(mi);
-    dre = f64_to_u64_wrap(rint(fr * 18446744073709551616.0));
-    dim = f64_to_u64_wrap(rint(fi * 18446744073709551616.0));
+    dre = f64_int_to_u64(rint(fr * 0x1p64));
+    dim = f64_int_to_u64(rint(fi * 0x1p64));
 }
 
 }  // namespace tfhe_mi355

@@ -12,31 +12,22 @@
 // The fork's PATTERN msgpack dump (bootstrap.rs:340-342) is deliberately not reproduced.
 //
 // Design (DESIGN.md "Kernels"): one workgroup per ciphertext, one wavefront per GLWE
-// polynomial (k+1 waves).  The accumulator GLWE lives in LDS as u64; each wave rotates,
-// decomposes and forward-FFTs its own polynomial (row r = wave), the (k+1) spectra are
-// exchanged through LDS, and wave c computes output column c = sum_r F_r * GGSW[r][c]
-// (GGSW streamed from HBM/L2, 16 B per lane, coalesced), inverse-FFTs it and adds it back.
+// polynomial (k+1 waves).  Each wave keeps its accumulator polynomial in registers (u64),
+// rotates it through its LDS buffer, decomposes and forward-FFTs it (row r = wave); the (k+1)
+// spectra are exchanged through LDS and wave c computes output column c = sum_r F_r * GGSW[r][c]
+// (GGSW streamed from L2/HBM, 16 B per lane, coalesced, prefetched at the top of the CMUX),
+// inverse-FFTs it and adds it back.  FFT twiddles and the twist live in LDS.
 #include "engine.h"
 #include "fft_device.h"
 
+#ifndef PBS_WAVES_PER_EU
+#define PBS_WAVES_PER_EU 1
+#endif
+#ifndef PBS_PREFETCH_GGSW
+#define PBS_PREFETCH_GGSW 1
+#endif
+
 namespace tfhe_mi355 {
-
-__device__ __forceinline__ uint64_t closest_representable(uint64_t x, int base_log, int level) {
-    int shift = 64 - base_log * level - 1;
-    uint64_t res = x >> shift;
-    res += 1;
-    res &= ~(uint64_t)1;
-    return res << shift;
-}
-
-__device__ __forceinline__ uint64_t decompose_one_level(int base_log, uint64_t &state, uint64_t mask) {
-    uint64_t res = state & mask;
-    state >>= base_log;
-    uint64_t carry = ((res - 1) | state) & res;
-    carry >>= base_log - 1;
-    state += carry;
-    return res - (carry << base_log);
-}
 
 template <int LOG2N>
 __device__ __forceinline__ uint32_t pbs_modulus_switch(uint64_t x) {
@@ -46,155 +37,221 @@ __device__ __forceinline__ uint32_t pbs_modulus_switch(uint64_t x) {
     return (uint32_t)o;  // in [0, 2N]
 }
 
-// (X^d * p)[j] for d = full*N + rem, full in {0,1,2}
-__device__ __forceinline__ uint64_t rotated_coeff(const uint64_t *p, int N, int j, int rem, int full_odd) {
-    uint64_t v;
-    if (j < rem) {
-        v = p[N - rem + j];
-        v = full_odd ? v : 0 - v;
-    } else {
-        v = p[j - rem];
-        v = full_odd ? 0 - v : v;
-    }
-    return v;
-}
-
 constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x / 2); }
 
 struct BlockSync {
     __device__ __forceinline__ void operator()() const { __syncthreads(); }
 };
 
+// digit extraction in 32-bit registers: valid when base_log * level <= 30 (all supported
+// parameter sets).  Bit-identical digits to the 64-bit SignedDecomposer (decomposer.rs:99-119,
+// iter.rs:134-141): the only divergence is the discarded final state when the rounding
+// overflows, where every digit is 0 in both.
+template <int L>
+__device__ __forceinline__ uint32_t decomp_state32(uint64_t x, int beta) {
+    const int shift = 63 - beta * L;  // >= 33
+    uint32_t s = (uint32_t)((x >> 32) >> (shift - 32));
+    return (s + 1) >> 1;
+}
+__device__ __forceinline__ int32_t decomp_digit32(uint32_t &state, int beta, uint32_t mask) {
+    uint32_t res = state & mask;
+    state >>= beta;
+    uint32_t carry = ((res - 1) | state) & res;
+    carry >>= beta - 1;
+    state += carry;
+    return (int32_t)(res - (carry << beta));
+}
+
+template <int M>
+struct PbsLds {
+    using Tw = typename WaveFft<M>::Lds;
+    static constexpr int XL = xbuf_len(M);
+    // layout (double2 units): [twist M][s1 table][s2 table][exchange (k+1) x XL]
+    static constexpr int twist_off = 0;
+    static constexpr int s1_off = M;
+    static constexpr int s2_off = s1_off + Tw::s1_len;
+    static constexpr int xbuf_off = ((s2_off + Tw::s2_len + 3) / 4) * 4;
+    static constexpr size_t bytes(int waves) { return sizeof(double2) * (size_t)(xbuf_off + waves * XL); }
+};
+
 template <int N, int K, int L>
-__global__ void __launch_bounds__(64 * (K + 1)) pbs_classic_kernel(ClassicPbsLaunch a) {
+__global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU) pbs_classic_kernel(ClassicPbsLaunch a) {
     constexpr int M = N / 2;
     constexpr int V = M / 64;
     constexpr int LOG2N = ilog2(N);
-    constexpr int XL = xbuf_len(M);
     using Fft = WaveFft<M>;
+    using Lay = PbsLds<M>;
+    constexpr int XL = Lay::XL;
+    static_assert(sizeof(cx) * XL >= sizeof(uint64_t) * N, "exchange buffer holds one polynomial");
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    cx *xbuf = reinterpret_cast<cx *>(smem);                              // (K+1) * XL
-    uint64_t *ct0 = reinterpret_cast<uint64_t *>(smem + sizeof(cx) * (K + 1) * XL);  // (K+1) * N
+    double2 *lds = reinterpret_cast<double2 *>(smem);
+    double2 *s_twist = lds + Lay::twist_off;
+    cx *xbuf = reinterpret_cast<cx *>(lds + Lay::xbuf_off);  // (K+1) * XL, one per wave
 
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const int ct = blockIdx.x;
     const int n = a.n;
     const int beta = a.base_log;
-    const uint64_t dmask = (1ULL << beta) - 1;
+    const uint32_t dmask = (1u << beta) - 1;
+    const double norm = 1.0 / (double)M;
     BlockSync sync;
 
-    uint64_t *my = ct0 + wave * N;
+    // twiddles and twist -> LDS (once per workgroup)
+    for (int e = threadIdx.x; e < M; e += blockDim.x) s_twist[e] = a.twist[e];
+    Fft::Lds::template fill<M>(lds + Lay::s1_off, lds + Lay::s2_off, a.W, threadIdx.x, blockDim.x);
+    const typename Fft::Lds tw{lds + Lay::s1_off, lds + Lay::s2_off};
+
     cx *xb = xbuf + wave * XL;
+    uint64_t *xb64 = reinterpret_cast<uint64_t *>(xb);
     const uint64_t *in = a.lwe_in + (size_t)ct * (n + 1);
     const uint32_t li = a.lut_indexes ? a.lut_indexes[ct] : 0u;
     const uint64_t *lut = a.luts + (size_t)li * (K + 1) * N + (size_t)wave * N;
 
-    // ct0 = LUT / X^{b~}  (bootstrap.rs:255-275)
+    // this wave's accumulator polynomial, in registers: c0[h] = position lane + 64 h
+    // (h < V: j < M; h >= V: j = M + lane + 64 (h - V)).  ct0 = LUT / X^{b~}
+    // (bootstrap.rs:255-275, polynomial_wrapping_monic_monomial_div)
+    uint64_t c0[2 * V];
     {
         const uint32_t bt = pbs_modulus_switch<LOG2N>(in[n]);
         const int full = bt / N, rem = bt % N;
-        for (int j = lane; j < N; j += 64) {
-            int src = j + rem;
-            uint64_t v = src < N ? lut[src] : 0 - lut[src - N];
-            my[j] = (full & 1) ? 0 - v : v;
+#pragma unroll
+        for (int h = 0; h < 2 * V; h++) {
+            const int src = lane + 64 * h + rem;
+            const bool wrap = src >= N;
+            uint64_t v = lut[wrap ? src - N : src];
+            c0[h] = (wrap != (bool)(full & 1)) ? 0 - v : v;
         }
     }
-    sync();
 
-    // twist factors for this lane's positions j = lane + 64 b
-    const double2 *__restrict__ fbsk = a.fbsk;
     constexpr size_t ggsw_stride = (size_t)L * (K + 1) * (K + 1) * M;
+    const double2 *gcol = a.fbsk + (size_t)wave * M + lane;  // column c = wave, this lane
 
     for (int i = 0; i < n; i++) {
         const uint64_t ai = in[i];
         if (ai == 0) continue;  // bootstrap.rs:285 (uniform across the workgroup)
         const uint32_t at = pbs_modulus_switch<LOG2N>(ai);
-        const int full_odd = (at / N) & 1;
+        const bool full_odd = (at / N) & 1;
         const int rem = at % N;
 
-        // ct1 = X^{a~} ct0 - ct0 for this wave's polynomial, rounded + decomposition states
-        uint64_t st[2 * V];
+        // prefetch this CMUX's GGSW column (level L first, rows 0..k) -- 16 B per lane per slot
+        const double2 *ggsw = gcol + (size_t)i * ggsw_stride;
+        double2 g[K + 1][V];
+        if (PBS_PREFETCH_GGSW)
 #pragma unroll
-        for (int b = 0; b < V; b++) {
-            const int j0 = lane + 64 * b, j1 = j0 + M;
-            uint64_t x0 = rotated_coeff(my, N, j0, rem, full_odd) - my[j0];
-            uint64_t x1 = rotated_coeff(my, N, j1, rem, full_odd) - my[j1];
-            st[2 * b] = closest_representable(x0, beta, L) >> (64 - beta * L);
-            st[2 * b + 1] = closest_representable(x1, beta, L) >> (64 - beta * L);
+        for (int r = 0; r <= K; r++)
+#pragma unroll
+            for (int s = 0; s < V; s++)
+                g[r][s] = ggsw[((size_t)(L - 1) * (K + 1) * (K + 1) + (size_t)r * (K + 1)) * M + s * 64];
+
+        // ct1 = X^{a~} ct0 - ct0 (polynomial_algorithms.rs:425-490) through the LDS buffer
+        sync();
+#pragma unroll
+        for (int h = 0; h < 2 * V; h++) xb64[lane + 64 * h] = c0[h];
+        sync();
+        uint32_t st[2 * V];
+#pragma unroll
+        for (int h = 0; h < 2 * V; h++) {
+            const int j = lane + 64 * h;
+            const bool wrap = j < rem;  // (X^d p)[j] = -p[N-d+j] (j < d), p[j-d] otherwise
+            uint64_t r = xb64[wrap ? N - rem + j : j - rem];
+            r = (wrap != full_odd) ? 0 - r : r;
+            st[h] = decomp_state32<L>(r - c0[h], beta);
         }
 
-        cx acc[V];
-        const double2 *ggsw = fbsk + (size_t)i * ggsw_stride;
+        cx acc[L > 1 ? V : 1];
 #pragma unroll
         for (int lvl = L; lvl >= 1; lvl--) {
+            if (lvl != L || !PBS_PREFETCH_GGSW) {  // (next level's) GGSW column
+#pragma unroll
+                for (int r = 0; r <= K; r++)
+#pragma unroll
+                    for (int s = 0; s < V; s++)
+                        g[r][s] = ggsw[((size_t)(lvl - 1) * (K + 1) * (K + 1) + (size_t)r * (K + 1)) * M + s * 64];
+            }
             cx v[V];
 #pragma unroll
             for (int b = 0; b < V; b++) {
-                const int j0 = lane + 64 * b;
-                uint64_t d0 = decompose_one_level(beta, st[2 * b], dmask);
-                uint64_t d1 = decompose_one_level(beta, st[2 * b + 1], dmask);
-                cx z = {(double)(int64_t)d0, (double)(int64_t)d1};
-                cx w = gld(a.twist + j0);
-                v[b] = cmulw(z, w.re, w.im);
+                const int32_t d0 = decomp_digit32(st[b], beta, dmask);
+                const int32_t d1 = decomp_digit32(st[V + b], beta, dmask);
+                const cx z = {(double)d0, (double)d1};
+                const double2 w = s_twist[lane + 64 * b];
+                v[b] = cmulw(z, w.x, w.y);  // convert_forward_integer (x86.rs:505-596)
             }
-            Fft::forward(v, xb, a.W, lane, sync);
-            // publish this row's spectrum
+            Fft::forward(v, xb, tw, lane, sync);
+            // publish this row's spectrum to the other waves
+            sync();
+#pragma unroll
+            for (int s = 0; s < V; s++)
+                reinterpret_cast<double2 *>(xb)[s * 64 + lane] = make_double2(v[s].re, v[s].im);
+            sync();
+            // output column c = wave: sum_r F_r * G[lvl][r][c]   (ggsw.rs:524-567, update_with_fmadd)
 #pragma unroll
             for (int s = 0; s < V; s++) {
-                reinterpret_cast<double2 *>(xb)[s * 64 + lane] = make_double2(v[s].re, v[s].im);
-            }
-            sync();
-            // output column c = wave: acc += sum_r F_r * G[lvl][r][c]   (ggsw.rs:524-567)
-            const double2 *lm = ggsw + (size_t)(lvl - 1) * (K + 1) * (K + 1) * M;
+                cx o = (L > 1 && lvl != L) ? acc[L > 1 ? s : 0] : cx{0.0, 0.0};
 #pragma unroll
-            for (int r = 0; r <= K; r++) {
-                const double2 *g = lm + ((size_t)r * (K + 1) + wave) * M + lane;
-                const double2 *fr = reinterpret_cast<const double2 *>(xbuf + r * XL) + lane;
-                const bool first = (lvl == L) && (r == 0);
-#pragma unroll
-                for (int s = 0; s < V; s++) {
-                    double2 gg = g[s * 64];
-                    double2 ff = fr[s * 64];
-                    if (first) {
-                        acc[s].re = fma(gg.x, ff.x, -(gg.y * ff.y));
-                        acc[s].im = fma(gg.x, ff.y, gg.y * ff.x);
+                for (int r = 0; r <= K; r++) {
+                    const double2 gg = g[r][s];
+                    double2 ff;
+                    if (r == wave) {
+                        ff = make_double2(v[s].re, v[s].im);
                     } else {
-                        acc[s].re = fma(gg.x, ff.x, fma(-gg.y, ff.y, acc[s].re));
-                        acc[s].im = fma(gg.x, ff.y, fma(gg.y, ff.x, acc[s].im));
+                        ff = reinterpret_cast<const double2 *>(xbuf + r * XL)[s * 64 + lane];
+                    }
+                    if (lvl == L && r == 0) {
+                        o.re = fma(gg.x, ff.x, -(gg.y * ff.y));
+                        o.im = fma(gg.x, ff.y, gg.y * ff.x);
+                    } else {
+                        o.re = fma(gg.x, ff.x, fma(-gg.y, ff.y, o.re));
+                        o.im = fma(gg.x, ff.y, fma(gg.y, ff.x, o.im));
                     }
                 }
+                if constexpr (L > 1) acc[s] = o;
+                else v[s] = o;
             }
-            sync();
-        }
-
-        Fft::inverse(acc, xb, a.W, lane, sync);
-        // acc[b] = position lane + 64 b; add back as torus (fft/mod.rs:487-494)
+            if constexpr (L == 1) {
+                Fft::inverse(v, xb, tw, lane, sync);
 #pragma unroll
-        for (int b = 0; b < V; b++) {
-            const int j0 = lane + 64 * b;
-            uint64_t dre, dim;
-            backward_convert(acc[b], gld(a.twist_inv + j0), dre, dim);
-            my[j0] += dre;
-            my[j0 + M] += dim;
+                for (int b = 0; b < V; b++) {
+                    uint64_t dre, dim;
+                    const double2 w = s_twist[lane + 64 * b];
+                    backward_convert(v[b], cx{norm * w.x, norm * w.y}, dre, dim);
+                    c0[b] += dre;
+                    c0[V + b] += dim;
+                }
+            }
         }
-        sync();
+        if constexpr (L > 1) {
+            Fft::inverse(acc, xb, tw, lane, sync);
+#pragma unroll
+            for (int b = 0; b < V; b++) {
+                uint64_t dre, dim;
+                const double2 w = s_twist[lane + 64 * b];
+                backward_convert(acc[b], cx{norm * w.x, norm * w.y}, dre, dim);
+                c0[b] += dre;
+                c0[V + b] += dim;
+            }
+        }
     }
 
     // sample extract at degree 0 (glwe_sample_extraction.rs:91-147)
     uint64_t *out = a.lwe_out + (size_t)ct * (K * N + 1);
+    sync();
+#pragma unroll
+    for (int h = 0; h < 2 * V; h++) xb64[lane + 64 * h] = c0[h];
+    sync();
     if (wave < K) {
-        for (int j = lane; j < N; j += 64) out[wave * N + j] = j == 0 ? my[0] : 0 - my[N - j];
+        for (int j = lane; j < N; j += 64) out[wave * N + j] = j == 0 ? xb64[0] : 0 - xb64[N - j];
     } else if (lane == 0) {
-        out[K * N] = my[0];
+        out[K * N] = c0[0];
     }
 }
 
 template <int N, int K, int L>
 static hipError_t launch_pbs_t(const ClassicPbsLaunch &a, hipStream_t s) {
     constexpr int M = N / 2;
-    size_t lds = sizeof(cx) * (K + 1) * xbuf_len(M) + sizeof(uint64_t) * (K + 1) * N;
+    const size_t lds = PbsLds<M>::bytes(K + 1);
     if (a.count == 0) return hipSuccess;
     hipLaunchKernelGGL((pbs_classic_kernel<N, K, L>), dim3(a.count), dim3(64 * (K + 1)), lds, s, a);
     return hipGetLastError();
@@ -219,10 +276,6 @@ hipError_t launch_classic_pbs(int N, int k, int L, const ClassicPbsLaunch &a, hi
 // standard -> Fourier BSK (forward_as_torus, fft/mod.rs:197-218 + 378-385): one wave per
 // polynomial; output in the engine layout [poly][slot*64 + lane].
 // ---------------------------------------------------------------------------------------
-struct WaveSync {
-    __device__ __forceinline__ void operator()() const { __syncthreads(); }
-};
-
 template <int N>
 __global__ void __launch_bounds__(64) bsk_to_fourier_kernel(const uint64_t *__restrict__ polys,
                                                             double2 *__restrict__ out, size_t npoly,
@@ -246,7 +299,7 @@ __global__ void __launch_bounds__(64) bsk_to_fourier_kernel(const uint64_t *__re
         v[b].re = xr * w.re - xi * w.im;
         v[b].im = xr * w.im + xi * w.re;
     }
-    WaveFft<M>::forward(v, xb, W, lane, WaveSync{});
+    WaveFft<M>::forward(v, xb, GlobalTwiddles<M>{W}, lane, BlockSync{});
     double2 *o = out + p * M + lane;
 #pragma unroll
     for (int s = 0; s < V; s++) o[s * 64] = make_double2(v[s].re, v[s].im);

@@ -10,7 +10,7 @@ import ctypes
 import os
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libtfhe_mi355.so")
+LIB_PATH = os.environ.get("TFHE_MI355_LIB") or os.path.join(_PKG_ROOT, "lib", "libtfhe_mi355.so")
 
 u64p = ctypes.POINTER(ctypes.c_uint64)
 u32p = ctypes.POINTER(ctypes.c_uint32)
