@@ -141,3 +141,25 @@ def test_oracle_keyswitch_round_trip(orc, keys_2_2):
     small = orc.keyswitch(keys_2_2.ksk, p.big_lwe_dimension, p.lwe_dimension, p.ks_base_log, p.ks_level, big)
     dec = decode(orc.lwe_decrypt(keys_2_2.lwe_sk, small), delta) % 16
     assert np.array_equal(dec, msgs)
+
+
+@pytest.mark.parametrize("beta", [23, 21, 15, 10])
+def test_single_level_digit_shortcut_matches_decomposer(orc, beta):
+    """The HIP kernel's L=1 digit shortcut (pbs_classic.hip digit_l1):
+    bfe((x_hi >> (31 - beta)) + 2^beta - 1, 1, beta) - (2^(beta-1) - 1)
+    must equal the SignedDecomposer digit (decomposer.rs:99-153, iter.rs:134-141)."""
+    rng = np.random.default_rng(beta)
+    xs = [int(x) for x in rng.integers(0, 2 ** 64, 3000, dtype=np.uint64)]
+    # rounding ties and overflow edges: values around multiples of 2^(63-beta)
+    for k in [0, 1, 2, (1 << beta) - 1, 1 << beta, (1 << (beta - 1)), (1 << (beta - 1)) + 1, (1 << (beta + 1)) - 1]:
+        for d in [-1, 0, 1]:
+            xs.append(((k << (63 - beta)) + d) % (1 << 64))
+    mask = (1 << beta) - 1
+    h = (1 << (beta - 1)) - 1
+    for x in xs:
+        hi = x >> 32
+        t = ((hi >> (31 - beta)) + mask) & 0xFFFFFFFF
+        d = ((t >> 1) & mask) - h
+        ref = orc.decompose(x, beta, 1)[0]
+        ref = ref - (1 << 64) if ref >= (1 << 63) else ref
+        assert d == ref, (hex(x), d, ref)

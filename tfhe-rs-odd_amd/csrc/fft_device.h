@@ -189,6 +189,22 @@ __device__ __forceinline__ cx lds_ld(const cx *xb, int p) {
     double2 t = reinterpret_cast<const double2 *>(xb)[xpad(p)];
     return {t.x, t.y};
 }
+// M = 1024 exchange addressing.  Default: one pad slot per 64 positions (p + p/64): both access
+// patterns (lane + 64 c, and 64 cc + a1 + 4 b) become a per-lane base + compile-time immediate
+// offsets.  TM_XCHG_XOR=1: unpadded buffer with an XOR swizzle of the 16-B slot,
+// p ^ ((p >> 6) & 15) (saves 256 B per buffer, costs per-access address math).
+#ifndef TM_XCHG_XOR
+#define TM_XCHG_XOR 1
+#endif
+__device__ __forceinline__ int xswz(int p) { return TM_XCHG_XOR ? (p ^ ((p >> 6) & 15)) : xpad(p); }
+constexpr int xbuf_len_1024() { return TM_XCHG_XOR ? 1024 : xbuf_len(1024); }
+__device__ __forceinline__ void lds_stx(cx *xb, int p, cx v) {
+    reinterpret_cast<double2 *>(xb)[xswz(p)] = make_double2(v.re, v.im);
+}
+__device__ __forceinline__ cx lds_ldx(const cx *xb, int p) {
+    double2 t = reinterpret_cast<const double2 *>(xb)[xswz(p)];
+    return {t.x, t.y};
+}
 __device__ __forceinline__ cx gld(const double2 *__restrict__ p) {
     double2 t = *p;
     return {t.x, t.y};
@@ -278,6 +294,7 @@ template <>
 struct WaveFft<1024> {
     static constexpr int M = 1024;
     static constexpr int V = 16;
+    static constexpr int XL = xbuf_len_1024();  // exchange buffer entries
     using Lds = LdsTwiddles<16, 16, 4>;
 
     template <class TW, class Sync>
@@ -286,20 +303,22 @@ struct WaveFft<1024> {
         dft16_fwd(v);
 #pragma unroll
         for (int c = 1; c < 16; c++) {
+            if ((c & 3) == 1) __builtin_amdgcn_sched_barrier(0);  // bound twiddle loads in flight
             cx w = tw.s1(c, lane);
             v[c] = cmulw(v[c], w.re, w.im);
         }
         sync();  // previous readers of xb done
 #pragma unroll
-        for (int c = 0; c < 16; c++) lds_st(xb, lane + 64 * c, v[c]);
+        for (int c = 0; c < 16; c++) lds_stx(xb, lane + 64 * c, v[c]);
         sync();
         // stage 2: blocks of 64 (cc), R=16, m=4 (a1 = row)
         const int cc = lane & 15, a1 = lane >> 4;
 #pragma unroll
-        for (int b = 0; b < 16; b++) v[b] = lds_ld(xb, 64 * cc + a1 + 4 * b);
+        for (int b = 0; b < 16; b++) v[b] = lds_ldx(xb, 64 * cc + a1 + 4 * b);
         dft16_fwd(v);
 #pragma unroll
         for (int c2 = 1; c2 < 16; c2++) {
+            if ((c2 & 3) == 1) __builtin_amdgcn_sched_barrier(0);
             cx w = tw.s2(c2, a1);
             v[c2] = cmulw(v[c2], w.re, w.im);
         }
@@ -343,12 +362,12 @@ struct WaveFft<1024> {
         dft16_inv(v);
         sync();  // previous readers of xb done
 #pragma unroll
-        for (int b = 0; b < 16; b++) lds_st(xb, 64 * cc + a1 + 4 * b, v[b]);
+        for (int b = 0; b < 16; b++) lds_stx(xb, 64 * cc + a1 + 4 * b, v[b]);
         sync();
-        v[0] = lds_ld(xb, lane);
+        v[0] = lds_ldx(xb, lane);
 #pragma unroll
         for (int c = 1; c < 16; c++) {
-            cx y = lds_ld(xb, lane + 64 * c);
+            cx y = lds_ldx(xb, lane + 64 * c);
             cx w = tw.s1(c, lane);
             v[c] = cmulw(y, w.re, -w.im);
         }
@@ -365,6 +384,7 @@ template <>
 struct WaveFft<512> {
     static constexpr int M = 512;
     static constexpr int V = 8;
+    static constexpr int XL = xbuf_len(512);  // exchange buffer entries (padded)
     using Lds = LdsTwiddles<8, 8, 8>;
 
     template <class TW, class Sync>
@@ -438,6 +458,23 @@ __device__ __forceinline__ uint64_t f64_int_to_u64(double v) {
     return ((uint64_t)(uint32_t)hu << 32) | (uint64_t)(uint32_t)lo;
 }
 
+// c += v (mod 2^64) for an integral double |v| <= 2^63, without building the u64:
+// hi = floor(v / 2^32) in [-2^31, 2^31] and lo = v - hi 2^32 in [0, 2^32) are exact; the
+// v_cvt_i32_f64 of hi is exact except hi = 2^31 (v = 2^63), where it clamps to 2^31 - 1 and is
+// corrected by +1 (2^31 mod 2^32 = 0x80000000).
+__device__ __forceinline__ void torus_add(uint64_t &c, double v) {
+    const double hi = floor(v * 0x1p-32);
+    const double lo = fma(hi, -0x1p32, v);
+    int32_t hi_i;
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(hi_i) : "v"(hi));
+    const uint32_t hi_u = (uint32_t)hi_i + (hi >= 0x1p31 ? 1u : 0u);
+    const uint32_t lo_u = (uint32_t)lo;
+    unsigned int cy;
+    const uint32_t nlo = __builtin_addc((uint32_t)c, lo_u, 0u, &cy);
+    const uint32_t nhi = (uint32_t)(c >> 32) + hi_u + cy;
+    c = ((uint64_t)nhi << 32) | (uint64_t)nlo;
+}
+
 // backward conversion (x86.rs:823-874 + 961-1044): with ws = twist / M,
 // torus increments for coefficient j (re) and j + M (im).
 __device__ __forceinline__ void backward_convert(cx z, cx ws, uint64_t &dre, uint64_t &dim) {
@@ -447,6 +484,15 @@ __device__ __forceinline__ void backward_convert(cx z, cx ws, uint64_t &dre, uin
     double fi = mi - rint(mi);
     dre = f64_int_to_u64(rint(fr * 0x1p64));
     dim = f64_int_to_u64(rint(fi * 0x1p64));
+}
+// same, added in place: c_re += increment(j), c_im += increment(j + M)
+__device__ __forceinline__ void backward_add(cx z, cx ws, uint64_t &c_re, uint64_t &c_im) {
+    double mr = fma(z.re, ws.re, z.im * ws.im);
+    double mi = fma(-z.re, ws.im, z.im * ws.re);
+    double fr = mr - rint(mr);
+    double fi = mi - rint(mi);
+    torus_add(c_re, rint(fr * 0x1p64));
+    torus_add(c_im, rint(fi * 0x1p64));
 }
 
 }  // namespace tfhe_mi355

@@ -11,20 +11,24 @@
 //   par_convert_polynomials_list_to_fourier           fft64/math/fft/mod.rs:719-764
 // The fork's PATTERN msgpack dump (bootstrap.rs:340-342) is deliberately not reproduced.
 //
-// Design (DESIGN.md "Kernels"): one workgroup per ciphertext, one wavefront per GLWE
-// polynomial (k+1 waves).  Each wave keeps its accumulator polynomial in registers (u64),
-// rotates it through its LDS buffer, decomposes and forward-FFTs it (row r = wave); the (k+1)
-// spectra are exchanged through LDS and wave c computes output column c = sum_r F_r * GGSW[r][c]
-// (GGSW streamed from L2/HBM, 16 B per lane, coalesced, prefetched at the top of the CMUX),
-// inverse-FFTs it and adds it back.  FFT twiddles and the twist live in LDS.
+// Design (DESIGN.md "Kernels"): a workgroup bootstraps CPW ciphertexts, one wavefront per
+// GLWE polynomial ((k+1) waves per ciphertext).  Each wave keeps its accumulator polynomial in
+// registers (u64), rotates it through its LDS buffer, decomposes and forward-FFTs it
+// (row r = its polynomial); the (k+1) spectra of a ciphertext are exchanged through LDS and
+// wave c computes output column c = sum_r F_r * GGSW[r][c] (GGSW streamed from L2/HBM, 16 B
+// per lane, coalesced), inverse-FFTs it and adds it back.  FFT twiddles and the twist live in
+// LDS, shared by the CPW ciphertexts.  At N = 2048: CPW = 4 -> 8 waves = 2 per SIMD, LDS
+// 32.7 KiB tables + 8 x 16 KiB buffers = 163,776 B.
+//
+// Control flow is uniform across the workgroup (barriers): a CMUX whose mask element is 0
+// (skipped by the reference, bootstrap.rs:285) is executed as a rotation by 0, which adds
+// exactly 0 to the accumulator (ct1 = 0 -> digits 0 -> spectra +-0 -> increments 0), so the
+// output bits are unchanged.
 #include "engine.h"
 #include "fft_device.h"
 
 #ifndef PBS_WAVES_PER_EU
 #define PBS_WAVES_PER_EU 1
-#endif
-#ifndef PBS_PREFETCH_GGSW
-#define PBS_PREFETCH_GGSW 1
 #endif
 
 namespace tfhe_mi355 {
@@ -53,6 +57,18 @@ __device__ __forceinline__ uint32_t decomp_state32(uint64_t x, int beta) {
     uint32_t s = (uint32_t)((x >> 32) >> (shift - 32));
     return (s + 1) >> 1;
 }
+template <int L>
+__device__ __forceinline__ uint32_t decomp_state32_hi(uint32_t x_hi, int beta) {
+    const int shift = 63 - beta * L;  // >= 33
+    return ((x_hi >> (shift - 32)) + 1) >> 1;
+}
+// L = 1: s = ((x >> (63 - beta)) + 1) >> 1, digit = s mod 2^beta balanced into
+// (-2^(beta-1), 2^(beta-1)] -- the SignedDecomposer's carry rule for one level, since the
+// state left after the level is 0 or 1 and only 1 when the digit is 0.
+// With c = 2^beta - 1 and h = 2^(beta-1) - 1:  digit = bfe(a + c, 1, beta) - h, a = x_hi >> (31 - beta).
+__device__ __forceinline__ int32_t digit_l1(uint32_t x_hi, int k, uint32_t c, int beta, int32_t h) {
+    return (int32_t)__builtin_amdgcn_ubfe((x_hi >> k) + c, 1, beta) - h;
+}
 __device__ __forceinline__ int32_t decomp_digit32(uint32_t &state, int beta, uint32_t mask) {
     uint32_t res = state & mask;
     state >>= beta;
@@ -64,9 +80,10 @@ __device__ __forceinline__ int32_t decomp_digit32(uint32_t &state, int beta, uin
 
 template <int M>
 struct PbsLds {
-    using Tw = typename WaveFft<M>::Lds;
-    static constexpr int XL = xbuf_len(M);
-    // layout (double2 units): [twist M][s1 table][s2 table][exchange (k+1) x XL]
+    using Fft = WaveFft<M>;
+    using Tw = typename Fft::Lds;
+    static constexpr int XL = Fft::XL;
+    // layout (double2 units): [twist M][s1 table][s2 table][exchange: one XL buffer per wave]
     static constexpr int twist_off = 0;
     static constexpr int s1_off = M;
     static constexpr int s2_off = s1_off + Tw::s1_len;
@@ -74,11 +91,21 @@ struct PbsLds {
     static constexpr size_t bytes(int waves) { return sizeof(double2) * (size_t)(xbuf_off + waves * XL); }
 };
 
+#ifndef PBS_CPW
+#define PBS_CPW 1
+#endif
+template <int N>
+struct PbsConfig {
+    static constexpr int CPW = PBS_CPW;  // ciphertexts per workgroup
+};
+
 template <int N, int K, int L>
-__global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU) pbs_classic_kernel(ClassicPbsLaunch a) {
+__global__ void __launch_bounds__(64 * (K + 1) * PbsConfig<N>::CPW, PBS_WAVES_PER_EU)
+    pbs_classic_kernel(ClassicPbsLaunch a) {
     constexpr int M = N / 2;
     constexpr int V = M / 64;
     constexpr int LOG2N = ilog2(N);
+    constexpr int CPW = PbsConfig<N>::CPW;
     using Fft = WaveFft<M>;
     using Lay = PbsLds<M>;
     constexpr int XL = Lay::XL;
@@ -86,24 +113,33 @@ __global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU) pbs_classic_ke
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double2 *lds = reinterpret_cast<double2 *>(smem);
-    double2 *s_twist = lds + Lay::twist_off;
-    cx *xbuf = reinterpret_cast<cx *>(lds + Lay::xbuf_off);  // (K+1) * XL, one per wave
+    const double2 *s_twist = lds + Lay::twist_off;
 
-    const int wave = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63;
-    const int ct = blockIdx.x;
+    // wave-uniform ids in SGPRs: per-ciphertext pointers and the mask element loads stay scalar
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane0 = threadIdx.x & 63;
+    int lane = lane0;
+    const int wave = wid % (K + 1);        // polynomial of the ciphertext this wave owns
+    const int slot = wid / (K + 1);        // ciphertext slot in the workgroup
+    const int ct_raw = blockIdx.x * CPW + slot;
+    const bool active = ct_raw < a.count;  // idle slots compute on a valid ct, store nothing
+    const int ct = active ? ct_raw : a.count - 1;
     const int n = a.n;
     const int beta = a.base_log;
     const uint32_t dmask = (1u << beta) - 1;
+    const int dk1 = 31 - beta;                        // L = 1 digit constants (digit_l1)
+    const uint32_t dc1 = dmask;
+    const int32_t dh1 = (int32_t)(1u << (beta - 1)) - 1;
     const double norm = 1.0 / (double)M;
     BlockSync sync;
 
     // twiddles and twist -> LDS (once per workgroup)
-    for (int e = threadIdx.x; e < M; e += blockDim.x) s_twist[e] = a.twist[e];
+    for (int e = threadIdx.x; e < M; e += blockDim.x) lds[Lay::twist_off + e] = a.twist[e];
     Fft::Lds::template fill<M>(lds + Lay::s1_off, lds + Lay::s2_off, a.W, threadIdx.x, blockDim.x);
     const typename Fft::Lds tw{lds + Lay::s1_off, lds + Lay::s2_off};
 
-    cx *xb = xbuf + wave * XL;
+    cx *xct = reinterpret_cast<cx *>(lds + Lay::xbuf_off) + (size_t)slot * (K + 1) * XL;  // this ct's buffers
+    cx *xb = xct + wave * XL;
     uint64_t *xb64 = reinterpret_cast<uint64_t *>(xb);
     const uint64_t *in = a.lwe_in + (size_t)ct * (n + 1);
     const uint32_t li = a.lut_indexes ? a.lut_indexes[ct] : 0u;
@@ -129,75 +165,76 @@ __global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU) pbs_classic_ke
     const double2 *gcol = a.fbsk + (size_t)wave * M + lane;  // column c = wave, this lane
 
     for (int i = 0; i < n; i++) {
-        const uint64_t ai = in[i];
-        if (ai == 0) continue;  // bootstrap.rs:285 (uniform across the workgroup)
-        const uint32_t at = pbs_modulus_switch<LOG2N>(ai);
+        // Every LDS/GGSW address below is a function of the lane only (loop invariant); hoisted
+        // out of the CMUX loop they pin ~100 VGPRs and spill.  An opaque per-iteration copy of the
+        // lane id makes them cheap per-iteration recomputations instead.
+        int lane = lane0;
+        asm volatile("" : "+v"(lane));
+        const uint32_t at = pbs_modulus_switch<LOG2N>(in[i]);
         const bool full_odd = (at / N) & 1;
         const int rem = at % N;
-
-        // prefetch this CMUX's GGSW column (level L first, rows 0..k) -- 16 B per lane per slot
         const double2 *ggsw = gcol + (size_t)i * ggsw_stride;
-        double2 g[K + 1][V];
-        if (PBS_PREFETCH_GGSW)
-#pragma unroll
-        for (int r = 0; r <= K; r++)
-#pragma unroll
-            for (int s = 0; s < V; s++)
-                g[r][s] = ggsw[((size_t)(L - 1) * (K + 1) * (K + 1) + (size_t)r * (K + 1)) * M + s * 64];
 
         // ct1 = X^{a~} ct0 - ct0 (polynomial_algorithms.rs:425-490) through the LDS buffer
         sync();
 #pragma unroll
         for (int h = 0; h < 2 * V; h++) xb64[lane + 64 * h] = c0[h];
         sync();
-        uint32_t st[2 * V];
+        // (X^d p)[j] = -p[N-d+j] for j < d, p[j-d] otherwise (sign flipped again when the
+        // rotation passes a full N); only the top 32 bits of ct1 feed the decomposition.
+        const int rbase = lane - rem;
+        auto ct1_hi = [&](int h) -> uint32_t {
+            const int jj = rbase + 64 * h;
+            const bool neg = (jj < 0) != full_odd;
+            const uint64_t x = xb64[(unsigned)jj & (unsigned)(N - 1)];
+            const uint64_t r = neg ? 0 - x : x;
+            return (uint32_t)((r - c0[h]) >> 32);
+        };
+        uint32_t st[L > 1 ? 2 * V : 1];
+        if constexpr (L > 1) {
 #pragma unroll
-        for (int h = 0; h < 2 * V; h++) {
-            const int j = lane + 64 * h;
-            const bool wrap = j < rem;  // (X^d p)[j] = -p[N-d+j] (j < d), p[j-d] otherwise
-            uint64_t r = xb64[wrap ? N - rem + j : j - rem];
-            r = (wrap != full_odd) ? 0 - r : r;
-            st[h] = decomp_state32<L>(r - c0[h], beta);
+            for (int h = 0; h < 2 * V; h++) st[h] = decomp_state32_hi<L>(ct1_hi(h), beta);
         }
 
         cx acc[L > 1 ? V : 1];
 #pragma unroll
         for (int lvl = L; lvl >= 1; lvl--) {
-            if (lvl != L || !PBS_PREFETCH_GGSW) {  // (next level's) GGSW column
-#pragma unroll
-                for (int r = 0; r <= K; r++)
-#pragma unroll
-                    for (int s = 0; s < V; s++)
-                        g[r][s] = ggsw[((size_t)(lvl - 1) * (K + 1) * (K + 1) + (size_t)r * (K + 1)) * M + s * 64];
-            }
             cx v[V];
 #pragma unroll
             for (int b = 0; b < V; b++) {
-                const int32_t d0 = decomp_digit32(st[b], beta, dmask);
-                const int32_t d1 = decomp_digit32(st[V + b], beta, dmask);
+                int32_t d0, d1;
+                if constexpr (L == 1) {
+                    d0 = digit_l1(ct1_hi(b), dk1, dc1, beta, dh1);
+                    d1 = digit_l1(ct1_hi(V + b), dk1, dc1, beta, dh1);
+                } else {
+                    d0 = decomp_digit32(st[b], beta, dmask);
+                    d1 = decomp_digit32(st[V + b], beta, dmask);
+                }
                 const cx z = {(double)d0, (double)d1};
                 const double2 w = s_twist[lane + 64 * b];
                 v[b] = cmulw(z, w.x, w.y);  // convert_forward_integer (x86.rs:505-596)
             }
             Fft::forward(v, xb, tw, lane, sync);
-            // publish this row's spectrum to the other waves
+            // publish this row's spectrum to the ciphertext's other waves
             sync();
 #pragma unroll
             for (int s = 0; s < V; s++)
                 reinterpret_cast<double2 *>(xb)[s * 64 + lane] = make_double2(v[s].re, v[s].im);
             sync();
             // output column c = wave: sum_r F_r * G[lvl][r][c]   (ggsw.rs:524-567, update_with_fmadd)
+            const double2 *lm = ggsw + (size_t)(lvl - 1) * (K + 1) * (K + 1) * M;
 #pragma unroll
             for (int s = 0; s < V; s++) {
+                if (s % 4 == 0) __builtin_amdgcn_sched_barrier(0);  // bound loads in flight
                 cx o = (L > 1 && lvl != L) ? acc[L > 1 ? s : 0] : cx{0.0, 0.0};
 #pragma unroll
                 for (int r = 0; r <= K; r++) {
-                    const double2 gg = g[r][s];
+                    const double2 gg = lm[(size_t)r * (K + 1) * M + s * 64];
                     double2 ff;
                     if (r == wave) {
                         ff = make_double2(v[s].re, v[s].im);
                     } else {
-                        ff = reinterpret_cast<const double2 *>(xbuf + r * XL)[s * 64 + lane];
+                        ff = reinterpret_cast<const double2 *>(xct + r * XL)[s * 64 + lane];
                     }
                     if (lvl == L && r == 0) {
                         o.re = fma(gg.x, ff.x, -(gg.y * ff.y));
@@ -214,11 +251,8 @@ __global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU) pbs_classic_ke
                 Fft::inverse(v, xb, tw, lane, sync);
 #pragma unroll
                 for (int b = 0; b < V; b++) {
-                    uint64_t dre, dim;
                     const double2 w = s_twist[lane + 64 * b];
-                    backward_convert(v[b], cx{norm * w.x, norm * w.y}, dre, dim);
-                    c0[b] += dre;
-                    c0[V + b] += dim;
+                    backward_add(v[b], cx{norm * w.x, norm * w.y}, c0[b], c0[V + b]);
                 }
             }
         }
@@ -226,21 +260,19 @@ __global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU) pbs_classic_ke
             Fft::inverse(acc, xb, tw, lane, sync);
 #pragma unroll
             for (int b = 0; b < V; b++) {
-                uint64_t dre, dim;
                 const double2 w = s_twist[lane + 64 * b];
-                backward_convert(acc[b], cx{norm * w.x, norm * w.y}, dre, dim);
-                c0[b] += dre;
-                c0[V + b] += dim;
+                backward_add(acc[b], cx{norm * w.x, norm * w.y}, c0[b], c0[V + b]);
             }
         }
     }
 
     // sample extract at degree 0 (glwe_sample_extraction.rs:91-147)
-    uint64_t *out = a.lwe_out + (size_t)ct * (K * N + 1);
     sync();
 #pragma unroll
     for (int h = 0; h < 2 * V; h++) xb64[lane + 64 * h] = c0[h];
     sync();
+    if (!active) return;
+    uint64_t *out = a.lwe_out + (size_t)ct * (K * N + 1);
     if (wave < K) {
         for (int j = lane; j < N; j += 64) out[wave * N + j] = j == 0 ? xb64[0] : 0 - xb64[N - j];
     } else if (lane == 0) {
@@ -251,9 +283,11 @@ __global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU) pbs_classic_ke
 template <int N, int K, int L>
 static hipError_t launch_pbs_t(const ClassicPbsLaunch &a, hipStream_t s) {
     constexpr int M = N / 2;
-    const size_t lds = PbsLds<M>::bytes(K + 1);
+    constexpr int CPW = PbsConfig<N>::CPW;
+    const size_t lds = PbsLds<M>::bytes((K + 1) * CPW);
     if (a.count == 0) return hipSuccess;
-    hipLaunchKernelGGL((pbs_classic_kernel<N, K, L>), dim3(a.count), dim3(64 * (K + 1)), lds, s, a);
+    const int blocks = (a.count + CPW - 1) / CPW;
+    hipLaunchKernelGGL((pbs_classic_kernel<N, K, L>), dim3(blocks), dim3(64 * (K + 1) * CPW), lds, s, a);
     return hipGetLastError();
 }
 
@@ -310,10 +344,10 @@ hipError_t launch_bsk_to_fourier(int N, const uint64_t *std_polys, double2 *four
     if (npoly == 0) return hipSuccess;
     if (N == 2048) {
         hipLaunchKernelGGL(bsk_to_fourier_kernel<2048>, dim3(npoly), dim3(64),
-                           sizeof(cx) * xbuf_len(1024), s, std_polys, fourier, npoly, t.W, t.twist);
+                           sizeof(cx) * WaveFft<1024>::XL, s, std_polys, fourier, npoly, t.W, t.twist);
     } else if (N == 1024) {
         hipLaunchKernelGGL(bsk_to_fourier_kernel<1024>, dim3(npoly), dim3(64),
-                           sizeof(cx) * xbuf_len(512), s, std_polys, fourier, npoly, t.W, t.twist);
+                           sizeof(cx) * WaveFft<512>::XL, s, std_polys, fourier, npoly, t.W, t.twist);
     } else {
         return hipErrorInvalidValue;
     }
