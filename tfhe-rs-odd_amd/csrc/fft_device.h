@@ -231,18 +231,19 @@ struct LdsTwiddles {
         double2 t = t1[(c - 1) * 64 + lane];
         return {t.x, t.y};
     }
+    // stage-2 twiddle W[(M/64) a1 c2] = W[lane' c2] with lane' = (64/A1) a1 < 64: an s1 entry
     __device__ __forceinline__ cx s2(int c2, int a1) const {
-        double2 t = t2[(c2 - 1) * A1 + a1];
+        static_assert(R2 <= R1, "stage-2 twiddles are read from the stage-1 table");
+        double2 t = t1[(c2 - 1) * 64 + (64 / A1) * a1];
         return {t.x, t.y};
     }
     static constexpr int s1_len = (R1 - 1) * 64;
-    static constexpr int s2_len = (R2 - 1) * A1;
+    static constexpr int s2_len = 0;
     // cooperative fill from the global W table by `nthreads` threads
     template <int M>
-    __device__ static void fill(double2 *t1, double2 *t2, const double2 *__restrict__ W, int tid,
+    __device__ static void fill(double2 *t1, double2 *, const double2 *__restrict__ W, int tid,
                                 int nthreads) {
         for (int e = tid; e < s1_len; e += nthreads) t1[e] = W[(e & 63) * ((e >> 6) + 1)];
-        for (int e = tid; e < s2_len; e += nthreads) t2[e] = W[(M / 64) * (e % A1) * (e / A1 + 1)];
     }
 };
 

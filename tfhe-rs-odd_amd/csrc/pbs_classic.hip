@@ -27,6 +27,9 @@
 #include "engine.h"
 #include "fft_device.h"
 
+#ifndef PBS_WAVE_LOCAL
+#define PBS_WAVE_LOCAL 1
+#endif
 #ifndef PBS_WAVES_PER_EU
 #define PBS_WAVES_PER_EU 1
 #endif
@@ -45,6 +48,16 @@ constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x / 2); }
 
 struct BlockSync {
     __device__ __forceinline__ void operator()() const { __syncthreads(); }
+};
+// Orders LDS accesses among the lanes of ONE wavefront: LDS executes a wave's ds_* operations
+// in issue order, so a compiler-level fence at wavefront scope is all a wave-private buffer
+// (rotation, FFT exchanges) needs -- no s_barrier across the workgroup.
+struct WaveLocalSync {
+    __device__ __forceinline__ void operator()() const {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
 };
 
 // digit extraction in 32-bit registers: valid when base_log * level <= 30 (all supported
@@ -131,12 +144,18 @@ __global__ void __launch_bounds__(64 * (K + 1) * PbsConfig<N>::CPW, PBS_WAVES_PE
     const uint32_t dc1 = dmask;
     const int32_t dh1 = (int32_t)(1u << (beta - 1)) - 1;
     const double norm = 1.0 / (double)M;
-    BlockSync sync;
+    BlockSync sync;       // cross-wave: spectrum exchange
+#if PBS_WAVE_LOCAL
+    WaveLocalSync wsync;  // wave-private buffer reuse
+#else
+    BlockSync wsync;
+#endif
 
     // twiddles and twist -> LDS (once per workgroup)
     for (int e = threadIdx.x; e < M; e += blockDim.x) lds[Lay::twist_off + e] = a.twist[e];
     Fft::Lds::template fill<M>(lds + Lay::s1_off, lds + Lay::s2_off, a.W, threadIdx.x, blockDim.x);
     const typename Fft::Lds tw{lds + Lay::s1_off, lds + Lay::s2_off};
+    sync();  // tables visible to every wave (the CMUX loop itself only syncs wave-locally)
 
     cx *xct = reinterpret_cast<cx *>(lds + Lay::xbuf_off) + (size_t)slot * (K + 1) * XL;  // this ct's buffers
     cx *xb = xct + wave * XL;
@@ -176,10 +195,11 @@ __global__ void __launch_bounds__(64 * (K + 1) * PbsConfig<N>::CPW, PBS_WAVES_PE
         const double2 *ggsw = gcol + (size_t)i * ggsw_stride;
 
         // ct1 = X^{a~} ct0 - ct0 (polynomial_algorithms.rs:425-490) through the LDS buffer
-        sync();
+        // (wave-private: the other waves' last reads of it ended at the post-MAC barrier)
+        wsync();
 #pragma unroll
         for (int h = 0; h < 2 * V; h++) xb64[lane + 64 * h] = c0[h];
-        sync();
+        wsync();
         // (X^d p)[j] = -p[N-d+j] for j < d, p[j-d] otherwise (sign flipped again when the
         // rotation passes a full N); only the top 32 bits of ct1 feed the decomposition.
         const int rbase = lane - rem;
@@ -214,9 +234,9 @@ __global__ void __launch_bounds__(64 * (K + 1) * PbsConfig<N>::CPW, PBS_WAVES_PE
                 const double2 w = s_twist[lane + 64 * b];
                 v[b] = cmulw(z, w.x, w.y);  // convert_forward_integer (x86.rs:505-596)
             }
-            Fft::forward(v, xb, tw, lane, sync);
+            Fft::forward(v, xb, tw, lane, wsync);
             // publish this row's spectrum to the ciphertext's other waves
-            sync();
+            wsync();
 #pragma unroll
             for (int s = 0; s < V; s++)
                 reinterpret_cast<double2 *>(xb)[s * 64 + lane] = make_double2(v[s].re, v[s].im);
@@ -247,8 +267,9 @@ __global__ void __launch_bounds__(64 * (K + 1) * PbsConfig<N>::CPW, PBS_WAVES_PE
                 if constexpr (L > 1) acc[s] = o;
                 else v[s] = o;
             }
+            sync();  // every wave is done reading the published spectra before xb is reused
             if constexpr (L == 1) {
-                Fft::inverse(v, xb, tw, lane, sync);
+                Fft::inverse(v, xb, tw, lane, wsync);
 #pragma unroll
                 for (int b = 0; b < V; b++) {
                     const double2 w = s_twist[lane + 64 * b];
@@ -257,7 +278,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PbsConfig<N>::CPW, PBS_WAVES_PE
             }
         }
         if constexpr (L > 1) {
-            Fft::inverse(acc, xb, tw, lane, sync);
+            Fft::inverse(acc, xb, tw, lane, wsync);
 #pragma unroll
             for (int b = 0; b < V; b++) {
                 const double2 w = s_twist[lane + 64 * b];
@@ -267,10 +288,10 @@ __global__ void __launch_bounds__(64 * (K + 1) * PbsConfig<N>::CPW, PBS_WAVES_PE
     }
 
     // sample extract at degree 0 (glwe_sample_extraction.rs:91-147)
-    sync();
+    wsync();
 #pragma unroll
     for (int h = 0; h < 2 * V; h++) xb64[lane + 64 * h] = c0[h];
-    sync();
+    wsync();
     if (!active) return;
     uint64_t *out = a.lwe_out + (size_t)ct * (K * N + 1);
     if (wave < K) {
