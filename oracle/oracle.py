@@ -71,6 +71,9 @@ def lib():
                                     ctypes.c_int]
         L.orc_keyswitch_batch.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, u64p, u64p, ctypes.c_size_t]
+        L.orc_mono_spectrum.argtypes = [ctypes.c_int, ctypes.c_uint32, f64p]
+        L.orc_fft_forward_integer.argtypes = [ctypes.c_int, u64p, f64p]
+        L.orc_pos_freq.argtypes = [ctypes.c_int, ctypes.c_int]
         if hasattr(L, "orc_mb_pbs_batch"):
             L.orc_mb_fbsk_create.restype = ctypes.c_void_p
             L.orc_mb_fbsk_create.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -219,6 +222,62 @@ class FourierBsk:
             idx = np.ascontiguousarray(lut_idx, dtype=np.uint32)
         lib().orc_pbs_batch(self.h, _p(lwe_in), _p(out), _p(luts),
                             idx.ctypes.data_as(u32p) if idx is not None else None, cnt, threads)
+        return out
+
+
+def mono_spectrum(N: int, d: int) -> np.ndarray:
+    """Closed-form spectrum of X^d in FFT position order (multi-bit keybundle monomials)."""
+    out = np.zeros(N // 2, dtype=np.complex128)
+    assert lib().orc_mono_spectrum(N, d, out.ctypes.data_as(f64p)) == 0
+    return out
+
+
+def fft_forward_integer(x) -> np.ndarray:
+    x = _u64(x)
+    out = np.zeros(x.size // 2, dtype=np.complex128)
+    assert lib().orc_fft_forward_integer(x.size, _p(x), out.ctypes.data_as(f64p)) == 0
+    return out
+
+
+def pos_freq(N: int) -> np.ndarray:
+    return np.array([lib().orc_pos_freq(N, P) for P in range(N // 2)], dtype=np.int64)
+
+
+def gen_mb_bsk(seed, lwe_sk, glwe_sk, k, N, base_log, level, g, std, threads=8) -> np.ndarray:
+    """Standard multi-bit BSK [n/g][2^g][L][k+1][k+1][N] (lwe_multi_bit_bootstrap_key_generation.rs)."""
+    lwe_sk, glwe_sk = _u64(lwe_sk), _u64(glwe_sk)
+    n = lwe_sk.size
+    out = np.zeros((n // g) * (1 << g) * level * (k + 1) ** 2 * N, dtype=np.uint64)
+    lib().orc_gen_mb_bsk(seed, _p(lwe_sk), n, _p(glwe_sk), k, N, base_log, level, g, std, _p(out),
+                         threads)
+    return out
+
+
+class MultiBitFourierBsk:
+    """Multi-bit Fourier BSK + deterministic multi-bit PBS
+    (lwe_multi_bit_programmable_bootstrapping.rs:548-828, 1035-1128)."""
+
+    def __init__(self, bsk, n, k, N, base_log, level, g):
+        self.n, self.k, self.N, self.base_log, self.level, self.g = n, k, N, base_log, level, g
+        self._bsk = _u64(bsk)
+        self.h = lib().orc_mb_fbsk_create(_p(self._bsk), n, k, N, base_log, level, g)
+        assert self.h
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_mb_fbsk_destroy(self.h)
+            self.h = None
+
+    def pbs(self, lwe_in, luts, lut_idx=None, threads=8) -> np.ndarray:
+        lwe_in = _u64(lwe_in).reshape(-1, self.n + 1)
+        luts = _u64(luts)
+        cnt = lwe_in.shape[0]
+        out = np.zeros((cnt, self.k * self.N + 1), dtype=np.uint64)
+        idx = None
+        if lut_idx is not None:
+            idx = np.ascontiguousarray(lut_idx, dtype=np.uint32)
+        lib().orc_mb_pbs_batch(self.h, _p(lwe_in), _p(out), _p(luts),
+                               idx.ctypes.data_as(u32p) if idx is not None else None, cnt, threads)
         return out
 
 

@@ -616,19 +616,17 @@ typedef struct {
     int k, N, base_log, level;
     double std;
     uint64_t *bsk;
+    int g;      /* 0: classic BSK; > 0: multi-bit grouping factor */
+    int items;  /* GGSWs to generate */
     int next;
     pthread_mutex_t mu;
 } bsk_job;
 
-/* BSK = GGSW_i(s_i): ggsw_encryption.rs:116-150,300-331; layout [n][L][k+1][k+1][N] */
-static void gen_one_ggsw(bsk_job *J, int i) {
+/* encrypt_constant_ggsw_ciphertext (ggsw_encryption.rs:116-150,300-331) of the plaintext m;
+ * layout [L][k+1][k+1][N], level lvl stored at lvl-1 */
+static void ggsw_encrypt_constant(const bsk_job *J, orc_rng *r, uint64_t *ggsw, uint64_t m) {
     int k = J->k, N = J->N, L = J->level;
     size_t glwe_len = (size_t)(k + 1) * N;
-    size_t ggsw_len = (size_t)L * (k + 1) * glwe_len;
-    uint64_t *ggsw = J->bsk + (size_t)i * ggsw_len;
-    orc_rng r;
-    rng_seed(&r, J->seed, 0x1000000ULL + (uint64_t)i);
-    uint64_t m = J->lwe_sk[i];
     for (int lvl = 1; lvl <= L; lvl++) {
         uint64_t factor = (0 - m) * (1ULL << (64 - J->base_log * lvl));
         for (int row = 0; row <= k; row++) {
@@ -641,9 +639,39 @@ static void gen_one_ggsw(bsk_job *J, int i) {
                 for (int j = 0; j < N; j++) body[j] = 0;
                 body[0] = 0 - factor;
             }
-            glwe_encrypt_assign(&r, g, J->glwe_sk, k, N, J->std);
+            glwe_encrypt_assign(r, g, J->glwe_sk, k, N, J->std);
         }
     }
+}
+
+/* combine_key_bits (lwe_multi_bit_bootstrap_key_generation.rs:401-427): GGSW number `sel` of a
+ * group encrypts prod_i (bit_{g-1-i}(sel) ? s_i : 1 - s_i), so GGSW 0 is the constant term. */
+static uint64_t combine_key_bits(int sel, const uint64_t *key, int g) {
+    uint64_t p = 1;
+    for (int i = 0; i < g; i++) {
+        uint64_t inv = (uint64_t)(((sel >> (g - 1 - i)) & 1) ^ 1);
+        p *= key[i] ^ inv;
+    }
+    return p;
+}
+
+/* classic: BSK = GGSW_i(s_i), [n][L][k+1][k+1][N] (lwe_bootstrap_key_generation.rs);
+ * multi-bit: [n/g][2^g][L][k+1][k+1][N], GGSW (j, sel) = GGSW(combine_key_bits(sel, s_{gj..}))
+ * (lwe_multi_bit_bootstrap_key_generation.rs:87-173).  RNG stream per GGSW. */
+static void gen_one_ggsw(bsk_job *J, int i) {
+    int k = J->k, N = J->N, L = J->level;
+    size_t ggsw_len = (size_t)L * (k + 1) * (k + 1) * N;
+    orc_rng r;
+    uint64_t m;
+    if (J->g == 0) {
+        rng_seed(&r, J->seed, 0x1000000ULL + (uint64_t)i);
+        m = J->lwe_sk[i];
+    } else {
+        int per = 1 << J->g;
+        rng_seed(&r, J->seed, 0x4000000ULL + (uint64_t)i);
+        m = combine_key_bits(i % per, J->lwe_sk + (size_t)(i / per) * J->g, J->g);
+    }
+    ggsw_encrypt_constant(J, &r, J->bsk + (size_t)i * ggsw_len, m);
 }
 
 static void *bsk_worker(void *arg) {
@@ -652,22 +680,32 @@ static void *bsk_worker(void *arg) {
         pthread_mutex_lock(&J->mu);
         int i = J->next++;
         pthread_mutex_unlock(&J->mu);
-        if (i >= J->n) break;
+        if (i >= J->items) break;
         gen_one_ggsw(J, i);
     }
     return NULL;
 }
 
-void orc_gen_bsk(uint64_t seed, const uint64_t *lwe_sk, int n, const uint64_t *glwe_sk, int k, int N,
-                 int base_log, int level, double std, uint64_t *bsk, int threads) {
-    bsk_job J = {seed, lwe_sk, n, glwe_sk, k, N, base_log, level, std, bsk, 0};
-    pthread_mutex_init(&J.mu, NULL);
+static void run_bsk_job(bsk_job *J, int threads) {
+    pthread_mutex_init(&J->mu, NULL);
     if (threads < 1) threads = 1;
     pthread_t th[64];
     if (threads > 64) threads = 64;
-    for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, bsk_worker, &J);
+    for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, bsk_worker, J);
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
-    pthread_mutex_destroy(&J.mu);
+    pthread_mutex_destroy(&J->mu);
+}
+
+void orc_gen_bsk(uint64_t seed, const uint64_t *lwe_sk, int n, const uint64_t *glwe_sk, int k, int N,
+                 int base_log, int level, double std, uint64_t *bsk, int threads) {
+    bsk_job J = {seed, lwe_sk, n, glwe_sk, k, N, base_log, level, std, bsk, 0, n, 0};
+    run_bsk_job(&J, threads);
+}
+
+void orc_gen_mb_bsk(uint64_t seed, const uint64_t *lwe_sk, int n, const uint64_t *glwe_sk, int k, int N,
+                    int base_log, int level, int g, double std, uint64_t *bsk, int threads) {
+    bsk_job J = {seed, lwe_sk, n, glwe_sk, k, N, base_log, level, std, bsk, g, (n / g) << g, 0};
+    run_bsk_job(&J, threads);
 }
 
 static void lwe_encrypt_one(orc_rng *r, const uint64_t *sk, int n, uint64_t pt, double std,
@@ -898,6 +936,204 @@ void orc_pbs_batch(const void *fbsk, const uint64_t *in, uint64_t *out, const ui
     if (threads > 256) threads = 256;
     pthread_t th[256];
     for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, pbs_worker, &J);
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    pthread_mutex_destroy(&J.mu);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Multi-bit PBS, deterministic group order                                               */
+/* (lwe_multi_bit_programmable_bootstrapping.rs:548-828, 18-84; ggsw.rs:699-754).          */
+/* ------------------------------------------------------------------------------------ */
+/* Frequency index of FFT output position P (the DIF butterflies leave the spectrum in
+ * digit-reversed order): P = c0 (M/R0) + c1 (M/(R0 R1)) + ...  ->  f = c0 + R0 c1 + R0 R1 c2 ... */
+static int pos_freq(const orc_fft *f, int P) {
+    int fr = 0, mult = 1, L = f->M;
+    for (int st = 0; st < f->nrad; st++) {
+        int m = L / f->rad[st];
+        fr += mult * (P / m);
+        P %= m;
+        mult *= f->rad[st];
+        L = m;
+    }
+    return fr;
+}
+
+/* Spectrum of the monomial X^d, d in [0, 2N], at frequency fr.  The reference builds it as
+ * factor * fwd_monomial(d mod M) (fft/mod.rs:407-445: unit 1 or i, twist[d mod M], sign of
+ * X^N = -1).  In closed form it is the 2N-th root of unity exp(i pi d (1 - 4 fr) / N) =
+ * i^q twist[r] with t = d (1 - 4 fr) mod 2N, q = t / M, r = t mod M: one table read and exact
+ * sign/swap operations, no rounding. */
+static cplx mono_spectrum(const orc_fft *f, uint32_t d, int fr) {
+    uint32_t t = (d - 4u * d * (uint32_t)fr) & (uint32_t)(2 * f->N - 1);
+    uint32_t q = t / (uint32_t)f->M, r = t % (uint32_t)f->M;
+    cplx w = f->twist[r];
+    switch (q) {
+    case 0: return w;
+    case 1: return (cplx){-w.im, w.re};
+    case 2: return (cplx){-w.re, -w.im};
+    default: return (cplx){w.im, -w.re};
+    }
+}
+
+/* test hooks: the closed form against the transform of X^d */
+int orc_mono_spectrum(int N, uint32_t d, double *out_reim) {
+    orc_fft f;
+    if (fft_init(&f, N)) return -1;
+    for (int P = 0; P < N / 2; P++) ((cplx *)out_reim)[P] = mono_spectrum(&f, d, pos_freq(&f, P));
+    fft_free(&f);
+    return 0;
+}
+int orc_fft_forward_integer(int N, const uint64_t *x, double *out_reim) {
+    orc_fft f;
+    if (fft_init(&f, N)) return -1;
+    forward_integer(&f, x, (cplx *)out_reim);
+    fft_free(&f);
+    return 0;
+}
+int orc_pos_freq(int N, int P) {
+    orc_fft f;
+    if (fft_init(&f, N)) return -1;
+    int r = pos_freq(&f, P);
+    fft_free(&f);
+    return r;
+}
+
+typedef struct {
+    orc_fbsk b;  /* b.fourier: [n/g][2^g][L][k+1][k+1][M] in position order */
+    int g;
+    int *freq;   /* frequency of each position */
+} orc_mb_fbsk;
+
+void *orc_mb_fbsk_create(const uint64_t *bsk, int n, int k, int N, int base_log, int level, int g) {
+    if (g < 1 || n % g) return NULL;
+    orc_mb_fbsk *mb = calloc(1, sizeof(orc_mb_fbsk));
+    orc_fbsk *b = &mb->b;
+    b->n = n;
+    b->k = k;
+    b->N = N;
+    b->base_log = base_log;
+    b->level = level;
+    mb->g = g;
+    if (fft_init(&b->fft, N)) {
+        free(mb);
+        return NULL;
+    }
+    int M = N / 2;
+    size_t npoly = (size_t)(n / g) * (1u << g) * level * (k + 1) * (k + 1);
+    b->fourier = malloc(sizeof(cplx) * npoly * M);
+    for (size_t p = 0; p < npoly; p++) forward_torus(&b->fft, bsk + p * N, b->fourier + p * M);
+    mb->freq = malloc(sizeof(int) * M);
+    for (int P = 0; P < M; P++) mb->freq[P] = pos_freq(&b->fft, P);
+    return mb;
+}
+
+void orc_mb_fbsk_destroy(void *h) {
+    orc_mb_fbsk *mb = h;
+    if (!mb) return;
+    fft_free(&mb->b.fft);
+    free(mb->b.fourier);
+    free(mb->freq);
+    free(mb);
+}
+
+/* keybundle (prepare_multi_bit_ggsw_mem_optimized, :18-84):
+ *   KB = GGSW_0 + sum_{sel=1}^{2^g-1} X^{deg_sel} GGSW_sel,
+ *   deg_sel = modswitch(sum_i bit_{g-1-i}(sel) a_i), accumulated in sel order per element:
+ *   kb.re = fma(g.re, m.re, fma(-g.im, m.im, kb.re)); kb.im = fma(g.re, m.im, fma(g.im, m.re, kb.im))
+ * (update_with_fmadd_factor computes factor*(ggsw*mono) + kb; here the factor is folded into the
+ * exact monomial spectrum, see mono_spectrum). */
+static void mb_keybundle(const orc_mb_fbsk *mb, const cplx *group, const uint64_t *a, cplx *kb, cplx *mono,
+                         int log2N) {
+    const orc_fbsk *b = &mb->b;
+    int g = mb->g, M = b->N / 2;
+    size_t npoly = (size_t)b->level * (b->k + 1) * (b->k + 1);
+    size_t ggsw_len = npoly * M;
+    memcpy(kb, group, sizeof(cplx) * ggsw_len);
+    for (int sel = 1; sel < (1 << g); sel++) {
+        uint64_t deg = 0;
+        for (int i = 0; i < g; i++)
+            if ((sel >> (g - 1 - i)) & 1) deg += a[i];
+        uint32_t d = (uint32_t)orc_pbs_modulus_switch(deg, log2N);
+        for (int P = 0; P < M; P++) mono[P] = mono_spectrum(&b->fft, d, mb->freq[P]);
+        const cplx *G = group + (size_t)sel * ggsw_len;
+        for (size_t q = 0; q < npoly; q++) {
+            for (int P = 0; P < M; P++) {
+                cplx gg = G[q * M + P], m = mono[P], *o = &kb[q * M + P];
+                o->re = fma(gg.re, m.re, fma(-gg.im, m.im, o->re));
+                o->im = fma(gg.re, m.im, fma(gg.im, m.re, o->im));
+            }
+        }
+    }
+}
+
+/* multi_bit_programmable_bootstrap_lwe_ciphertext (:1035-1128) with the deterministic blind
+ * rotation (:548-828): acc = LUT / X^{b~}; for each group j in order: acc <- ExtProd(KB_j, acc)
+ * into a zeroed GLWE (ping-pong buffers, :782-800); sample extract at degree 0. */
+static void mb_pbs_one(const orc_mb_fbsk *mb, const uint64_t *lwe_in, uint64_t *lwe_out, const uint64_t *lut,
+                       uint64_t *acc, uint64_t *tmp, cplx *kb, cplx *mono, pbs_scratch *s) {
+    const orc_fbsk *b = &mb->b;
+    int n = b->n, k = b->k, N = b->N, M = N / 2, g = mb->g;
+    int log2N = 0;
+    while ((1 << log2N) < N) log2N++;
+    size_t ggsw_len = (size_t)b->level * (k + 1) * (k + 1) * M;
+    size_t gl = (size_t)(k + 1) * N;
+    uint64_t bt = orc_pbs_modulus_switch(lwe_in[n], log2N);
+    for (int p = 0; p <= k; p++) monomial_div(acc + (size_t)p * N, lut + (size_t)p * N, N, bt);
+    for (int j = 0; j < n / g; j++) {
+        mb_keybundle(mb, b->fourier + (size_t)j * ((size_t)1 << g) * ggsw_len, lwe_in + (size_t)j * g, kb,
+                     mono, log2N);
+        memset(tmp, 0, sizeof(uint64_t) * gl);
+        external_product_add(b, kb, tmp, acc, s);
+        memcpy(acc, tmp, sizeof(uint64_t) * gl);
+    }
+    sample_extract0(acc, lwe_out, k, N);
+}
+
+typedef struct {
+    const orc_mb_fbsk *mb;
+    const uint64_t *in, *luts;
+    const uint32_t *lut_idx;
+    uint64_t *out;
+    size_t count;
+    size_t next;
+    pthread_mutex_t mu;
+} mb_pbs_job;
+
+static void *mb_pbs_worker(void *arg) {
+    mb_pbs_job *J = arg;
+    const orc_fbsk *b = &J->mb->b;
+    int k = b->k, N = b->N, M = N / 2;
+    pbs_scratch s;
+    scratch_alloc(&s, k, N);
+    size_t gl = (size_t)(k + 1) * N;
+    uint64_t *acc = malloc(sizeof(uint64_t) * gl), *tmp = malloc(sizeof(uint64_t) * gl);
+    cplx *kb = malloc(sizeof(cplx) * (size_t)b->level * (k + 1) * (k + 1) * M);
+    cplx *mono = malloc(sizeof(cplx) * M);
+    for (;;) {
+        pthread_mutex_lock(&J->mu);
+        size_t c = J->next++;
+        pthread_mutex_unlock(&J->mu);
+        if (c >= J->count) break;
+        size_t li = J->lut_idx ? J->lut_idx[c] : 0;
+        mb_pbs_one(J->mb, J->in + c * (size_t)(b->n + 1), J->out + c * (size_t)(k * N + 1),
+                   J->luts + li * gl, acc, tmp, kb, mono, &s);
+    }
+    free(acc);
+    free(tmp);
+    free(kb);
+    free(mono);
+    scratch_free(&s);
+    return NULL;
+}
+
+void orc_mb_pbs_batch(const void *h, const uint64_t *in, uint64_t *out, const uint64_t *luts,
+                      const uint32_t *lut_idx, size_t count, int threads) {
+    mb_pbs_job J = {h, in, luts, lut_idx, out, count, 0};
+    pthread_mutex_init(&J.mu, NULL);
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, mb_pbs_worker, &J);
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
     pthread_mutex_destroy(&J.mu);
 }

@@ -45,10 +45,18 @@ class KeySet:
         self.seed = seed
         self.lwe_sk = O.binary_key(seed, 1, p.lwe_dimension)
         self.glwe_sk = O.binary_key(seed, 2, p.glwe_dimension * p.polynomial_size)
-        self.bsk = O.gen_bsk(seed, self.lwe_sk, self.glwe_sk, p.glwe_dimension, p.polynomial_size,
-                             p.pbs_base_log, p.pbs_level, p.glwe_modular_std_dev, threads=8)
-        self.fbsk = O.FourierBsk(self.bsk, p.lwe_dimension, p.glwe_dimension, p.polynomial_size,
-                                 p.pbs_base_log, p.pbs_level)
+        if p.grouping_factor:
+            self.bsk = O.gen_mb_bsk(seed, self.lwe_sk, self.glwe_sk, p.glwe_dimension, p.polynomial_size,
+                                    p.pbs_base_log, p.pbs_level, p.grouping_factor,
+                                    p.glwe_modular_std_dev, threads=8)
+            self.fbsk = O.MultiBitFourierBsk(self.bsk, p.lwe_dimension, p.glwe_dimension,
+                                             p.polynomial_size, p.pbs_base_log, p.pbs_level,
+                                             p.grouping_factor)
+        else:
+            self.bsk = O.gen_bsk(seed, self.lwe_sk, self.glwe_sk, p.glwe_dimension, p.polynomial_size,
+                                 p.pbs_base_log, p.pbs_level, p.glwe_modular_std_dev, threads=8)
+            self.fbsk = O.FourierBsk(self.bsk, p.lwe_dimension, p.glwe_dimension, p.polynomial_size,
+                                     p.pbs_base_log, p.pbs_level)
         self._ksk = None
         self._O = O
 
@@ -78,6 +86,13 @@ def keys_manticore(orc):
     from tfhe_mi355.parameters import MANTICORE_PARAMETERS
 
     return KeySet(orc, MANTICORE_PARAMETERS, seed=11)
+
+
+@pytest.fixture(scope="session")
+def keys_mb(orc):
+    from tfhe_mi355.parameters import PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS
+
+    return KeySet(orc, PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS, seed=5)
 
 
 def decode(pts, delta):

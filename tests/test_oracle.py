@@ -133,6 +133,52 @@ def test_oracle_pbs_round_trip_manticore(orc, keys_manticore):
     assert np.array_equal(dec, (msgs + 1) % 4)
 
 
+@pytest.mark.parametrize("N", [1024, 2048, 32768])
+def test_position_frequency_map(orc, N):
+    """FFT output position P holds frequency pos_freq(P): the transform of e_1 is W^f(P)."""
+    M = N // 2
+    f = orc.pos_freq(N)
+    assert np.array_equal(np.sort(f), np.arange(M))
+    z = np.zeros(M, dtype=np.complex128)
+    z[1] = 1.0
+    out = orc.fft_complex(z)
+    assert np.allclose(out, np.exp(-2j * np.pi * f / M), atol=1e-12)
+
+
+@pytest.mark.parametrize("N", [1024, 2048])
+def test_monomial_spectrum_closed_form(orc, N):
+    """Multi-bit keybundle monomials (incomplete_monomial_forward_as_integer, fft/mod.rs:407-445):
+    the closed form i^q twist[r] equals the transform of X^d for d in [0, 2N]."""
+    M = N // 2
+    ds = [0, 1, 2, 3, M - 1, M, M + 1, N - 1, N, N + 1, N + M, 2 * N - 1, 2 * N]
+    ds += [int(d) for d in np.random.default_rng(N).integers(0, 2 * N + 1, 20)]
+    for d in ds:
+        x = np.zeros(N, dtype=np.uint64)
+        dm = d % (2 * N)
+        if dm < N:
+            x[dm] = 1
+        else:
+            x[dm - N] = np.uint64(2 ** 64 - 1)
+        ref = orc.fft_forward_integer(x)
+        got = orc.mono_spectrum(N, d)
+        assert np.max(np.abs(ref - got)) < 1e-9, d
+        assert np.allclose(np.abs(got), 1.0, atol=1e-15)
+
+
+def test_oracle_multi_bit_pbs_round_trip(orc, keys_mb):
+    """multi_bit_programmable_bootstrap_lwe_ciphertext (lwe_multi_bit_programmable_bootstrapping.rs:
+    1035-1128) at PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS, deterministic group order:
+    decode(decrypt(PBS(ct))) == f(msg) for every message (test/lwe_multi_bit_programmable_bootstrapping.rs)."""
+    p = keys_mb.params
+    delta = (1 << 63) // 16
+    acc = orc.fill_accumulator(p.polynomial_size, p.glwe_dimension, 4, 4, lambda x: (3 * x + 1) % 16)
+    msgs = np.arange(16, dtype=np.uint64)
+    cts = orc.lwe_encrypt(24, keys_mb.lwe_sk, msgs * np.uint64(delta), p.lwe_modular_std_dev)
+    out = keys_mb.fbsk.pbs(cts, acc, threads=8)
+    dec = decode(orc.lwe_decrypt(keys_mb.glwe_sk, out), delta) % 16
+    assert np.array_equal(dec, (3 * msgs + 1) % 16)
+
+
 def test_oracle_keyswitch_round_trip(orc, keys_2_2):
     p = keys_2_2.params
     delta = (1 << 63) // 16
