@@ -33,26 +33,51 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 vector (= matrix) spec, SURVEY.md 8d
 
 
+PARAMS = {  # --params choice -> (parameter set name, workload text, kernel name)
+    "2_2": ("PARAM_MESSAGE_2_CARRY_2_KS_PBS",
+            "BASELINE config 2: batch of 4096 independent classic PBS per GPU, identity LUT",
+            "pbs_classic_kernel<2048,1,1>"),
+    "mb3": ("PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS",
+            "BASELINE config 5: batch of 4096 independent multi-bit (grouping 3) PBS per GPU, identity LUT",
+            "pbs_multibit_kernel<2048,1,1,3>"),
+    "mb2": ("PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS",
+            "batch of 4096 independent multi-bit (grouping 2) PBS per GPU, identity LUT",
+            "pbs_multibit_kernel<2048,1,1,2>"),
+}
+
+
+def ggsw_count(p) -> int:
+    g = p.grouping_factor
+    return (p.lwe_dimension // g) << g if g else p.lwe_dimension
+
+
 def pbs_algorithmic_bytes(p) -> int:
-    """SURVEY.md 8d BSK-streaming model: |BSK_fourier| + 8(n+1) + 8(kN+1) + 8(k+1)N."""
+    """SURVEY.md 8d BSK-streaming model: |BSK_fourier| + 8(n+1) + 8(kN+1) + 8(k+1)N
+    (multi-bit: (n/g) 2^g GGSWs in the BSK)."""
     M = p.polynomial_size // 2
     k1 = p.glwe_dimension + 1
-    fbsk = p.lwe_dimension * p.pbs_level * k1 * k1 * M * 16
+    fbsk = ggsw_count(p) * p.pbs_level * k1 * k1 * M * 16
     return fbsk + 8 * (p.lwe_dimension + 1) + 8 * (p.glwe_dimension * p.polynomial_size + 1) + 8 * k1 * p.polynomial_size
 
 
 def pbs_flops(p) -> float:
-    """per CMUX ((k+1)L + (k+1)) (5 M log2 M + 6 M) + (k+1)^2 L M 8, times n."""
+    """per CMUX ((k+1)L + (k+1)) (5 M log2 M + 6 M) + (k+1)^2 L M 8, times n.
+    Multi-bit: the same external product per group of g, plus the keybundle's (2^g - 1)
+    complex FMAs (8 flop) per GGSW element, times n/g."""
     M = p.polynomial_size // 2
     k1 = p.glwe_dimension + 1
     per = (k1 * p.pbs_level + k1) * (5 * M * math.log2(M) + 6 * M) + k1 * k1 * p.pbs_level * M * 8
+    g = p.grouping_factor
+    if g:
+        per += ((1 << g) - 1) * k1 * k1 * p.pbs_level * M * 8
+        return per * (p.lwe_dimension // g)
     return per * p.lwe_dimension
 
 
-def load_pmc_traffic(batch: int):
+def load_pmc_traffic(batch: int, tag: str):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json,
     FETCH_SIZE doubled per MI355X_MICROARCH.md 'HBM' + WRITE_SIZE), scaled to this batch."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json" if tag == "2_2" else f"pmc_traffic_{tag}.json")
     try:
         d = json.load(open(path))
         return float(d["hbm_bytes_per_pbs"]) * batch
@@ -67,8 +92,12 @@ def cpu_baseline(params, bsk, cts, acc, threads: int):
     from oracle import oracle as O
 
     O.build()
-    fb = O.FourierBsk(bsk, params.lwe_dimension, params.glwe_dimension, params.polynomial_size,
-                      params.pbs_base_log, params.pbs_level)
+    if params.grouping_factor:
+        fb = O.MultiBitFourierBsk(bsk, params.lwe_dimension, params.glwe_dimension, params.polynomial_size,
+                                  params.pbs_base_log, params.pbs_level, params.grouping_factor)
+    else:
+        fb = O.FourierBsk(bsk, params.lwe_dimension, params.glwe_dimension, params.polynomial_size,
+                          params.pbs_base_log, params.pbs_level)
     t = time.perf_counter()
     fb.pbs(cts[:1], acc, threads=1)
     t1 = time.perf_counter() - t
@@ -82,7 +111,7 @@ def cpu_baseline(params, bsk, cts, acc, threads: int):
         "unit": "PBS/s",
         "cores": threads,
         "kind": "port",
-        "sample": (f"{count} PBS of the same PARAM_MESSAGE_2_CARRY_2 batch, oracle C restatement of the "
+        "sample": (f"{count} PBS of the same {params.name} batch, oracle C restatement of the "
                    f"reference fft64 PBS, 1 PBS per thread on {threads} threads ({wall:.1f} s wall); "
                    f"single-thread latency {t1 * 1e3:.1f} ms/PBS (reference published 16.6 ms KS+PBS "
                    f"on Xeon 8375C AVX-512, benchmarks.md:42)"),
@@ -98,6 +127,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--params", choices=sorted(PARAMS), default="2_2",
+                    help="2_2 = the BASELINE metric; mb3/mb2 = multi-bit PBS (config 5)")
     args = ap.parse_args()
 
     import torch
@@ -105,7 +136,10 @@ def main():
 
     from tfhe_mi355 import Engine, client, fill_accumulator
     from tfhe_mi355.distributed import broadcast_u64, env_rank_world
-    from tfhe_mi355.parameters import PARAM_MESSAGE_2_CARRY_2_KS_PBS as P
+    from tfhe_mi355.parameters import ALL
+
+    pname, workload, kname = PARAMS[args.params]
+    P = ALL[pname]
 
     rank, world, local = env_rank_world()
     torch.cuda.set_device(local)
@@ -124,15 +158,21 @@ def main():
     # secret keys: derived from the seed on every rank (cheap); the BSK once on rank 0
     lwe_sk = client.gen_binary_key(args.seed, 1, P.lwe_dimension)
     glwe_sk = client.gen_binary_key(args.seed, 2, P.big_lwe_dimension)
-    bsk_len = P.lwe_dimension * P.pbs_level * (P.glwe_dimension + 1) ** 2 * P.polynomial_size
+    bsk_len = ggsw_count(P) * P.pbs_level * (P.glwe_dimension + 1) ** 2 * P.polynomial_size
     bsk = None
     t_key = time.perf_counter()
     if rank == 0:
-        bsk = client.gen_bootstrap_key(args.seed + 100, lwe_sk, glwe_sk, P.glwe_dimension, P.polynomial_size,
-                                       P.pbs_base_log, P.pbs_level, P.glwe_modular_std_dev)
+        if P.grouping_factor:
+            bsk = client.gen_multi_bit_bootstrap_key(args.seed + 100, lwe_sk, glwe_sk, P.glwe_dimension,
+                                                     P.polynomial_size, P.pbs_base_log, P.pbs_level,
+                                                     P.grouping_factor, P.glwe_modular_std_dev)
+        else:
+            bsk = client.gen_bootstrap_key(args.seed + 100, lwe_sk, glwe_sk, P.glwe_dimension,
+                                           P.polynomial_size, P.pbs_base_log, P.pbs_level,
+                                           P.glwe_modular_std_dev)
     t_gen = time.perf_counter() - t_key
     t_bc = time.perf_counter()
-    d_bsk = broadcast_u64(bsk, bsk_len, 0, device)  # one RCCL broadcast of 48.6 MB
+    d_bsk = broadcast_u64(bsk, bsk_len, 0, device)  # one RCCL broadcast (48.6 MB at 2_2)
     torch.cuda.synchronize()
     t_bc = time.perf_counter() - t_bc
     eng.convert_bootstrap_key_device(d_bsk, bsk_len)
@@ -183,7 +223,8 @@ def main():
         achieved = per_launch_bytes / (kernel_ms * 1e-3) / 1e9
         flops = pbs_flops(P) * B / (kernel_ms * 1e-3) / 1e12
         line = {
-            "metric": "programmable bootstraps/sec (PARAM_MESSAGE_2_CARRY_2) at 1/2/4/8 MI355X",
+            "metric": ("programmable bootstraps/sec (PARAM_MESSAGE_2_CARRY_2) at 1/2/4/8 MI355X"
+                       if args.params == "2_2" else f"programmable bootstraps/sec ({pname}) at 1/2/4/8 MI355X"),
             "value": value,
             "unit": "PBS/s",
             "n_gpus": world,
@@ -196,22 +237,25 @@ def main():
             "dtype": "f64",
             "data": "synthetic (seeded LWE encryptions of uniform 4-bit messages; keys from the engine's client-side keygen)",
             "config": {
-                "workload": "BASELINE config 2: batch of 4096 independent classic PBS per GPU, identity LUT",
-                "parameters": "PARAM_MESSAGE_2_CARRY_2_KS_PBS (n=742, k=1, N=2048, pbs 2^23 x 1)",
+                "workload": workload,
+                "parameters": (f"{pname} (n={P.lwe_dimension}, k={P.glwe_dimension}, N={P.polynomial_size}, "
+                               f"pbs 2^{P.pbs_base_log} x {P.pbs_level}"
+                               + (f", grouping {P.grouping_factor})" if P.grouping_factor else ")")),
                 "batch_per_gpu": B,
                 "global_batch": world * B,
                 "parallelism": f"dp{world} (batch shards, BSK replicated by one RCCL broadcast)",
             },
             "roofline": {
                 "bound": "hbm",
-                "model": "BSK-streaming (SURVEY.md 8d): 48,682,816 B per PBS; frac > 1 would mean reuse beyond streaming",
-                "kernel": "pbs_classic_kernel<2048,1,1>",
+                "model": (f"BSK-streaming (SURVEY.md 8d): {pbs_algorithmic_bytes(P):,} B per PBS; "
+                          "frac > 1 would mean reuse beyond streaming"),
+                "kernel": kname,
                 "kernel_ms": kernel_ms,
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": load_pmc_traffic(B),
+                "traffic": load_pmc_traffic(B, args.params),
                 "fp64": {"achieved": flops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": flops / FP64_PEAK_TFLOPS,
                          "flop_per_pbs": pbs_flops(P)},

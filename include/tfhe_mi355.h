@@ -50,7 +50,7 @@ typedef struct {
     uint32_t ks_level;
     uint32_t message_modulus;
     uint32_t carry_modulus;
-    uint32_t grouping_factor; /* 0 = classic; 2, 3, 4 = multi-bit              */
+    uint32_t grouping_factor; /* 0 = classic; 2, 3 = multi-bit (N=2048, L=1)  */
 } TfheMi355Parameters;
 
 /* Thread-local text of the last failure ("" if none). */
@@ -148,6 +148,11 @@ int tfhe_mi355_client_gen_bootstrap_key(uint64_t seed, const uint64_t *lwe_sk, u
                                         const uint64_t *glwe_sk, uint32_t k, uint32_t N,
                                         uint32_t base_log, uint32_t level, double std_dev,
                                         uint64_t *bsk, uint32_t threads);
+/* multi-bit BSK [n/g][2^g][L][k+1][k+1][N] (lwe_multi_bit_bootstrap_key_generation.rs:87-173) */
+int tfhe_mi355_client_gen_multi_bit_bootstrap_key(uint64_t seed, const uint64_t *lwe_sk, uint32_t n,
+                                                  const uint64_t *glwe_sk, uint32_t k, uint32_t N,
+                                                  uint32_t base_log, uint32_t level, uint32_t grouping_factor,
+                                                  double std_dev, uint64_t *bsk, uint32_t threads);
 int tfhe_mi355_client_gen_keyswitch_key(uint64_t seed, const uint64_t *in_sk, uint32_t in_dim,
                                         const uint64_t *out_sk, uint32_t out_dim, uint32_t base_log,
                                         uint32_t level, double std_dev, uint64_t *ksk);

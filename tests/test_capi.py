@@ -97,3 +97,32 @@ def test_unsupported_parameters_are_rejected(params_2_2):
 
     with pytest.raises(EngineError, match="polynomial_size"):
         Engine(params_2_2.with_(polynomial_size=3000), 0)
+
+
+def test_client_multi_bit_bootstrap_key_is_valid_for_the_oracle(orc):
+    """tfhe_mi355_client_gen_multi_bit_bootstrap_key (combine_key_bits layout) bootstraps
+    correctly through the oracle's multi-bit PBS."""
+    from tfhe_mi355 import client
+    from tfhe_mi355.parameters import PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS as p
+
+    lwe_sk = client.gen_binary_key(7, 1, p.lwe_dimension)
+    glwe_sk = client.gen_binary_key(7, 2, p.big_lwe_dimension)
+    bsk = client.gen_multi_bit_bootstrap_key(7, lwe_sk, glwe_sk, 1, 2048, p.pbs_base_log, 1, 2,
+                                             p.glwe_modular_std_dev, threads=8)
+    assert bsk.size == (p.lwe_dimension // 2) * 4 * 4 * 2048
+    fb = orc.MultiBitFourierBsk(bsk, p.lwe_dimension, 1, 2048, p.pbs_base_log, 1, 2)
+    msgs = np.array([1, 6, 11, 15], dtype=np.uint64)
+    cts = client.lwe_encrypt(9, lwe_sk, msgs * np.uint64(p.delta), p.lwe_modular_std_dev)
+    acc = orc.fill_accumulator(2048, 1, 4, 4, lambda x: (x + 5) % 16)
+    out = fb.pbs(cts, acc, threads=4)
+    assert np.array_equal(decode(client.lwe_decrypt(glwe_sk, out), p.delta) % 16, (msgs + 5) % 16)
+
+
+def test_unsupported_multi_bit_parameters_are_rejected():
+    from tfhe_mi355 import Engine, EngineError
+    from tfhe_mi355.parameters import PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS as mb
+
+    with pytest.raises(EngineError, match="multi-bit"):
+        Engine(mb.with_(grouping_factor=5), 0)
+    with pytest.raises(EngineError, match="multiple of grouping_factor"):
+        Engine(mb.with_(lwe_dimension=889), 0)

@@ -89,11 +89,15 @@ struct TfheMi355Context {
     size_t N() const { return p.polynomial_size; }
     size_t big_dim() const { return k() * N(); }
     size_t glwe_len() const { return (k() + 1) * N(); }
+    // GGSWs in the key: n (classic) or (n/g) 2^g (multi-bit, lwe_multi_bit_bootstrap_key.rs:40-55)
+    size_t ggsw_count() const {
+        return p.grouping_factor ? (n() / p.grouping_factor) << p.grouping_factor : n();
+    }
     size_t std_bsk_len() const {
-        return n() * p.pbs_level * (k() + 1) * (k() + 1) * N();
+        return ggsw_count() * p.pbs_level * (k() + 1) * (k() + 1) * N();
     }
     size_t fourier_bsk_bytes() const {
-        return n() * p.pbs_level * (k() + 1) * (k() + 1) * (N() / 2) * sizeof(double2);
+        return ggsw_count() * p.pbs_level * (k() + 1) * (k() + 1) * (N() / 2) * sizeof(double2);
     }
     size_t ksk_len() const { return big_dim() * p.ks_level * (n() + 1); }
 };
@@ -137,6 +141,22 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
     require_fbsk(c);
     if (lut_count == 0) fail("lut_count must be >= 1");
     if (count > 0x7fffffff) fail("batch too large");
+    if (c->p.grouping_factor) {
+        MultiBitPbsLaunch a;
+        a.lwe_in = d_in;
+        a.lwe_out = d_out;
+        a.luts = d_luts;
+        a.lut_indexes = d_idx;
+        a.fbsk = reinterpret_cast<const double2 *>(c->fbsk.ptr);
+        a.W = c->tables.W;
+        a.twist = c->tables.twist;
+        a.n = (int)c->n();
+        a.base_log = (int)c->p.pbs_base_log;
+        a.count = (int)count;
+        check(launch_multibit_pbs((int)c->N(), (int)c->k(), (int)c->p.pbs_level, (int)c->p.grouping_factor, a, s),
+              "launch multi-bit pbs");
+        return;
+    }
     ClassicPbsLaunch a;
     a.lwe_in = d_in;
     a.lwe_out = d_out;
@@ -195,9 +215,16 @@ int tfhe_mi355_context_create(const TfheMi355Parameters *params, int device, Tfh
         if (!params) fail("null params");
         const TfheMi355Parameters &p = *params;
         if (!is_pow2(p.polynomial_size)) fail("polynomial_size must be a power of two");
-        if (p.grouping_factor != 0) fail("multi-bit PBS (grouping_factor %u) is not available in this build", p.grouping_factor);
-        if (!classic_pbs_supported((int)p.polynomial_size, (int)p.glwe_dimension, (int)p.pbs_level))
+        if (p.grouping_factor != 0) {
+            if (!multibit_pbs_supported((int)p.polynomial_size, (int)p.glwe_dimension, (int)p.pbs_level,
+                                        (int)p.grouping_factor))
+                fail("no multi-bit kernel for N=%u k=%u pbs_level=%u grouping_factor=%u", p.polynomial_size,
+                     p.glwe_dimension, p.pbs_level, p.grouping_factor);
+            if (p.lwe_dimension % p.grouping_factor)
+                fail("lwe_dimension %u is not a multiple of grouping_factor %u", p.lwe_dimension, p.grouping_factor);
+        } else if (!classic_pbs_supported((int)p.polynomial_size, (int)p.glwe_dimension, (int)p.pbs_level)) {
             fail("no kernel for N=%u k=%u pbs_level=%u", p.polynomial_size, p.glwe_dimension, p.pbs_level);
+        }
         if (p.pbs_base_log < 2 || p.pbs_base_log * p.pbs_level > 30)
             fail("pbs decomposition base_log*level must be in [2, 30] (got %u x %u)", p.pbs_base_log, p.pbs_level);
         if (p.ks_level && (p.ks_base_log == 0 || p.ks_base_log * p.ks_level >= 64)) fail("invalid ks decomposition");

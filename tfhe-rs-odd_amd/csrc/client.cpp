@@ -109,41 +109,78 @@ int tfhe_mi355_client_gen_binary_key(uint64_t seed, uint64_t stream, uint64_t *k
     });
 }
 
+}  // extern "C"
+
+namespace {
+// GGSW list generation shared by the classic and multi-bit keys: GGSW i encrypts the constant
+// plaintext msg(i) (ggsw_encryption.rs:116-150,300-331), with its own RNG stream.
+template <class Msg>
+void gen_ggsw_list(uint64_t seed, uint64_t stream_base, uint32_t items, const uint64_t *glwe_sk, uint32_t k,
+                   uint32_t N, uint32_t base_log, uint32_t level, double std, uint64_t *out, uint32_t threads,
+                   Msg msg) {
+    const size_t glwe_len = (size_t)(k + 1) * N, ggsw_len = (size_t)level * (k + 1) * glwe_len;
+    std::atomic<uint32_t> next{0};
+    auto work = [&] {
+        for (;;) {
+            uint32_t i = next++;
+            if (i >= items) break;
+            Rng r(seed, stream_base + i);
+            const uint64_t m = msg(i);
+            uint64_t *ggsw = out + (size_t)i * ggsw_len;
+            for (uint32_t lvl = 1; lvl <= level; lvl++) {
+                uint64_t factor = (0 - m) * (1ULL << (64 - base_log * lvl));
+                for (uint32_t row = 0; row <= k; row++) {
+                    uint64_t *g = ggsw + ((size_t)(lvl - 1) * (k + 1) + row) * glwe_len;
+                    uint64_t *body = g + (size_t)k * N;
+                    if (row < k) {
+                        for (uint32_t j = 0; j < N; j++) body[j] = glwe_sk[(size_t)row * N + j] * factor;
+                    } else {
+                        std::memset(body, 0, sizeof(uint64_t) * N);
+                        body[0] = 0 - factor;
+                    }
+                    glwe_encrypt_assign(r, g, glwe_sk, (int)k, (int)N, std);
+                }
+            }
+        }
+    };
+    uint32_t nt = threads ? threads : std::max(1u, std::thread::hardware_concurrency());
+    std::vector<std::thread> th;
+    for (uint32_t t = 1; t < nt; t++) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+}
+}  // namespace
+
+extern "C" {
+
 int tfhe_mi355_client_gen_bootstrap_key(uint64_t seed, const uint64_t *lwe_sk, uint32_t n,
                                         const uint64_t *glwe_sk, uint32_t k, uint32_t N, uint32_t base_log,
                                         uint32_t level, double std, uint64_t *bsk, uint32_t threads) {
     return guard([&] {
         if (!lwe_sk || !glwe_sk || !bsk) throw std::invalid_argument("null argument");
-        const size_t glwe_len = (size_t)(k + 1) * N, ggsw_len = (size_t)level * (k + 1) * glwe_len;
-        std::atomic<uint32_t> next{0};
-        auto work = [&] {
-            for (;;) {
-                uint32_t i = next++;
-                if (i >= n) break;
-                Rng r(seed, 0x1000000ULL + i);
-                uint64_t m = lwe_sk[i];
-                uint64_t *ggsw = bsk + (size_t)i * ggsw_len;
-                for (uint32_t lvl = 1; lvl <= level; lvl++) {
-                    uint64_t factor = (0 - m) * (1ULL << (64 - base_log * lvl));
-                    for (uint32_t row = 0; row <= k; row++) {
-                        uint64_t *g = ggsw + ((size_t)(lvl - 1) * (k + 1) + row) * glwe_len;
-                        uint64_t *body = g + (size_t)k * N;
-                        if (row < k) {
-                            for (uint32_t j = 0; j < N; j++) body[j] = glwe_sk[(size_t)row * N + j] * factor;
-                        } else {
-                            std::memset(body, 0, sizeof(uint64_t) * N);
-                            body[0] = 0 - factor;
-                        }
-                        glwe_encrypt_assign(r, g, glwe_sk, (int)k, (int)N, std);
-                    }
-                }
-            }
-        };
-        uint32_t nt = threads ? threads : std::max(1u, std::thread::hardware_concurrency());
-        std::vector<std::thread> th;
-        for (uint32_t t = 1; t < nt; t++) th.emplace_back(work);
-        work();
-        for (auto &t : th) t.join();
+        gen_ggsw_list(seed, 0x1000000ULL, n, glwe_sk, k, N, base_log, level, std, bsk, threads,
+                      [&](uint32_t i) { return lwe_sk[i]; });
+    });
+}
+
+// [n/g][2^g][L][k+1][k+1][N]; GGSW (j, sel) encrypts combine_key_bits(sel, s_{gj..gj+g-1})
+// (lwe_multi_bit_bootstrap_key_generation.rs:87-173, 401-427)
+int tfhe_mi355_client_gen_multi_bit_bootstrap_key(uint64_t seed, const uint64_t *lwe_sk, uint32_t n,
+                                                  const uint64_t *glwe_sk, uint32_t k, uint32_t N,
+                                                  uint32_t base_log, uint32_t level, uint32_t grouping_factor,
+                                                  double std, uint64_t *bsk, uint32_t threads) {
+    return guard([&] {
+        if (!lwe_sk || !glwe_sk || !bsk) throw std::invalid_argument("null argument");
+        const uint32_t g = grouping_factor;
+        if (g == 0 || g > 6 || n % g) throw std::invalid_argument("invalid grouping factor");
+        gen_ggsw_list(seed, 0x4000000ULL, (n / g) << g, glwe_sk, k, N, base_log, level, std, bsk, threads,
+                      [&](uint32_t i) {
+                          const uint32_t sel = i & ((1u << g) - 1);
+                          const uint64_t *key = lwe_sk + (size_t)(i >> g) * g;
+                          uint64_t p = 1;
+                          for (uint32_t b = 0; b < g; b++) p *= key[b] ^ (uint64_t)(((sel >> (g - 1 - b)) & 1) ^ 1);
+                          return p;
+                      });
     });
 }
 

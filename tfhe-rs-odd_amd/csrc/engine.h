@@ -30,6 +30,20 @@ struct ClassicPbsLaunch {
 bool classic_pbs_supported(int N, int k, int L);
 hipError_t launch_classic_pbs(int N, int k, int L, const ClassicPbsLaunch &a, hipStream_t s);
 
+struct MultiBitPbsLaunch {
+    const uint64_t *lwe_in;      // [count][n+1]
+    uint64_t *lwe_out;           // [count][k*N+1]
+    const uint64_t *luts;        // [lut_count][(k+1)*N]
+    const uint32_t *lut_indexes; // [count] or null
+    const double2 *fbsk;         // [n/g][2^g][L][k+1][k+1] polys, engine Fourier layout
+    const double2 *W, *twist;
+    int n;
+    int base_log;
+    int count;
+};
+bool multibit_pbs_supported(int N, int k, int L, int g);
+hipError_t launch_multibit_pbs(int N, int k, int L, int g, const MultiBitPbsLaunch &a, hipStream_t s);
+
 // standard BSK polys (npoly x N u64) -> Fourier (npoly x M double2, engine layout)
 hipError_t launch_bsk_to_fourier(int N, const uint64_t *std_polys, double2 *fourier, size_t npoly,
                                  const FftTables &t, hipStream_t s);

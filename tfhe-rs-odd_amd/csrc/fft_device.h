@@ -297,6 +297,11 @@ struct WaveFft<1024> {
     static constexpr int V = 16;
     static constexpr int XL = xbuf_len_1024();  // exchange buffer entries
     using Lds = LdsTwiddles<16, 16, 4>;
+    // Spectrum element (slot s, lane) sits at FFT position P = 64 (lane & 15) + 16 (lane >> 4) + s;
+    // the DIF output is digit reversed (P = 64 c0 + 4 c1 + c2 -> f = c0 + 16 c1 + 256 c2), so its
+    // frequency is freq_lane(lane) + freq_slot(s) (oracle pos_freq).
+    __device__ __forceinline__ static uint32_t freq_lane(int lane) { return (lane & 15) + 64 * (lane >> 4); }
+    static constexpr uint32_t freq_slot(int s) { return 16 * (s >> 2) + 256 * (s & 3); }
 
     template <class TW, class Sync>
     __device__ __forceinline__ static void forward(cx *v, cx *xb, const TW &tw, int lane, Sync sync) {

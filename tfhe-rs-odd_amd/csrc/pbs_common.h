@@ -1,0 +1,82 @@
+// pbs_common.h -- device helpers shared by the classic and multi-bit PBS kernels.
+#pragma once
+#include "fft_device.h"
+
+#ifndef PBS_WAVE_LOCAL
+#define PBS_WAVE_LOCAL 1
+#endif
+#ifndef PBS_WAVES_PER_EU
+#define PBS_WAVES_PER_EU 1
+#endif
+
+namespace tfhe_mi355 {
+
+template <int LOG2N>
+__device__ __forceinline__ uint32_t pbs_modulus_switch(uint64_t x) {
+    uint64_t o = x >> (64 - LOG2N - 2);
+    o += 1;
+    o >>= 1;
+    return (uint32_t)o;  // in [0, 2N]
+}
+
+constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x / 2); }
+
+struct BlockSync {
+    __device__ __forceinline__ void operator()() const { __syncthreads(); }
+};
+// Orders LDS accesses among the lanes of ONE wavefront: LDS executes a wave's ds_* operations
+// in issue order, so a compiler-level fence at wavefront scope is all a wave-private buffer
+// (rotation, FFT exchanges) needs -- no s_barrier across the workgroup.
+struct WaveLocalSync {
+    __device__ __forceinline__ void operator()() const {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+};
+
+// digit extraction in 32-bit registers: valid when base_log * level <= 30 (all supported
+// parameter sets).  Bit-identical digits to the 64-bit SignedDecomposer (decomposer.rs:99-119,
+// iter.rs:134-141): the only divergence is the discarded final state when the rounding
+// overflows, where every digit is 0 in both.
+template <int L>
+__device__ __forceinline__ uint32_t decomp_state32(uint64_t x, int beta) {
+    const int shift = 63 - beta * L;  // >= 33
+    uint32_t s = (uint32_t)((x >> 32) >> (shift - 32));
+    return (s + 1) >> 1;
+}
+template <int L>
+__device__ __forceinline__ uint32_t decomp_state32_hi(uint32_t x_hi, int beta) {
+    const int shift = 63 - beta * L;  // >= 33
+    return ((x_hi >> (shift - 32)) + 1) >> 1;
+}
+// L = 1: s = ((x >> (63 - beta)) + 1) >> 1, digit = s mod 2^beta balanced into
+// (-2^(beta-1), 2^(beta-1)] -- the SignedDecomposer's carry rule for one level, since the
+// state left after the level is 0 or 1 and only 1 when the digit is 0.
+// With c = 2^beta - 1 and h = 2^(beta-1) - 1:  digit = bfe(a + c, 1, beta) - h, a = x_hi >> (31 - beta).
+__device__ __forceinline__ int32_t digit_l1(uint32_t x_hi, int k, uint32_t c, int beta, int32_t h) {
+    return (int32_t)__builtin_amdgcn_ubfe((x_hi >> k) + c, 1, beta) - h;
+}
+__device__ __forceinline__ int32_t decomp_digit32(uint32_t &state, int beta, uint32_t mask) {
+    uint32_t res = state & mask;
+    state >>= beta;
+    uint32_t carry = ((res - 1) | state) & res;
+    carry >>= beta - 1;
+    state += carry;
+    return (int32_t)(res - (carry << beta));
+}
+
+template <int M>
+struct PbsLds {
+    using Fft = WaveFft<M>;
+    using Tw = typename Fft::Lds;
+    static constexpr int XL = Fft::XL;
+    // layout (double2 units): [twist M][s1 table][s2 table][exchange: one XL buffer per wave]
+    static constexpr int twist_off = 0;
+    static constexpr int s1_off = M;
+    static constexpr int s2_off = s1_off + Tw::s1_len;
+    static constexpr int xbuf_off = ((s2_off + Tw::s2_len + 3) / 4) * 4;
+    static constexpr size_t bytes(int waves) { return sizeof(double2) * (size_t)(xbuf_off + waves * XL); }
+};
+
+}  // namespace tfhe_mi355

@@ -1,0 +1,255 @@
+// pbs_multibit.hip -- batched multi-bit programmable bootstrap on gfx950.
+//
+// Replaces (reference tfhe-rs-odd, CPU Rust):
+//   multi_bit_programmable_bootstrap_lwe_ciphertext    lwe_multi_bit_programmable_bootstrapping.rs:1035-1128
+//   multi_bit_deterministic_blind_rotate_assign        same file :548-828 (group order 0..n/g-1)
+//   prepare_multi_bit_ggsw_mem_optimized (keybundle)   same file :18-84
+//   update_with_fmadd_factor                           fft64/crypto/ggsw.rs:699-754
+//   incomplete_monomial_forward_as_integer             fft64/math/fft/mod.rs:407-445
+//   add_external_product_assign                        fft64/crypto/ggsw.rs:477-598
+//
+// Design (DESIGN.md "Kernels"): the classic kernel's shape -- one workgroup per ciphertext, one
+// wavefront per GLWE polynomial, accumulator in registers -- with the CMUX replaced by the
+// multi-bit step  acc <- ExtProd(KB_j, acc),  KB_j = sum_sel X^{deg_sel} GGSW_{j,sel}.
+// The keybundle is never materialised: wave c builds KB_j[lvl][r][c] for its column frequency
+// by frequency in registers while it streams the 2^g GGSW columns, and immediately contracts it
+// with the published row spectra.  The monomial spectra are 2N-th roots of unity read from the
+// twist table in LDS (exact sign/swap, no rounding; oracle mono_spectrum), so the keybundle
+// costs 2^g - 1 complex FMAs per GGSW element and one LDS read per (monomial, frequency).
+// No rotation is needed (ct1 = acc), and the backward transform overwrites the accumulator
+// (the reference's zeroed ping-pong destination, :782-800).
+#include "engine.h"
+#include "pbs_common.h"
+
+namespace tfhe_mi355 {
+
+template <int N, int K, int L, int G>
+__global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU)
+    pbs_multibit_kernel(MultiBitPbsLaunch a) {
+    constexpr int M = N / 2;
+    constexpr int V = M / 64;
+    constexpr int LOG2N = ilog2(N);
+    constexpr int LOG2M = LOG2N - 1;
+    constexpr int NSEL = 1 << G;
+    using Fft = WaveFft<M>;
+    using Lay = PbsLds<M>;
+    constexpr int XL = Lay::XL;
+    static_assert(sizeof(cx) * XL >= sizeof(uint64_t) * N, "exchange buffer holds one polynomial");
+
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double2 *lds = reinterpret_cast<double2 *>(smem);
+    const double2 *s_twist = lds + Lay::twist_off;
+
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // polynomial / column
+    const int lane0 = threadIdx.x & 63;
+    int lane = lane0;
+    const int ct = blockIdx.x;
+    const int n = a.n;
+    const int beta = a.base_log;
+    const uint32_t dmask = (1u << beta) - 1;
+    const int dk1 = 31 - beta;
+    const uint32_t dc1 = dmask;
+    const int32_t dh1 = (int32_t)(1u << (beta - 1)) - 1;
+    const double norm = 1.0 / (double)M;
+    BlockSync sync;
+    WaveLocalSync wsync;
+
+    for (int e = threadIdx.x; e < M; e += blockDim.x) lds[Lay::twist_off + e] = a.twist[e];
+    Fft::Lds::template fill<M>(lds + Lay::s1_off, lds + Lay::s2_off, a.W, threadIdx.x, blockDim.x);
+    const typename Fft::Lds tw{lds + Lay::s1_off, lds + Lay::s2_off};
+    sync();
+
+    cx *xct = reinterpret_cast<cx *>(lds + Lay::xbuf_off);
+    cx *xb = xct + wave * XL;
+    uint64_t *xb64 = reinterpret_cast<uint64_t *>(xb);
+    const uint64_t *in = a.lwe_in + (size_t)ct * (n + 1);
+    const uint32_t li = a.lut_indexes ? a.lut_indexes[ct] : 0u;
+    const uint64_t *lut = a.luts + (size_t)li * (K + 1) * N + (size_t)wave * N;
+
+    // acc = LUT / X^{b~}  (:635-650), position lane + 64 h
+    uint64_t c0[2 * V];
+    {
+        const uint32_t bt = pbs_modulus_switch<LOG2N>(in[n]);
+        const int full = bt / N, rem = bt % N;
+#pragma unroll
+        for (int h = 0; h < 2 * V; h++) {
+            const int src = lane + 64 * h + rem;
+            const bool wrap = src >= N;
+            uint64_t v = lut[wrap ? src - N : src];
+            c0[h] = (wrap != (bool)(full & 1)) ? 0 - v : v;
+        }
+    }
+
+    constexpr size_t ggsw_len = (size_t)L * (K + 1) * (K + 1) * M;
+    constexpr size_t lvl_len = (size_t)(K + 1) * (K + 1) * M;
+    const double2 *gcol = a.fbsk + (size_t)wave * M + lane;  // column c = wave, this lane
+    const int groups = n / G;
+
+    for (int j = 0; j < groups; j++) {
+        int lane = lane0;
+        asm volatile("" : "+v"(lane));
+        // monomial degrees of the 2^g - 1 non-constant GGSWs (wave-uniform, :700-716)
+        uint32_t d4[NSEL];
+        {
+            uint64_t av[G];
+#pragma unroll
+            for (int i = 0; i < G; i++) av[i] = in[j * G + i];
+#pragma unroll
+            for (int sel = 1; sel < NSEL; sel++) {
+                uint64_t deg = 0;
+#pragma unroll
+                for (int i = 0; i < G; i++)
+                    if ((sel >> (G - 1 - i)) & 1) deg += av[i];
+                d4[sel] = pbs_modulus_switch<LOG2N>(deg);
+            }
+        }
+        // per-lane part of t = d (1 - 4 f) mod 2N with f = freq_lane + freq_slot
+        const uint32_t fl = Fft::freq_lane(lane);
+        uint32_t tb[NSEL];
+#pragma unroll
+        for (int sel = 1; sel < NSEL; sel++) {
+            tb[sel] = d4[sel] - 4u * d4[sel] * fl;
+            d4[sel] *= 4u;
+        }
+        const double2 *grp = gcol + (size_t)j * NSEL * ggsw_len;
+
+        uint32_t st[L > 1 ? 2 * V : 1];
+        if constexpr (L > 1) {
+#pragma unroll
+            for (int h = 0; h < 2 * V; h++) st[h] = decomp_state32_hi<L>((uint32_t)(c0[h] >> 32), beta);
+        }
+
+        cx acc[L > 1 ? V : 1];
+#pragma unroll
+        for (int lvl = L; lvl >= 1; lvl--) {
+            cx v[V];
+#pragma unroll
+            for (int b = 0; b < V; b++) {
+                int32_t d0, d1;
+                if constexpr (L == 1) {
+                    d0 = digit_l1((uint32_t)(c0[b] >> 32), dk1, dc1, beta, dh1);
+                    d1 = digit_l1((uint32_t)(c0[V + b] >> 32), dk1, dc1, beta, dh1);
+                } else {
+                    d0 = decomp_digit32(st[b], beta, dmask);
+                    d1 = decomp_digit32(st[V + b], beta, dmask);
+                }
+                const cx z = {(double)d0, (double)d1};
+                const double2 w = s_twist[lane + 64 * b];
+                v[b] = cmulw(z, w.x, w.y);
+            }
+            Fft::forward(v, xb, tw, lane, wsync);
+            wsync();
+#pragma unroll
+            for (int s = 0; s < V; s++)
+                reinterpret_cast<double2 *>(xb)[s * 64 + lane] = make_double2(v[s].re, v[s].im);
+            sync();
+            const double2 *lm = grp + (size_t)(lvl - 1) * lvl_len;
+#pragma unroll
+            for (int s = 0; s < V; s++) {
+                // Issue window: slot s's GGSW loads and monomial reads take their addresses from
+                // an opaque copy that depends on the result of slot s-2, so at most two slots of
+                // operands are in flight (hoisted all at once they need ~1 KiB/lane and spill).
+                if (s >= 2) {
+                    const double dep = (L > 1) ? acc[L > 1 ? s - 2 : 0].re : v[s - 2].re;
+                    asm volatile("" : "+v"(lm) : "v"(dep));
+#pragma unroll
+                    for (int sel = 1; sel < NSEL; sel++) asm volatile("" : "+v"(tb[sel]) : "v"(dep));
+                }
+                // monomial spectra at this frequency: i^q twist[r], t = q M + r
+                cx mono[NSEL];
+#pragma unroll
+                for (int sel = 1; sel < NSEL; sel++) {
+                    const uint32_t t = (tb[sel] - d4[sel] * Fft::freq_slot(s)) & (uint32_t)(2 * N - 1);
+                    const uint32_t q = t >> LOG2M;
+                    const double2 w = s_twist[t & (uint32_t)(M - 1)];
+                    const bool sw = q & 1;
+                    double re = sw ? w.y : w.x;
+                    double im = sw ? w.x : w.y;
+                    mono[sel].re = (q == 1 || q == 2) ? -re : re;
+                    mono[sel].im = (q & 2) ? -im : im;
+                }
+                cx o = (L > 1 && lvl != L) ? acc[L > 1 ? s : 0] : cx{0.0, 0.0};
+#pragma unroll
+                for (int r = 0; r <= K; r++) {
+                    // KB[lvl][r][c] at this frequency (keybundle, oracle mb_keybundle order)
+                    const double2 *gp = lm + (size_t)r * (K + 1) * M + s * 64;
+                    double2 kb = gp[0];
+#pragma unroll
+                    for (int sel = 1; sel < NSEL; sel++) {
+                        const double2 gg = gp[(size_t)sel * ggsw_len];
+                        kb.x = fma(gg.x, mono[sel].re, fma(-gg.y, mono[sel].im, kb.x));
+                        kb.y = fma(gg.x, mono[sel].im, fma(gg.y, mono[sel].re, kb.y));
+                    }
+                    double2 ff;
+                    if (r == wave) {
+                        ff = make_double2(v[s].re, v[s].im);
+                    } else {
+                        ff = reinterpret_cast<const double2 *>(xct + r * XL)[s * 64 + lane];
+                    }
+                    if (lvl == L && r == 0) {
+                        o.re = fma(kb.x, ff.x, -(kb.y * ff.y));
+                        o.im = fma(kb.x, ff.y, kb.y * ff.x);
+                    } else {
+                        o.re = fma(kb.x, ff.x, fma(-kb.y, ff.y, o.re));
+                        o.im = fma(kb.x, ff.y, fma(kb.y, ff.x, o.im));
+                    }
+                }
+                if constexpr (L > 1) acc[s] = o;
+                else v[s] = o;
+            }
+            sync();  // every wave is done reading the published spectra before xb is reused
+            if constexpr (L == 1) {
+                Fft::inverse(v, xb, tw, lane, wsync);
+#pragma unroll
+                for (int b = 0; b < V; b++) {
+                    const double2 w = s_twist[lane + 64 * b];
+                    backward_convert(v[b], cx{norm * w.x, norm * w.y}, c0[b], c0[V + b]);
+                }
+            }
+        }
+        if constexpr (L > 1) {
+            Fft::inverse(acc, xb, tw, lane, wsync);
+#pragma unroll
+            for (int b = 0; b < V; b++) {
+                const double2 w = s_twist[lane + 64 * b];
+                backward_convert(acc[b], cx{norm * w.x, norm * w.y}, c0[b], c0[V + b]);
+            }
+        }
+    }
+
+    // sample extract at degree 0 (glwe_sample_extraction.rs:91-147)
+    wsync();
+#pragma unroll
+    for (int h = 0; h < 2 * V; h++) xb64[lane + 64 * h] = c0[h];
+    wsync();
+    uint64_t *out = a.lwe_out + (size_t)ct * (K * N + 1);
+    if (wave < K) {
+        for (int j = lane; j < N; j += 64) out[wave * N + j] = j == 0 ? xb64[0] : 0 - xb64[N - j];
+    } else if (lane == 0) {
+        out[K * N] = c0[0];
+    }
+}
+
+template <int N, int K, int L, int G>
+static hipError_t launch_mb_t(const MultiBitPbsLaunch &a, hipStream_t s) {
+    constexpr int M = N / 2;
+    const size_t lds = PbsLds<M>::bytes(K + 1);
+    if (a.count == 0) return hipSuccess;
+    if (a.n % G) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((pbs_multibit_kernel<N, K, L, G>), dim3(a.count), dim3(64 * (K + 1)), lds, s, a);
+    return hipGetLastError();
+}
+
+// The reference's multi-bit parameter sets at N = 2048 (shortint/parameters/multi_bit.rs) all
+// use a single decomposition level; L > 1 is compiled by the template but not instantiated.
+bool multibit_pbs_supported(int N, int k, int L, int g) {
+    return N == 2048 && k == 1 && L == 1 && (g == 2 || g == 3);
+}
+
+hipError_t launch_multibit_pbs(int N, int k, int L, int g, const MultiBitPbsLaunch &a, hipStream_t s) {
+    if (N == 2048 && k == 1 && L == 1 && g == 3) return launch_mb_t<2048, 1, 1, 3>(a, s);
+    if (N == 2048 && k == 1 && L == 1 && g == 2) return launch_mb_t<2048, 1, 1, 2>(a, s);
+    return hipErrorInvalidValue;
+}
+
+}  // namespace tfhe_mi355

@@ -62,6 +62,9 @@ SIGNATURES = [
     ("tfhe_mi355_client_gen_bootstrap_key", ctypes.c_int,
      [ctypes.c_uint64, u64p, ctypes.c_uint32, u64p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
       ctypes.c_uint32, ctypes.c_double, u64p, ctypes.c_uint32]),
+    ("tfhe_mi355_client_gen_multi_bit_bootstrap_key", ctypes.c_int,
+     [ctypes.c_uint64, u64p, ctypes.c_uint32, u64p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double, u64p, ctypes.c_uint32]),
     ("tfhe_mi355_client_gen_keyswitch_key", ctypes.c_int,
      [ctypes.c_uint64, u64p, ctypes.c_uint32, u64p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
       ctypes.c_double, u64p]),

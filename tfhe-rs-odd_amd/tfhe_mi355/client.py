@@ -37,6 +37,20 @@ def gen_bootstrap_key(seed, lwe_sk, glwe_sk, glwe_dimension, polynomial_size, ba
     return bsk
 
 
+def gen_multi_bit_bootstrap_key(seed, lwe_sk, glwe_sk, glwe_dimension, polynomial_size, base_log, level,
+                                grouping_factor, std_dev, threads: int = 0) -> np.ndarray:
+    """[n/g][2^g][L][k+1][k+1][N] (lwe_multi_bit_bootstrap_key_generation.rs:87-173)."""
+    lwe_sk = np.ascontiguousarray(lwe_sk, dtype=np.uint64)
+    glwe_sk = np.ascontiguousarray(glwe_sk, dtype=np.uint64)
+    k, N, g = glwe_dimension, polynomial_size, grouping_factor
+    bsk = np.empty((len(lwe_sk) // g) * (1 << g) * level * (k + 1) * (k + 1) * N, dtype=np.uint64)
+    if threads <= 0:
+        threads = min(16, os.cpu_count() or 1)
+    _lib.call("tfhe_mi355_client_gen_multi_bit_bootstrap_key", seed, _ptr(lwe_sk), len(lwe_sk), _ptr(glwe_sk),
+              k, N, base_log, level, g, std_dev, _ptr(bsk), threads)
+    return bsk
+
+
 def gen_keyswitch_key(seed, in_sk, out_sk, base_log, level, std_dev) -> np.ndarray:
     in_sk = np.ascontiguousarray(in_sk, dtype=np.uint64)
     out_sk = np.ascontiguousarray(out_sk, dtype=np.uint64)

@@ -4,6 +4,7 @@ authoritative -- see SURVEY.md 0.4 for the BASELINE.json annotation mismatch).
   PARAM_MESSAGE_2_CARRY_2_KS_PBS   shortint/parameters/mod.rs:703-717 (alias :1256)
   PARAM_MESSAGE_4_CARRY_4_KS_PBS   shortint/parameters/mod.rs:1063-1077 (alias :1271)
   PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS   shortint/parameters/multi_bit.rs:173-190
+  PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS   shortint/parameters/multi_bit.rs:115-132
   MANTICORE_PARAMETERS (fork)      gadget/parameters/mod.rs:224-235
   TEST_PARAMS_4_BITS_NATIVE_U64    core_crypto/algorithms/test/mod.rs:56-73
 """
@@ -67,6 +68,14 @@ PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS = ClassicPBSParameters(
     message_modulus=4, carry_modulus=4, grouping_factor=3,
     name="PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS")
 
+PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS = ClassicPBSParameters(
+    lwe_dimension=818, glwe_dimension=1, polynomial_size=2048,
+    lwe_modular_std_dev=0.000002226459789930014,
+    glwe_modular_std_dev=0.0000000000000003152931493498455,
+    pbs_base_log=22, pbs_level=1, ks_base_log=5, ks_level=3,
+    message_modulus=4, carry_modulus=4, grouping_factor=2,
+    name="PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS")
+
 # fork: GadgetParameters carry no message/carry moduli; 2 x 2 used here for LUT boxes
 MANTICORE_PARAMETERS = ClassicPBSParameters(
     lwe_dimension=754, glwe_dimension=1, polynomial_size=1024,
@@ -78,4 +87,5 @@ MANTICORE_PARAMETERS = ClassicPBSParameters(
 TEST_PARAMS_4_BITS_NATIVE_U64 = PARAM_MESSAGE_2_CARRY_2_KS_PBS.with_(name="TEST_PARAMS_4_BITS_NATIVE_U64")
 
 ALL = {p.name: p for p in [PARAM_MESSAGE_2_CARRY_2_KS_PBS, PARAM_MESSAGE_4_CARRY_4_KS_PBS,
-                           PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS, MANTICORE_PARAMETERS]}
+                           PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS,
+                           PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS, MANTICORE_PARAMETERS]}

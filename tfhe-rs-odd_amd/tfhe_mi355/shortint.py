@@ -123,9 +123,14 @@ class ServerKey:
         self.engine = engine or Engine(p, device)
         if client_key is not None and bsk is None:
             ck = client_key
-            bsk = client.gen_bootstrap_key(ck.seed * 7 + 3, ck.small_lwe_secret_key, ck.glwe_secret_key,
-                                           p.glwe_dimension, p.polynomial_size, p.pbs_base_log, p.pbs_level,
-                                           p.glwe_modular_std_dev)
+            if p.grouping_factor:
+                bsk = client.gen_multi_bit_bootstrap_key(
+                    ck.seed * 7 + 3, ck.small_lwe_secret_key, ck.glwe_secret_key, p.glwe_dimension,
+                    p.polynomial_size, p.pbs_base_log, p.pbs_level, p.grouping_factor, p.glwe_modular_std_dev)
+            else:
+                bsk = client.gen_bootstrap_key(ck.seed * 7 + 3, ck.small_lwe_secret_key, ck.glwe_secret_key,
+                                               p.glwe_dimension, p.polynomial_size, p.pbs_base_log,
+                                               p.pbs_level, p.glwe_modular_std_dev)
             ksk = client.gen_keyswitch_key(ck.seed * 7 + 4, ck.large_lwe_secret_key, ck.small_lwe_secret_key,
                                            p.ks_base_log, p.ks_level, p.lwe_modular_std_dev)
         if bsk is not None:
