@@ -40,6 +40,9 @@ PARAMS = {  # --params choice -> (parameter set name, workload text, kernel name
     "mb3": ("PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS",
             "BASELINE config 5: batch of 4096 independent multi-bit (grouping 3) PBS per GPU, identity LUT",
             "pbs_multibit_kernel<2048,1,1,3>"),
+    "4_4": ("PARAM_MESSAGE_4_CARRY_4_KS_PBS",
+            "BASELINE config 3: shortint apply_lookup_table (keyswitch -> PBS) at N=32768 per GPU batch",
+            "large_fwd_kernel<1,2> + large_inv_kernel<1,2> (+ keyswitch_kernel)"),
     "mb2": ("PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS",
             "batch of 4096 independent multi-bit (grouping 2) PBS per GPU, identity LUT",
             "pbs_multibit_kernel<2048,1,1,2>"),
@@ -85,11 +88,25 @@ def load_pmc_traffic(batch: int, tag: str):
         return None
 
 
-def cpu_baseline(params, bsk, cts, acc, threads: int):
+def cpu_baseline(params, bsk, cts, acc, threads: int, ksk=None):
     """Oracle (C restatement of the reference fft64 PBS) on the host cores, one PBS per thread,
-    as the reference's pbs_throughput bench (benches/core_crypto/pbs_bench.rs:430-549)."""
+    as the reference's pbs_throughput bench (benches/core_crypto/pbs_bench.rs:430-549).
+    With `ksk` (config 3) each ciphertext is keyswitched first (threads split the batch)."""
     sys.path.insert(0, ROOT)
+    from concurrent.futures import ThreadPoolExecutor
+
     from oracle import oracle as O
+
+    p = params
+
+    def ks(batch):
+        if ksk is None:
+            return batch
+        parts = np.array_split(batch, min(threads, batch.shape[0]))
+        with ThreadPoolExecutor(len(parts)) as ex:
+            outs = list(ex.map(lambda c: O.keyswitch(ksk, p.big_lwe_dimension, p.lwe_dimension, p.ks_base_log,
+                                                     p.ks_level, c), parts))
+        return np.concatenate(outs)
 
     O.build()
     if params.grouping_factor:
@@ -99,22 +116,23 @@ def cpu_baseline(params, bsk, cts, acc, threads: int):
         fb = O.FourierBsk(bsk, params.lwe_dimension, params.glwe_dimension, params.polynomial_size,
                           params.pbs_base_log, params.pbs_level)
     t = time.perf_counter()
-    fb.pbs(cts[:1], acc, threads=1)
+    fb.pbs(ks(cts[:1]), acc, threads=1)
     t1 = time.perf_counter() - t
     count = max(threads, int(round(15.0 / max(t1, 1e-3))))
     count = min(((count + threads - 1) // threads) * threads, cts.shape[0])
     t = time.perf_counter()
-    fb.pbs(cts[:count], acc, threads=threads)
+    fb.pbs(ks(cts[:count]), acc, threads=threads)
     wall = time.perf_counter() - t
     return {
         "value": count / wall,
         "unit": "PBS/s",
         "cores": threads,
         "kind": "port",
-        "sample": (f"{count} PBS of the same {params.name} batch, oracle C restatement of the "
-                   f"reference fft64 PBS, 1 PBS per thread on {threads} threads ({wall:.1f} s wall); "
-                   f"single-thread latency {t1 * 1e3:.1f} ms/PBS (reference published 16.6 ms KS+PBS "
-                   f"on Xeon 8375C AVX-512, benchmarks.md:42)"),
+        "sample": (f"{count} {'KS+' if ksk is not None else ''}PBS of the same {params.name} batch, oracle C "
+                   f"restatement of the reference fft64 PBS, 1 PBS per thread on {threads} threads ({wall:.1f} s wall); "
+                   f"single-thread latency {t1 * 1e3:.1f} ms/PBS (reference published "
+                   f"{'811 ms' if p.polynomial_size == 32768 else '16.6 ms'} KS+PBS at "
+                   f"{'4_4' if p.polynomial_size == 32768 else '2_2'} on Xeon 8375C AVX-512, benchmarks.md:42)"),
     }
 
 
@@ -123,7 +141,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=4096, help="ciphertexts per GPU per step")
+    ap.add_argument("--batch", type=int, default=0, help="ciphertexts per GPU per step (default 4096; 1024 at 4_4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--seed", type=int, default=1)
@@ -153,7 +171,9 @@ def main():
             dist.all_reduce(t)
         torch.cuda.synchronize()
 
-    B = args.batch
+    B = args.batch or (1024 if args.params == "4_4" else 4096)
+    with_ks = args.params == "4_4"   # config 3 is the shortint KS -> PBS
+    msg_space = P.message_modulus * P.carry_modulus
     eng = Engine(P, local)
     # secret keys: derived from the seed on every rank (cheap); the BSK once on rank 0
     lwe_sk = client.gen_binary_key(args.seed, 1, P.lwe_dimension)
@@ -178,18 +198,40 @@ def main():
     eng.convert_bootstrap_key_device(d_bsk, bsk_len)
     torch.cuda.synchronize()
     del d_bsk
+    if with_ks:
+        ksk_len = P.big_lwe_dimension * P.ks_level * (P.lwe_dimension + 1)
+        ksk = None
+        if rank == 0:
+            ksk = client.gen_keyswitch_key(args.seed + 200, glwe_sk, lwe_sk, P.ks_base_log, P.ks_level,
+                                           P.lwe_modular_std_dev)
+        d_ksk = broadcast_u64(ksk, ksk_len, 0, device)
+        eng.upload_keyswitch_key_device(d_ksk, ksk_len)
+        torch.cuda.synchronize()
+        del d_ksk
+    else:
+        ksk = None
 
     rng = np.random.default_rng(args.seed * 1000 + rank)
-    msgs = rng.integers(0, 16, B).astype(np.uint64)
-    cts = client.lwe_encrypt(args.seed * 1000 + rank, lwe_sk, msgs * np.uint64(P.delta), P.lwe_modular_std_dev)
+    msgs = rng.integers(0, msg_space, B).astype(np.uint64)
+    if with_ks:
+        cts = client.lwe_encrypt(args.seed * 1000 + rank, glwe_sk, msgs * np.uint64(P.delta),
+                                 P.glwe_modular_std_dev)
+    else:
+        cts = client.lwe_encrypt(args.seed * 1000 + rank, lwe_sk, msgs * np.uint64(P.delta),
+                                 P.lwe_modular_std_dev)
     acc = fill_accumulator(P, lambda x: x)
     d_in = torch.from_numpy(cts.view(np.int64)).to(device)
     d_out = torch.zeros((B, P.big_lwe_dimension + 1), dtype=torch.int64, device=device)
     d_lut = torch.from_numpy(acc.view(np.int64)).to(device)
     stream = torch.cuda.current_stream()
+    if with_ks:
+        d_scratch = torch.empty(eng.ks_pbs_scratch_bytes(B), dtype=torch.uint8, device=device)
 
     def step():
-        eng.programmable_bootstrap_async(d_in, d_out, d_lut, 1, B, stream=stream)
+        if with_ks:
+            eng.keyswitch_programmable_bootstrap_async(d_in, d_out, d_lut, 1, B, d_scratch, stream=stream)
+        else:
+            eng.programmable_bootstrap_async(d_in, d_out, d_lut, 1, B, stream=stream)
 
     for _ in range(args.warmup):
         step()
@@ -210,7 +252,7 @@ def main():
 
     # correctness of this rank's outputs (decrypt with the big key)
     out = d_out.cpu().numpy().view(np.uint64)
-    dec = client.decode(client.lwe_decrypt(glwe_sk, out), P.delta) % np.uint64(16)
+    dec = client.decode(client.lwe_decrypt(glwe_sk, out), P.delta) % np.uint64(msg_space)
     ok = int(np.count_nonzero(dec == msgs))
     okt = torch.tensor([ok, B], dtype=torch.int64, device=device)
     if world > 1:
@@ -265,7 +307,7 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            line["cpu_baseline"] = cpu_baseline(P, bsk, cts, acc, threads)
+            line["cpu_baseline"] = cpu_baseline(P, bsk, cts, acc, threads, ksk)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

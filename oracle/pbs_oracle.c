@@ -341,6 +341,12 @@ static int radix_plan(int M, int *rad) {
     }
 }
 
+/* cos and sin are called separately through opaque pointers: a compiler may otherwise fuse the
+ * pair into sincos(), whose last bits can differ; the engine builds its tables the same way
+ * (capi.cpp build_tables), so both sides see identical twiddles. */
+static double (*volatile orc_cos)(double) = cos;
+static double (*volatile orc_sin)(double) = sin;
+
 static int fft_init(orc_fft *f, int N) {
     f->N = N;
     f->M = N / 2;
@@ -351,14 +357,14 @@ static int fft_init(orc_fft *f, int N) {
     f->twist = (cplx *)malloc(sizeof(cplx) * M);
     for (int t = 0; t < M; t++) {
         double ang = 2.0 * M_PI * (double)t / (double)M;
-        f->W[t].re = cos(ang);
-        f->W[t].im = -sin(ang);
+        f->W[t].re = orc_cos(ang);
+        f->W[t].im = -orc_sin(ang);
     }
     double unit = M_PI / (2.0 * (double)M);
     for (int j = 0; j < M; j++) {
         double a = (double)j * unit;
-        f->twist[j].re = cos(a);
-        f->twist[j].im = sin(a);
+        f->twist[j].re = orc_cos(a);
+        f->twist[j].im = orc_sin(a);
     }
     return 0;
 }

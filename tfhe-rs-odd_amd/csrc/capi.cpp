@@ -82,6 +82,7 @@ struct TfheMi355Context {
     FftTables tables;
     DeviceBuffer fbsk, ksk, std_staging;
     DeviceBuffer io_in, io_out, io_luts, io_idx, io_tmp;
+    DeviceBuffer pbs_scratch;  // N = 32768: accumulators + spectra of one chunk of ciphertexts
     bool fbsk_ready = false, ksk_ready = false;
 
     size_t n() const { return p.lwe_dimension; }
@@ -104,19 +105,24 @@ struct TfheMi355Context {
 
 namespace {
 
+// cos and sin called separately through opaque pointers (no compiler fusion into sincos, whose
+// last bits can differ): the same tables as the oracle's fft_init, bit for bit.
+double (*volatile host_cos)(double) = static_cast<double (*)(double)>(std::cos);
+double (*volatile host_sin)(double) = static_cast<double (*)(double)>(std::sin);
+
 void build_tables(TfheMi355Context *c) {
     const int N = c->p.polynomial_size, M = N / 2;
     // W[t] = exp(-2 pi i t / M); twist w_j = exp(i pi j / N) as fft/mod.rs:58-69
     std::vector<double2> W(M), tw(M), twi(M);
     for (int t = 0; t < M; t++) {
         double ang = 2.0 * M_PI * (double)t / (double)M;
-        W[t] = make_double2(std::cos(ang), -std::sin(ang));
+        W[t] = make_double2(host_cos(ang), -host_sin(ang));
     }
     double unit = M_PI / (2.0 * (double)M);
     double norm = 1.0 / (double)M;
     for (int j = 0; j < M; j++) {
         double a = (double)j * unit;
-        tw[j] = make_double2(std::cos(a), std::sin(a));
+        tw[j] = make_double2(host_cos(a), host_sin(a));
         twi[j] = make_double2(norm * tw[j].x, norm * tw[j].y);
     }
     size_t bytes = sizeof(double2) * M;
@@ -134,6 +140,12 @@ void require_fbsk(TfheMi355Context *c) {
 }
 void require_ksk(TfheMi355Context *c) {
     if (!c->ksk_ready) fail("keyswitching key not uploaded");
+}
+
+hipError_t convert_bsk(TfheMi355Context *c, const uint64_t *d_std, size_t npoly, hipStream_t s) {
+    if (large_pbs_supported((int)c->N(), (int)c->k(), (int)c->p.pbs_level))
+        return launch_large_bsk_to_fourier(d_std, (double2 *)c->fbsk.ptr, npoly, c->tables, s);
+    return launch_bsk_to_fourier((int)c->N(), d_std, (double2 *)c->fbsk.ptr, npoly, c->tables, s);
 }
 
 void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, const uint64_t *d_luts,
@@ -155,6 +167,26 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
         a.count = (int)count;
         check(launch_multibit_pbs((int)c->N(), (int)c->k(), (int)c->p.pbs_level, (int)c->p.grouping_factor, a, s),
               "launch multi-bit pbs");
+        return;
+    }
+    if (large_pbs_supported((int)c->N(), (int)c->k(), (int)c->p.pbs_level)) {
+        constexpr size_t kChunk = 4096;  // ciphertexts per pass: 6 GiB of scratch at 4_4
+        const size_t per_ct = large_pbs_scratch_per_ct((int)c->N(), (int)c->k(), (int)c->p.pbs_level);
+        c->pbs_scratch.reserve(per_ct * std::max<size_t>(1, std::min(count, kChunk)));
+        LargePbsLaunch a{};
+        a.lwe_in = d_in;
+        a.lwe_out = d_out;
+        a.luts = d_luts;
+        a.lut_indexes = d_idx;
+        a.fbsk = reinterpret_cast<const double2 *>(c->fbsk.ptr);
+        a.W = c->tables.W;
+        a.twist = c->tables.twist;
+        a.n = (int)c->n();
+        a.base_log = (int)c->p.pbs_base_log;
+        a.count = (int)count;
+        a.scratch = c->pbs_scratch.ptr;
+        a.scratch_bytes = c->pbs_scratch.bytes;
+        check(launch_large_pbs((int)c->N(), (int)c->k(), (int)c->p.pbs_level, a, s), "launch large pbs");
         return;
     }
     ClassicPbsLaunch a;
@@ -222,7 +254,8 @@ int tfhe_mi355_context_create(const TfheMi355Parameters *params, int device, Tfh
                      p.glwe_dimension, p.pbs_level, p.grouping_factor);
             if (p.lwe_dimension % p.grouping_factor)
                 fail("lwe_dimension %u is not a multiple of grouping_factor %u", p.lwe_dimension, p.grouping_factor);
-        } else if (!classic_pbs_supported((int)p.polynomial_size, (int)p.glwe_dimension, (int)p.pbs_level)) {
+        } else if (!classic_pbs_supported((int)p.polynomial_size, (int)p.glwe_dimension, (int)p.pbs_level) &&
+                   !large_pbs_supported((int)p.polynomial_size, (int)p.glwe_dimension, (int)p.pbs_level)) {
             fail("no kernel for N=%u k=%u pbs_level=%u", p.polynomial_size, p.glwe_dimension, p.pbs_level);
         }
         if (p.pbs_base_log < 2 || p.pbs_base_log * p.pbs_level > 30)
@@ -250,7 +283,7 @@ int tfhe_mi355_context_destroy(TfheMi355Context *ctx) {
         (void)hipSetDevice(ctx->device);
         if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
         for (DeviceBuffer *b : {&ctx->fbsk, &ctx->ksk, &ctx->std_staging, &ctx->io_in, &ctx->io_out,
-                                &ctx->io_luts, &ctx->io_idx, &ctx->io_tmp})
+                                &ctx->io_luts, &ctx->io_idx, &ctx->io_tmp, &ctx->pbs_scratch})
             b->release();
         if (ctx->tables.W) (void)hipFree(ctx->tables.W);
         if (ctx->tables.twist) (void)hipFree(ctx->tables.twist);
@@ -270,8 +303,7 @@ int tfhe_mi355_bootstrap_key_upload(TfheMi355Context *ctx, const uint64_t *bsk, 
         check(hipMemcpyAsync(ctx->std_staging.ptr, bsk, len * sizeof(uint64_t), hipMemcpyHostToDevice,
                              ctx->stream), "upload bsk");
         ctx->fbsk.reserve(ctx->fourier_bsk_bytes());
-        check(launch_bsk_to_fourier((int)ctx->N(), (const uint64_t *)ctx->std_staging.ptr,
-                                    (double2 *)ctx->fbsk.ptr, len / ctx->N(), ctx->tables, ctx->stream),
+        check(convert_bsk(ctx, (const uint64_t *)ctx->std_staging.ptr, len / ctx->N(), ctx->stream),
               "bsk conversion");
         check(hipStreamSynchronize(ctx->stream), "bsk conversion sync");
         ctx->std_staging.release();
@@ -287,9 +319,7 @@ int tfhe_mi355_bootstrap_key_convert_async(TfheMi355Context *ctx, const uint64_t
         check(hipSetDevice(ctx->device), "hipSetDevice");
         if (len != ctx->std_bsk_len()) fail("bootstrapping key has %zu words, expected %zu", len, ctx->std_bsk_len());
         ctx->fbsk.reserve(ctx->fourier_bsk_bytes());
-        check(launch_bsk_to_fourier((int)ctx->N(), d_bsk, (double2 *)ctx->fbsk.ptr, len / ctx->N(), ctx->tables,
-                                    (hipStream_t)stream),
-              "bsk conversion");
+        check(convert_bsk(ctx, d_bsk, len / ctx->N(), (hipStream_t)stream), "bsk conversion");
         ctx->fbsk_ready = true;
     });
 }

@@ -9,7 +9,11 @@
 // The randomness source is a seeded xoshiro256** (the reference's AES-CTR CSPRNG is not part of
 // the GPU path); keys are deterministic per (seed, index) whatever the thread count.
 #include <cmath>
+#include <complex>
 #include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -73,7 +77,70 @@ int guard(F &&f) {
     }
 }
 
+// Complex radix-2 FFT (host), used for exact negacyclic products at large N.
+struct HostFft {
+    int n;
+    std::vector<std::complex<double>> w, psi;  // w[k] = exp(-2 pi i k / n); psi[j] = exp(i pi j / n)
+    std::vector<int> rev;
+    explicit HostFft(int n_) : n(n_), w(n_ / 2), psi(n_), rev(n_) {
+        for (int k = 0; k < n / 2; k++) w[k] = std::polar(1.0, -2.0 * M_PI * k / n);
+        for (int j = 0; j < n; j++) psi[j] = std::polar(1.0, M_PI * j / n);
+        int lg = 0;
+        while ((1 << lg) < n) lg++;
+        for (int i = 0; i < n; i++) {
+            int r = 0;
+            for (int b = 0; b < lg; b++) r |= ((i >> b) & 1) << (lg - 1 - b);
+            rev[i] = r;
+        }
+    }
+    void run(std::complex<double> *x, bool inverse) const {
+        for (int i = 0; i < n; i++)
+            if (i < rev[i]) std::swap(x[i], x[rev[i]]);
+        for (int len = 2; len <= n; len <<= 1) {
+            const int half = len / 2, step = n / len;
+            for (int i = 0; i < n; i += len)
+                for (int k = 0; k < half; k++) {
+                    std::complex<double> t = inverse ? std::conj(w[k * step]) : w[k * step];
+                    std::complex<double> u = x[i + k], v = x[i + k + half] * t;
+                    x[i + k] = u + v;
+                    x[i + k + half] = u - v;
+                }
+        }
+    }
+};
+
+const HostFft &host_fft(int n) {
+    static std::mutex mu;
+    static std::map<int, std::unique_ptr<HostFft>> cache;
+    std::lock_guard<std::mutex> g(mu);
+    auto &p = cache[n];
+    if (!p) p.reset(new HostFft(n));
+    return *p;
+}
+
+// body += a * s (negacyclic, s binary), exact mod 2^64: four 16-bit limbs of a, each convolved
+// with s in f64 through a psi-weighted FFT (|limb conv| < 2^31, so rounding is exact; checked).
+void negacyclic_binary_add_fft(uint64_t *body, const uint64_t *a, const uint64_t *s, int N) {
+    const HostFft &F = host_fft(N);
+    std::vector<std::complex<double>> S(N), A(N);
+    for (int j = 0; j < N; j++) S[j] = (double)s[j] * F.psi[j];
+    F.run(S.data(), false);
+    for (int limb = 0; limb < 4; limb++) {
+        for (int j = 0; j < N; j++) A[j] = (double)((a[j] >> (16 * limb)) & 0xffff) * F.psi[j];
+        F.run(A.data(), false);
+        for (int j = 0; j < N; j++) A[j] *= S[j];
+        F.run(A.data(), true);
+        for (int j = 0; j < N; j++) {
+            const double v = (A[j] * std::conj(F.psi[j])).real() / N;
+            const double r = std::nearbyint(v);
+            if (std::fabs(v - r) > 0.25) throw std::runtime_error("inexact negacyclic product");
+            body[j] += (uint64_t)(int64_t)r << (16 * limb);
+        }
+    }
+}
+
 void negacyclic_binary_add(uint64_t *body, const uint64_t *a, const uint64_t *s, int N) {
+    if (N >= 4096) return negacyclic_binary_add_fft(body, a, s, N);
     for (int i = 0; i < N; i++) {
         if (!s[i]) continue;
         for (int j = 0; j < i; j++) body[j] -= a[j - i + N];

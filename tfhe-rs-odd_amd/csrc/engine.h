@@ -44,6 +44,28 @@ struct MultiBitPbsLaunch {
 bool multibit_pbs_supported(int N, int k, int L, int g);
 hipError_t launch_multibit_pbs(int N, int k, int L, int g, const MultiBitPbsLaunch &a, hipStream_t s);
 
+// N = 32768 classic PBS: accumulator and spectra in device scratch, two launches per CMUX
+struct LargePbsLaunch {
+    const uint64_t *lwe_in;      // [count][n+1]
+    uint64_t *lwe_out;           // [count][k*N+1]
+    const uint64_t *luts;        // [lut_count][(k+1)*N]
+    const uint32_t *lut_indexes; // [count] or null
+    const double2 *fbsk;         // engine Fourier layout
+    const double2 *W, *twist;
+    int n;
+    int base_log;
+    int count;
+    void *scratch;               // >= large_pbs_scratch_per_ct() bytes per ciphertext of a chunk
+    size_t scratch_bytes;
+    uint64_t *acc;               // set by the launcher
+    double2 *spectra;            // set by the launcher
+};
+bool large_pbs_supported(int N, int k, int L);
+size_t large_pbs_scratch_per_ct(int N, int k, int L);
+hipError_t launch_large_pbs(int N, int k, int L, const LargePbsLaunch &a, hipStream_t s);
+hipError_t launch_large_bsk_to_fourier(const uint64_t *std_polys, double2 *fourier, size_t npoly,
+                                       const FftTables &t, hipStream_t s);
+
 // standard BSK polys (npoly x N u64) -> Fourier (npoly x M double2, engine layout)
 hipError_t launch_bsk_to_fourier(int N, const uint64_t *std_polys, double2 *fourier, size_t npoly,
                                  const FftTables &t, hipStream_t s);

@@ -1,0 +1,361 @@
+// pbs_large.hip -- classic PBS for N = 32768 (PARAM_MESSAGE_4_CARRY_4_KS_PBS: n=996, k=1, L=2,
+// base 2^15) on gfx950.
+//
+// Replaces the same reference functions as pbs_classic.hip (bootstrap.rs:243-380,
+// ggsw.rs:477-697, polynomial_algorithms.rs:219-490, glwe_sample_extraction.rs:91-147,
+// fft/mod.rs:197-557) at the 4_4 shapes.
+//
+// Why a different structure (DESIGN.md "Kernels"): at N = 32768 one ciphertext's accumulator is
+// (k+1) N u64 = 512 KiB and one spectrum M = 16384 c64 = 256 KiB -- neither fits a CU (160 KiB
+// LDS), so the accumulator lives in HBM scratch and each CMUX is two batch-wide launches:
+//   large_fwd  : one workgroup per (ciphertext, row r, level): ct1 = X^{a~} acc_r - acc_r,
+//                decompose, twist, FFT -> spectrum F[ct][lvl][r]   (global)
+//   large_inv  : one workgroup per (ciphertext, column c): sum_{lvl,r} F * GGSW[lvl][r][c],
+//                inverse FFT, acc_c += rounded result                  (global)
+// The M = 16384 FFT is the oracle's [16, 16, 16, 4] DAG: the top radix-16 stage runs across the
+// workgroup (512 threads x 2 butterflies, exchange through LDS in a real and an imaginary pass of
+// 128 KiB each), then each wave runs the 1024-point WaveFft on its two contiguous sub-blocks.
+// Twiddles: top stage W_M[a c] from the global table; sub-blocks W_M[16 x] through the LDS s1
+// table (the oracle's tstride-16 reads of the same table, so bit-identical).
+#include "engine.h"
+#include "pbs_common.h"
+
+namespace tfhe_mi355 {
+
+namespace {
+constexpr int LN = 32768;
+constexpr int LM = LN / 2;
+constexpr int LT = 512;                    // threads per workgroup (8 waves)
+constexpr int LW = LT / 64;
+using SubFft = WaveFft<1024>;
+constexpr int XCH_DOUBLES = LM;            // 128 KiB exchange region
+constexpr int S1_OFF = XCH_DOUBLES / 2;    // in double2 units
+constexpr size_t LARGE_LDS = sizeof(double2) * (S1_OFF + SubFft::Lds::s1_len);
+static_assert(LW * SubFft::XL * 2 <= XCH_DOUBLES, "wave buffers fit the exchange region");
+
+struct LargeCtx {
+    double *xch;        // exchange region (doubles)
+    cx *wxb;            // this wave's 1024-entry buffer inside it
+    SubFft::Lds tw;     // sub-block twiddles (LDS)
+    const double2 *W;   // W_M, global
+    int t, lane, wave;
+};
+
+__device__ __forceinline__ LargeCtx large_setup(const double2 *W) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double2 *lds = reinterpret_cast<double2 *>(smem);
+    LargeCtx c;
+    c.t = threadIdx.x;
+    c.lane = threadIdx.x & 63;
+    c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    c.xch = reinterpret_cast<double *>(smem);
+    c.wxb = reinterpret_cast<cx *>(smem) + c.wave * SubFft::XL;
+    double2 *s1 = lds + S1_OFF;
+    // sub-block stage twiddles W_1024[lane c] = W_M[16 lane c]  (oracle dif_rec tstride 16)
+    for (int e = threadIdx.x; e < SubFft::Lds::s1_len; e += LT) s1[e] = W[16 * (e & 63) * ((e >> 6) + 1)];
+    c.tw = SubFft::Lds{s1, s1};
+    c.W = W;
+    __syncthreads();
+    return c;
+}
+
+// top stage butterflies of thread t: a = t + 512 h (h = 0, 1), values at positions a + 1024 b.
+// After it, wave w owns sub-blocks 2w + h' (positions 1024 (2w+h') + [0, 1024)).
+__device__ __forceinline__ void large_exchange_to_blocks(const LargeCtx &c, cx (&u)[2][16]) {
+#pragma unroll
+    for (int part = 0; part < 2; part++) {
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) c.xch[c.t + 512 * h + 1024 * q] = part ? u[h][q].im : u[h][q].re;
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+            for (int b = 0; b < 16; b++) {
+                const double x = c.xch[1024 * (2 * c.wave + h) + c.lane + 64 * b];
+                if (part) u[h][b].im = x;
+                else u[h][b].re = x;
+            }
+    }
+    __syncthreads();  // the region now serves as the per-wave buffers
+}
+__device__ __forceinline__ void large_exchange_to_top(const LargeCtx &c, cx (&u)[2][16]) {
+#pragma unroll
+    for (int part = 0; part < 2; part++) {
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+            for (int b = 0; b < 16; b++)
+                c.xch[1024 * (2 * c.wave + h) + c.lane + 64 * b] = part ? u[h][b].im : u[h][b].re;
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const double x = c.xch[c.t + 512 * h + 1024 * q];
+                if (part) u[h][q].im = x;
+                else u[h][q].re = x;
+            }
+    }
+}
+
+// forward: u[h][b] = twisted input at position (t + 512 h) + 1024 b; on exit u[h] holds
+// sub-block 2 wave + h in the WaveFft<1024> Fourier layout.
+__device__ __forceinline__ void large_forward(const LargeCtx &c, cx (&u)[2][16]) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int a = c.t + 512 * h;
+        dft16_fwd(u[h]);
+#pragma unroll
+        for (int q = 1; q < 16; q++) {
+            const cx w = gld(c.W + a * q);
+            u[h][q] = cmulw(u[h][q], w.re, w.im);
+        }
+    }
+    large_exchange_to_blocks(c, u);
+    WaveLocalSync wsync;
+#pragma unroll
+    for (int h = 0; h < 2; h++) SubFft::forward(u[h], c.wxb, c.tw, c.lane, wsync);
+}
+
+// inverse of the above: on exit u[h][b] = position (t + 512 h) + 1024 b (unnormalised).
+__device__ __forceinline__ void large_inverse(const LargeCtx &c, cx (&u)[2][16]) {
+    WaveLocalSync wsync;
+#pragma unroll
+    for (int h = 0; h < 2; h++) SubFft::inverse(u[h], c.wxb, c.tw, c.lane, wsync);
+    large_exchange_to_top(c, u);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int a = c.t + 512 * h;
+#pragma unroll
+        for (int q = 1; q < 16; q++) {
+            const cx w = gld(c.W + a * q);
+            u[h][q] = cmulw(u[h][q], w.re, -w.im);
+        }
+        dft16_inv(u[h]);
+    }
+}
+
+// spectrum element (h, slot s) of thread (wave, lane) <-> offset in a poly's engine layout
+__device__ __forceinline__ size_t spec_off(int wave, int h, int s, int lane) {
+    return ((size_t)(2 * wave + h) * 16 + s) * 64 + lane;
+}
+
+}  // namespace
+
+// acc[ct] = LUT[idx] / X^{b~}  (bootstrap.rs:255-275)
+template <int K>
+__global__ void __launch_bounds__(256) large_init_kernel(LargePbsLaunch a, int ct0, int cnt) {
+    const size_t per = (size_t)(K + 1) * LN;
+    const size_t e = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= per * cnt) return;
+    const int cl = (int)(e / per);
+    const int p = (int)((e % per) / LN), j = (int)(e % LN);
+    const int ct = ct0 + cl;
+    const uint64_t *in = a.lwe_in + (size_t)ct * (a.n + 1);
+    const uint32_t bt = pbs_modulus_switch<15>(in[a.n]);
+    const uint32_t li = a.lut_indexes ? a.lut_indexes[ct] : 0u;
+    const uint64_t *lut = a.luts + (size_t)li * (K + 1) * LN + (size_t)p * LN;
+    const int full = bt / LN, rem = bt % LN;
+    const int src = j + rem;
+    const bool wrap = src >= LN;
+    const uint64_t v = lut[wrap ? src - LN : src];
+    a.acc[e] = (wrap != (bool)(full & 1)) ? 0 - v : v;
+}
+
+template <int K, int L>
+__global__ void __launch_bounds__(LT) large_fwd_kernel(LargePbsLaunch a, int ct0, int i) {
+    const LargeCtx c = large_setup(a.W);
+    const int blk = blockIdx.x;
+    const int lvl = L - blk % L;                 // level of this workgroup's digits
+    const int r = (blk / L) % (K + 1);
+    const int cl = blk / (L * (K + 1));
+    const uint64_t *in = a.lwe_in + (size_t)(ct0 + cl) * (a.n + 1);
+    const uint32_t at = pbs_modulus_switch<15>(in[i]);
+    const bool full_odd = (at / LN) & 1;
+    const int rem = at % LN;
+    const uint64_t *acc = a.acc + ((size_t)cl * (K + 1) + r) * LN;
+    const int beta = a.base_log;
+    const uint32_t dmask = (1u << beta) - 1;
+
+    cx u[2][16];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+#pragma unroll
+        for (int b = 0; b < 16; b++) {
+            const int j = c.t + 512 * h + 1024 * b;
+            int32_t dg[2];
+#pragma unroll
+            for (int half = 0; half < 2; half++) {
+                // ct1 = X^{a~} acc - acc  (polynomial_wrapping_monic_monomial_mul_and_subtract)
+                const int jj = j + half * LM - rem;
+                const bool neg = (jj < 0) != full_odd;
+                const uint64_t x = acc[(unsigned)jj & (unsigned)(LN - 1)];
+                const uint64_t d = (neg ? 0 - x : x) - acc[j + half * LM];
+                uint32_t st = decomp_state32_hi<L>((uint32_t)(d >> 32), beta);
+                int32_t dig = 0;
+#pragma unroll
+                for (int l = L; l >= 1; l--) {
+                    const int32_t v = decomp_digit32(st, beta, dmask);
+                    if (l == lvl) dig = v;
+                }
+                dg[half] = dig;
+            }
+            const cx tw = gld(a.twist + j);
+            u[h][b] = cmulw(cx{(double)dg[0], (double)dg[1]}, tw.re, tw.im);
+        }
+    }
+    large_forward(c, u);
+    double2 *F = a.spectra + (((size_t)cl * L + (lvl - 1)) * (K + 1) + r) * LM;
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int s = 0; s < 16; s++) F[spec_off(c.wave, h, s, c.lane)] = make_double2(u[h][s].re, u[h][s].im);
+}
+
+template <int K, int L>
+__global__ void __launch_bounds__(LT) large_inv_kernel(LargePbsLaunch a, int ct0, int i) {
+    const LargeCtx c = large_setup(a.W);
+    const int col = blockIdx.x % (K + 1);
+    const int cl = blockIdx.x / (K + 1);
+    const double2 *F = a.spectra + (size_t)cl * L * (K + 1) * LM;
+    const double2 *G = a.fbsk + (size_t)i * L * (K + 1) * (K + 1) * LM + (size_t)col * LM;
+
+    cx u[2][16];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+#pragma unroll
+        for (int s = 0; s < 16; s++) {
+            const size_t off = spec_off(c.wave, h, s, c.lane);
+            cx o{0.0, 0.0};
+            // column col: sum over levels L..1 and rows 0..k (ggsw.rs:524-567), oracle order
+#pragma unroll
+            for (int lvl = L; lvl >= 1; lvl--) {
+#pragma unroll
+                for (int r = 0; r <= K; r++) {
+                    const double2 gg = G[((size_t)(lvl - 1) * (K + 1) + r) * (K + 1) * LM + off];
+                    const double2 ff = F[((size_t)(lvl - 1) * (K + 1) + r) * LM + off];
+                    if (lvl == L && r == 0) {
+                        o.re = fma(gg.x, ff.x, -(gg.y * ff.y));
+                        o.im = fma(gg.x, ff.y, gg.y * ff.x);
+                    } else {
+                        o.re = fma(gg.x, ff.x, fma(-gg.y, ff.y, o.re));
+                        o.im = fma(gg.x, ff.y, fma(gg.y, ff.x, o.im));
+                    }
+                }
+            }
+            u[h][s] = o;
+        }
+    }
+    large_inverse(c, u);
+    uint64_t *acc = a.acc + ((size_t)cl * (K + 1) + col) * LN;
+    const double norm = 1.0 / (double)LM;
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int b = 0; b < 16; b++) {
+            const int j = c.t + 512 * h + 1024 * b;
+            const cx w = gld(a.twist + j);
+            uint64_t lo = acc[j], hi = acc[j + LM];
+            backward_add(u[h][b], cx{norm * w.re, norm * w.im}, lo, hi);
+            acc[j] = lo;
+            acc[j + LM] = hi;
+        }
+}
+
+// sample extract at degree 0 (glwe_sample_extraction.rs:91-147)
+template <int K>
+__global__ void __launch_bounds__(256) large_extract_kernel(LargePbsLaunch a, int ct0, int cnt) {
+    const size_t per = (size_t)K * LN + 1;
+    const size_t e = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= per * cnt) return;
+    const int cl = (int)(e / per);
+    const size_t q = e % per;
+    const uint64_t *acc = a.acc + (size_t)cl * (K + 1) * LN;
+    uint64_t v;
+    if (q == (size_t)K * LN) {
+        v = acc[(size_t)K * LN];
+    } else {
+        const int p = (int)(q / LN), j = (int)(q % LN);
+        v = j == 0 ? acc[(size_t)p * LN] : 0 - acc[(size_t)p * LN + LN - j];
+    }
+    a.lwe_out[(size_t)(ct0 + cl) * per + q] = v;
+}
+
+// standard -> Fourier BSK at N = 32768 (forward_as_torus, fft/mod.rs:197-218): one workgroup per poly
+__global__ void __launch_bounds__(LT) large_bsk_to_fourier_kernel(const uint64_t *__restrict__ polys,
+                                                                  double2 *__restrict__ out,
+                                                                  const double2 *__restrict__ W,
+                                                                  const double2 *__restrict__ twist) {
+    const LargeCtx c = large_setup(W);
+    const uint64_t *x = polys + (size_t)blockIdx.x * LN;
+    cx u[2][16];
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int b = 0; b < 16; b++) {
+            const int j = c.t + 512 * h + 1024 * b;
+            const double xr = (double)(int64_t)x[j] * 0x1p-64;
+            const double xi = (double)(int64_t)x[j + LM] * 0x1p-64;
+            const cx w = gld(twist + j);
+            u[h][b].re = xr * w.re - xi * w.im;
+            u[h][b].im = xr * w.im + xi * w.re;
+        }
+    large_forward(c, u);
+    double2 *o = out + (size_t)blockIdx.x * LM;
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int s = 0; s < 16; s++) o[spec_off(c.wave, h, s, c.lane)] = make_double2(u[h][s].re, u[h][s].im);
+}
+
+bool large_pbs_supported(int N, int k, int L) { return N == LN && k == 1 && (L == 1 || L == 2); }
+
+size_t large_pbs_scratch_per_ct(int N, int k, int L) {
+    return (size_t)(k + 1) * N * sizeof(uint64_t) + (size_t)L * (k + 1) * (N / 2) * sizeof(double2);
+}
+
+template <int K, int L>
+static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
+    if (a0.count == 0) return hipSuccess;
+    const size_t per_ct = large_pbs_scratch_per_ct(LN, K, L);
+    const int chunk = (int)std::min<size_t>((size_t)a0.count, a0.scratch_bytes / per_ct);
+    if (chunk <= 0) return hipErrorInvalidValue;
+    LargePbsLaunch a = a0;
+    a.acc = reinterpret_cast<uint64_t *>(a0.scratch);
+    a.spectra = reinterpret_cast<double2 *>(reinterpret_cast<char *>(a0.scratch) +
+                                            (size_t)chunk * (K + 1) * LN * sizeof(uint64_t));
+    for (int ct0 = 0; ct0 < a.count; ct0 += chunk) {
+        const int cnt = std::min(chunk, a.count - ct0);
+        const size_t init_elems = (size_t)cnt * (K + 1) * LN;
+        hipLaunchKernelGGL(large_init_kernel<K>, dim3((unsigned)((init_elems + 255) / 256)), dim3(256), 0, s, a,
+                           ct0, cnt);
+        for (int i = 0; i < a.n; i++) {
+            hipLaunchKernelGGL((large_fwd_kernel<K, L>), dim3(cnt * (K + 1) * L), dim3(LT), LARGE_LDS, s, a, ct0, i);
+            hipLaunchKernelGGL((large_inv_kernel<K, L>), dim3(cnt * (K + 1)), dim3(LT), LARGE_LDS, s, a, ct0, i);
+        }
+        const size_t out_elems = (size_t)cnt * (K * LN + 1);
+        hipLaunchKernelGGL(large_extract_kernel<K>, dim3((unsigned)((out_elems + 255) / 256)), dim3(256), 0, s, a,
+                           ct0, cnt);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_large_pbs(int N, int k, int L, const LargePbsLaunch &a, hipStream_t s) {
+    if (N == LN && k == 1 && L == 2) return launch_large_t<1, 2>(a, s);
+    if (N == LN && k == 1 && L == 1) return launch_large_t<1, 1>(a, s);
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_large_bsk_to_fourier(const uint64_t *std_polys, double2 *fourier, size_t npoly,
+                                       const FftTables &t, hipStream_t s) {
+    if (npoly == 0) return hipSuccess;
+    hipLaunchKernelGGL(large_bsk_to_fourier_kernel, dim3((unsigned)npoly), dim3(LT), LARGE_LDS, s, std_polys,
+                       fourier, t.W, t.twist);
+    return hipGetLastError();
+}
+
+}  // namespace tfhe_mi355
