@@ -43,6 +43,10 @@ PARAMS = {  # --params choice -> (parameter set name, workload text, kernel name
     "4_4": ("PARAM_MESSAGE_4_CARRY_4_KS_PBS",
             "BASELINE config 3: shortint apply_lookup_table (keyswitch -> PBS) at N=32768 per GPU batch",
             "large_fwd_kernel<1,2> + large_inv_kernel<1,2> (+ keyswitch_kernel)"),
+    "mul32": ("PARAM_MESSAGE_2_CARRY_2_KS_PBS",
+              "BASELINE config 4: FheUint32 multiply (16-block radix DAG, radix_parallel/mul.rs), "
+              "K independent pairs per GPU, every DAG layer one batched KS+PBS launch",
+              "pbs_classic_kernel<2048,1,1> + keyswitch_kernel"),
     "mb2": ("PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS",
             "batch of 4096 independent multi-bit (grouping 2) PBS per GPU, identity LUT",
             "pbs_multibit_kernel<2048,1,1,2>"),
@@ -171,6 +175,8 @@ def main():
             dist.all_reduce(t)
         torch.cuda.synchronize()
 
+    if args.params == "mul32":
+        return run_mul32(args, P, workload, kname, rank, world, local, device, barrier)
     B = args.batch or (1024 if args.params == "4_4" else 4096)
     with_ks = args.params == "4_4"   # config 3 is the shortint KS -> PBS
     msg_space = P.message_modulus * P.carry_modulus
@@ -312,6 +318,118 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def run_mul32(args, P, workload, kname, rank, world, local, device, barrier):
+    """Config 4: K FheUint32 multiplies per GPU per step through the batched integer DAG
+    (tfhe_mi355.integer); value = multiplies/s over all ranks."""
+    import torch
+    import torch.distributed as dist
+
+    from tfhe_mi355 import Engine, client, integer, shortint
+    from tfhe_mi355.distributed import broadcast_u64
+
+    K = args.batch or 64
+    ck = shortint.ClientKey(P, args.seed)
+    eng = Engine(P, local)
+    bsk_len = ggsw_count(P) * P.pbs_level * (P.glwe_dimension + 1) ** 2 * P.polynomial_size
+    ksk_len = P.big_lwe_dimension * P.ks_level * (P.lwe_dimension + 1)
+    bsk = ksk = None
+    if rank == 0:
+        bsk = client.gen_bootstrap_key(args.seed + 100, ck.small_lwe_secret_key, ck.glwe_secret_key,
+                                       P.glwe_dimension, P.polynomial_size, P.pbs_base_log, P.pbs_level,
+                                       P.glwe_modular_std_dev)
+        ksk = client.gen_keyswitch_key(args.seed + 200, ck.large_lwe_secret_key, ck.small_lwe_secret_key,
+                                       P.ks_base_log, P.ks_level, P.lwe_modular_std_dev)
+    d = broadcast_u64(bsk, bsk_len, 0, device)
+    eng.convert_bootstrap_key_device(d, bsk_len)
+    d = broadcast_u64(ksk, ksk_len, 0, device)
+    eng.upload_keyswitch_key_device(d, ksk_len)
+    torch.cuda.synchronize()
+    del d
+    sks = integer.ServerKey(shortint.ServerKey(None, engine=eng, parameters=P))
+    cks = integer.ClientKey(ck, 16)
+    rng = np.random.default_rng(args.seed * 1000 + rank)
+    a = rng.integers(0, 2 ** 32, K, dtype=np.uint64)
+    b = rng.integers(0, 2 ** 32, K, dtype=np.uint64)
+    ca, cb = cks.encrypt(a), cks.encrypt(b)
+
+    out = None
+    for _ in range(args.warmup):
+        out = sks.mul_parallelized(ca, cb)
+    barrier()
+    pbs0, l0 = sks.pbs_count, sks.launches
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = sks.mul_parallelized(ca, cb)
+    barrier()
+    wall = time.perf_counter() - t0
+    pbs_per_mul = (sks.pbs_count - pbs0) / (args.steps * K)
+    launches = (sks.launches - l0) / args.steps
+    tt = torch.tensor([wall], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    wall_max = float(tt.item())
+    ok = int(np.count_nonzero(cks.decrypt(out) == (a * b) % np.uint64(1 << 32)))
+    okt = torch.tensor([ok, K], dtype=torch.int64, device=device)
+    if world > 1:
+        dist.all_reduce(okt)
+    if rank == 0:
+        muls = world * K * args.steps
+        pbs_rate = muls * pbs_per_mul / wall_max
+        line = {
+            "metric": "FheUint32 multiplies/sec (PARAM_MESSAGE_2_CARRY_2 radix, 16 blocks) at 1/2/4/8 MI355X",
+            "value": muls / wall_max,
+            "unit": "mul/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": wall_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (uniform u32 operand pairs, seeded encryptions)",
+            "config": {"workload": workload, "parameters": P.name, "pairs_per_gpu": K,
+                       "global_pairs": world * K, "pbs_per_multiply": pbs_per_mul,
+                       "launches_per_multiply_batch": launches,
+                       "parallelism": f"dp{world} (whole multiplies sharded, keys broadcast once)"},
+            "pbs_per_sec": pbs_rate,
+            "roofline": {"bound": "hbm", "kernel": kname,
+                         "achieved": pbs_rate * pbs_algorithmic_bytes(P) / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": pbs_rate * pbs_algorithmic_bytes(P) / 1e9 / HBM_PEAK_GBS,
+                         "traffic": None,
+                         "model": "BSK-streaming bytes per PBS x PBS/s of the whole DAG (host orchestration included)"},
+            "check": {"decrypted_ok": int(okt[0].item()), "of": int(okt[1].item())},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            sys.path.insert(0, ROOT)
+            from oracle.oracle import OracleEngine  # oracle behind the engine API (test infrastructure)
+
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            oe = OracleEngine(P, threads=threads)
+            oe.upload_bootstrap_key(bsk)
+            oe.upload_keyswitch_key(ksk)
+            csk = integer.ServerKey(shortint.ServerKey(None, engine=oe, parameters=P))
+            t = time.perf_counter()
+            csk.mul_parallelized(RadixSlice(ca, 2), RadixSlice(cb, 2))
+            cw = time.perf_counter() - t
+            line["cpu_baseline"] = {
+                "value": 2 / cw, "unit": "mul/s", "cores": threads, "kind": "port",
+                "sample": (f"2 FheUint32 multiplies through the same DAG with the oracle C restatement behind "
+                           f"the engine API, {threads} threads ({cw:.1f} s); reference published 333 ms/mul "
+                           f"on a 128-vCPU m6i.metal (benchmarks.md:17)"),
+            }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def RadixSlice(rb, n):
+    from tfhe_mi355.integer import RadixBatch
+
+    return RadixBatch(rb.data[:n].copy(), list(rb.degree), list(rb.noise))
 
 
 if __name__ == "__main__":

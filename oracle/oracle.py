@@ -287,3 +287,37 @@ def keyswitch(ksk, in_dim, out_dim, base_log, level, lwe_in) -> np.ndarray:
     lib().orc_keyswitch_batch(_p(_u64(ksk)), in_dim, out_dim, base_log, level, _p(lwe_in),
                               _p(out), lwe_in.shape[0])
     return out
+
+
+class OracleEngine:
+    """The oracle (CPU restatement) behind the Engine's host API, so host-side orchestration
+    (shortint / integer layers) can run its exact DAG on the CPU as the parity reference."""
+
+    def __init__(self, params, threads=8):
+        import sys
+
+        O = sys.modules[__name__]
+        build()
+        self.O, self.p, self.threads = O, params, threads
+        self.fb = self.ksk = None
+
+    def upload_bootstrap_key(self, bsk):
+        p = self.p
+        self.fb = self.O.FourierBsk(bsk, p.lwe_dimension, p.glwe_dimension, p.polynomial_size,
+                                    p.pbs_base_log, p.pbs_level)
+
+    def upload_keyswitch_key(self, ksk):
+        self.ksk = np.ascontiguousarray(ksk, dtype=np.uint64)
+
+    def keyswitch(self, x):
+        from concurrent.futures import ThreadPoolExecutor
+
+        p = self.p
+        parts = [c for c in np.array_split(np.asarray(x), min(self.threads, len(x))) if len(c)]
+        with ThreadPoolExecutor(len(parts)) as ex:
+            outs = list(ex.map(lambda c: self.O.keyswitch(self.ksk, p.big_lwe_dimension, p.lwe_dimension,
+                                                          p.ks_base_log, p.ks_level, c), parts))
+        return np.concatenate(outs)
+
+    def keyswitch_programmable_bootstrap(self, x, luts, lut_indexes=None):
+        return self.fb.pbs(self.keyswitch(x), luts, lut_indexes, threads=self.threads)

@@ -99,3 +99,6 @@ def decode(pts, delta):
     d = np.asarray(pts, dtype=np.uint64)
     rounding = (d & np.uint64(delta >> 1)) << np.uint64(1)
     return (d + rounding) // np.uint64(delta)
+
+
+from oracle.oracle import OracleEngine  # noqa: E402,F401  (re-exported for the tests)

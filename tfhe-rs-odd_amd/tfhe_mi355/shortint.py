@@ -172,6 +172,12 @@ class ServerKey:
         ct[-1] = np.uint64((value % (p.message_modulus * p.carry_modulus)) * p.delta)
         return Ciphertext(ct, value, NOISE_ZERO, p.message_modulus, p.carry_modulus, self.pbs_order)
 
+    def engine_ks_pbs(self, x: np.ndarray, luts: np.ndarray, lut_indexes=None) -> np.ndarray:
+        """One batched launch of the key's PBS order over rows of x (big-key LWEs for KS->PBS)."""
+        if self.pbs_order == KEYSWITCH_BOOTSTRAP:
+            return self.engine.keyswitch_programmable_bootstrap(x, luts, lut_indexes)
+        return self.engine.programmable_bootstrap_keyswitch(x, luts, lut_indexes)
+
     def apply_lookup_table_batch_assign(self, cts: list[Ciphertext], accs) -> None:
         """One GPU launch for a whole layer; accs: one LookupTable or one per ciphertext."""
         if isinstance(accs, LookupTable):
