@@ -193,6 +193,9 @@ __device__ __forceinline__ cx lds_ld(const cx *xb, int p) {
 // patterns (lane + 64 c, and 64 cc + a1 + 4 b) become a per-lane base + compile-time immediate
 // offsets.  TM_XCHG_XOR=1: unpadded buffer with an XOR swizzle of the 16-B slot,
 // p ^ ((p >> 6) & 15) (saves 256 B per buffer, costs per-access address math).
+#ifndef TM_TW_SB
+#define TM_TW_SB 16 // twiddle multiplies per scheduling region (16 = one region)
+#endif
 #ifndef TM_XCHG_XOR
 #define TM_XCHG_XOR 1
 #endif
@@ -309,7 +312,7 @@ struct WaveFft<1024> {
         dft16_fwd(v);
 #pragma unroll
         for (int c = 1; c < 16; c++) {
-            if ((c & 3) == 1) __builtin_amdgcn_sched_barrier(0);  // bound twiddle loads in flight
+            if (c % TM_TW_SB == 1) __builtin_amdgcn_sched_barrier(0);  // bound twiddle loads in flight
             cx w = tw.s1(c, lane);
             v[c] = cmulw(v[c], w.re, w.im);
         }
@@ -324,7 +327,7 @@ struct WaveFft<1024> {
         dft16_fwd(v);
 #pragma unroll
         for (int c2 = 1; c2 < 16; c2++) {
-            if ((c2 & 3) == 1) __builtin_amdgcn_sched_barrier(0);
+            if (c2 % TM_TW_SB == 1) __builtin_amdgcn_sched_barrier(0);
             cx w = tw.s2(c2, a1);
             v[c2] = cmulw(v[c2], w.re, w.im);
         }

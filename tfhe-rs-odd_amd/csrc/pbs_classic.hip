@@ -170,13 +170,15 @@ __global__ void __launch_bounds__(64 * (K + 1) * PbsConfig<N>::CPW, PBS_WAVES_PE
             const double2 *lm = ggsw + (size_t)(lvl - 1) * (K + 1) * (K + 1) * M;
 #pragma unroll
             for (int s = 0; s < V; s++) {
-                if (s % 4 == 0) __builtin_amdgcn_sched_barrier(0);  // bound loads in flight
+                if (s % PBS_MAC_SB == 0) __builtin_amdgcn_sched_barrier(0);  // bound loads in flight
                 cx o = (L > 1 && lvl != L) ? acc[L > 1 ? s : 0] : cx{0.0, 0.0};
 #pragma unroll
                 for (int r = 0; r <= K; r++) {
                     const double2 gg = lm[(size_t)r * (K + 1) * M + s * 64];
                     double2 ff;
-                    if (r == wave) {
+                    if (PBS_MAC_FROM_LDS) {  // every row from LDS: no wave-dependent branch
+                        ff = reinterpret_cast<const double2 *>(xct + r * XL)[s * 64 + lane];
+                    } else if (r == wave) {
                         ff = make_double2(v[s].re, v[s].im);
                     } else {
                         ff = reinterpret_cast<const double2 *>(xct + r * XL)[s * 64 + lane];

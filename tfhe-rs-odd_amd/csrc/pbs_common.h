@@ -5,6 +5,12 @@
 #ifndef PBS_WAVE_LOCAL
 #define PBS_WAVE_LOCAL 1
 #endif
+#ifndef PBS_MAC_SB
+#define PBS_MAC_SB 4  // MAC slots per scheduling region
+#endif
+#ifndef PBS_MAC_FROM_LDS
+#define PBS_MAC_FROM_LDS 0
+#endif
 #ifndef PBS_WAVES_PER_EU
 #define PBS_WAVES_PER_EU 1
 #endif

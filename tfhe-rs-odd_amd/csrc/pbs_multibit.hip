@@ -181,7 +181,9 @@ __global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU)
                         kb.y = fma(gg.x, mono[sel].im, fma(gg.y, mono[sel].re, kb.y));
                     }
                     double2 ff;
-                    if (r == wave) {
+                    if (PBS_MAC_FROM_LDS) {  // every row from LDS: no wave-dependent branch
+                        ff = reinterpret_cast<const double2 *>(xct + r * XL)[s * 64 + lane];
+                    } else if (r == wave) {
                         ff = make_double2(v[s].re, v[s].im);
                     } else {
                         ff = reinterpret_cast<const double2 *>(xct + r * XL)[s * 64 + lane];
