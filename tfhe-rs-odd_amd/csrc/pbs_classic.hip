@@ -11,14 +11,15 @@
 //   par_convert_polynomials_list_to_fourier           fft64/math/fft/mod.rs:719-764
 // The fork's PATTERN msgpack dump (bootstrap.rs:340-342) is deliberately not reproduced.
 //
-// Design (DESIGN.md "Kernels"): a workgroup bootstraps CPW ciphertexts, one wavefront per
-// GLWE polynomial ((k+1) waves per ciphertext).  Each wave keeps its accumulator polynomial in
-// registers (u64), rotates it through its LDS buffer, decomposes and forward-FFTs it
-// (row r = its polynomial); the (k+1) spectra of a ciphertext are exchanged through LDS and
-// wave c computes output column c = sum_r F_r * GGSW[r][c] (GGSW streamed from L2/HBM, 16 B
-// per lane, coalesced), inverse-FFTs it and adds it back.  FFT twiddles and the twist live in
-// LDS, shared by the CPW ciphertexts.  At N = 2048: CPW = 4 -> 8 waves = 2 per SIMD, LDS
-// 32.7 KiB tables + 8 x 16 KiB buffers = 163,776 B.
+// Design (DESIGN.md "Kernels"): a workgroup bootstraps CPW ciphertexts (CPW = 1 by default),
+// one wavefront per GLWE polynomial ((k+1) waves per ciphertext).  Each wave keeps its
+// accumulator polynomial in registers (u64), rotates it through its LDS buffer, decomposes and
+// forward-FFTs it (row r = its polynomial); the (k+1) spectra of a ciphertext are exchanged
+// through LDS and wave c computes output column c = sum_r F_r * GGSW[r][c] (GGSW streamed from
+// L2/MALL, 16 B per lane, coalesced), inverse-FFTs it and adds it back.  FFT twiddles and the
+// twist live in LDS.  At N = 2048: 2 waves, 256 VGPR + ~106 AGPR (1 wave per SIMD), LDS
+// 31 KiB of tables + 2 x 16 KiB buffers -> 2 ciphertexts per CU.  Wave-private LDS reuse is
+// ordered with wave-local fences; only the spectrum exchange uses workgroup barriers.
 //
 // Control flow is uniform across the workgroup (barriers): a CMUX whose mask element is 0
 // (skipped by the reference, bootstrap.rs:285) is executed as a rotation by 0, which adds
