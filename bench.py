@@ -329,7 +329,7 @@ def run_mul32(args, P, workload, kname, rank, world, local, device, barrier):
     from tfhe_mi355 import Engine, client, integer, shortint
     from tfhe_mi355.distributed import broadcast_u64
 
-    K = args.batch or 64
+    K = args.batch or 256
     ck = shortint.ClientKey(P, args.seed)
     eng = Engine(P, local)
     bsk_len = ggsw_count(P) * P.pbs_level * (P.glwe_dimension + 1) ** 2 * P.polynomial_size
@@ -353,15 +353,16 @@ def run_mul32(args, P, workload, kname, rank, world, local, device, barrier):
     a = rng.integers(0, 2 ** 32, K, dtype=np.uint64)
     b = rng.integers(0, 2 ** 32, K, dtype=np.uint64)
     ca, cb = cks.encrypt(a), cks.encrypt(b)
+    ca_d, cb_d = sks.to_device(ca), sks.to_device(cb)   # operands resident in HBM
 
     out = None
     for _ in range(args.warmup):
-        out = sks.mul_parallelized(ca, cb)
+        out = sks.mul_parallelized(ca_d, cb_d)
     barrier()
     pbs0, l0 = sks.pbs_count, sks.launches
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out = sks.mul_parallelized(ca, cb)
+        out = sks.mul_parallelized(ca_d, cb_d)
     barrier()
     wall = time.perf_counter() - t0
     pbs_per_mul = (sks.pbs_count - pbs0) / (args.steps * K)

@@ -133,6 +133,19 @@ int tfhe_mi355_programmable_bootstrap_keyswitch(TfheMi355Context *ctx, const uin
                                                 uint64_t *lwe_out, const uint64_t *luts, size_t lut_count,
                                                 const uint32_t *lut_indexes, size_t count);
 
+/* Batched LWE linear algebra on device rows of u64 words (wrapping mod 2^64):
+ *   y[r] = y[r] * scalar + (d_x ? x[r] : 0)   for r < rows, `words` words per row,
+ * row strides in words.  Replaces shortint unchecked_add_assign / unchecked_scalar_mul_assign and
+ * the bivariate packing left*factor + right (shortint/server_key/bivariate_pbs.rs:167-182) for
+ * device-resident radix ciphertexts. */
+int tfhe_mi355_lwe_scalar_mul_add_async(TfheMi355Context *ctx, uint64_t *d_y, const uint64_t *d_x, uint64_t scalar,
+                                        size_t rows, size_t words, size_t y_stride, size_t x_stride, void *stream);
+/* trivial_pbs_assign (shortint/server_key/mod.rs:763-781) on the bodies of `rows` trivial
+ * ciphertexts (d_body points at the first body, rows `stride` words apart) with the GLWE
+ * accumulator d_lut ((k+1)*N words, device). */
+int tfhe_mi355_trivial_pbs_async(TfheMi355Context *ctx, uint64_t *d_body, size_t rows, size_t stride,
+                                 const uint64_t *d_lut, void *stream);
+
 /* Fill a shortint lookup table (GLWE accumulator, (k+1)*N words) from f(i), i < msg*carry.
  * Replaces shortint fill_accumulator (shortint/engine/mod.rs:72-128). */
 int tfhe_mi355_fill_accumulator(const TfheMi355Parameters *params, const uint64_t *f_values,

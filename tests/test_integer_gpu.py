@@ -27,8 +27,8 @@ def test_fheuint32_mul_bit_exact_vs_oracle_dag():
     a = np.array([0xFFFFFFFF, 0x80000001, 7], dtype=np.uint64)
     b = np.array([0xFFFFFFFF, 3, 0x0F0F0F0F], dtype=np.uint64)
     ca, cb = cks.encrypt(a), cks.encrypt(b)
-    g = gpu.mul_parallelized(ca, cb)
-    c = cpu.mul_parallelized(ca, cb)
+    g = gpu.to_host(gpu.mul_parallelized(ca, cb))   # device-resident DAG (lwe_ops kernels)
+    c = cpu.mul_parallelized(ca, cb)                 # host numpy DAG, oracle engine
     assert gpu.pbs_count == cpu.pbs_count
     assert g.degree == c.degree and g.noise == c.noise
     assert np.array_equal(g.data, c.data), f"{np.count_nonzero(g.data != c.data)} words differ"

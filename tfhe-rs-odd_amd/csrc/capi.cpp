@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -170,7 +171,13 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
         return;
     }
     if (large_pbs_supported((int)c->N(), (int)c->k(), (int)c->p.pbs_level)) {
-        constexpr size_t kChunk = 4096;  // ciphertexts per pass: 6 GiB of scratch at 4_4
+        // ciphertexts per pass: the chunk's accumulators + spectra (1.5 MiB per ciphertext at 4_4)
+        // should stay resident in the 256 MiB Infinity Cache across the two launches of a CMUX
+        static const size_t kChunk = [] {
+            const char *e = std::getenv("TFHE_MI355_LARGE_CHUNK");
+            const long v = e ? std::atol(e) : 0;
+            return v > 0 ? (size_t)v : (size_t)128;  // 128: best of 64..1024 at 4_4 (profiles)
+        }();
         const size_t per_ct = large_pbs_scratch_per_ct((int)c->N(), (int)c->k(), (int)c->p.pbs_level);
         c->pbs_scratch.reserve(per_ct * std::max<size_t>(1, std::min(count, kChunk)));
         LargePbsLaunch a{};
@@ -540,6 +547,30 @@ int tfhe_mi355_programmable_bootstrap_keyswitch(TfheMi355Context *ctx, const uin
         launch_ks_dev(ctx, (const uint64_t *)ctx->io_tmp.ptr, (uint64_t *)ctx->io_out.ptr, count, s);
         check(hipMemcpyAsync(lwe_out, ctx->io_out.ptr, small_b, hipMemcpyDeviceToHost, s), "D2H out");
         check(hipStreamSynchronize(s), "pbs-ks sync");
+    });
+}
+
+int tfhe_mi355_lwe_scalar_mul_add_async(TfheMi355Context *ctx, uint64_t *d_y, const uint64_t *d_x, uint64_t scalar,
+                                        size_t rows, size_t words, size_t y_stride, size_t x_stride, void *stream) {
+    return guarded([&] {
+        if (!ctx || (!d_y && rows * words)) fail("null argument");
+        if (words > y_stride || (d_x && words > x_stride)) fail("row stride smaller than the row");
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        check(launch_lwe_scalar_mul_add(d_y, d_x, scalar, rows, words, y_stride, x_stride, (hipStream_t)stream),
+              "lwe scalar_mul_add");
+    });
+}
+
+int tfhe_mi355_trivial_pbs_async(TfheMi355Context *ctx, uint64_t *d_body, size_t rows, size_t stride,
+                                 const uint64_t *d_lut, void *stream) {
+    return guarded([&] {
+        if (!ctx || ((!d_body || !d_lut) && rows)) fail("null argument");
+        const uint64_t msup = (uint64_t)ctx->p.message_modulus * ctx->p.carry_modulus;
+        if (msup == 0 || ctx->N() % msup) fail("message space does not divide the polynomial size");
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        check(launch_trivial_pbs(d_body, rows, stride, d_lut + ctx->k() * ctx->N(), (1ULL << 63) / msup, msup,
+                                 ctx->N() / msup, (hipStream_t)stream),
+              "trivial pbs");
     });
 }
 

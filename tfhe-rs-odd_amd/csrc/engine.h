@@ -79,4 +79,10 @@ struct KeyswitchLaunch {
 };
 hipError_t launch_keyswitch(const KeyswitchLaunch &a, hipStream_t s);
 
+// batched LWE linear algebra / trivial PBS (lwe_ops.hip)
+hipError_t launch_lwe_scalar_mul_add(uint64_t *y, const uint64_t *x, uint64_t scalar, size_t rows, size_t words,
+                                     size_t y_stride, size_t x_stride, hipStream_t s);
+hipError_t launch_trivial_pbs(uint64_t *body, size_t rows, size_t stride, const uint64_t *lut_body, uint64_t delta,
+                              uint64_t modulus_sup, uint64_t box, hipStream_t s);
+
 }  // namespace tfhe_mi355

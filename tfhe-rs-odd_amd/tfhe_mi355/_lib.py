@@ -62,6 +62,9 @@ SIGNATURES = [
     ("tfhe_mi355_client_gen_bootstrap_key", ctypes.c_int,
      [ctypes.c_uint64, u64p, ctypes.c_uint32, u64p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
       ctypes.c_uint32, ctypes.c_double, u64p, ctypes.c_uint32]),
+    ("tfhe_mi355_lwe_scalar_mul_add_async", ctypes.c_int,
+     [vp, vp, vp, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, vp]),
+    ("tfhe_mi355_trivial_pbs_async", ctypes.c_int, [vp, vp, ctypes.c_size_t, ctypes.c_size_t, vp, vp]),
     ("tfhe_mi355_client_gen_multi_bit_bootstrap_key", ctypes.c_int,
      [ctypes.c_uint64, u64p, ctypes.c_uint32, u64p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
       ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double, u64p, ctypes.c_uint32]),

@@ -190,6 +190,16 @@ class Engine:
                   _dev_ptr(d_out), _dev_ptr(d_luts), lut_count, _dev_ptr(d_lut_indexes), count,
                   _dev_ptr(d_scratch), _stream_ptr(stream))
 
+    def lwe_scalar_mul_add_async(self, y_ptr: int, x_ptr, scalar: int, rows: int, words: int, y_stride: int,
+                                 x_stride: int = 0, stream=None) -> None:
+        """y[r] = y[r] * scalar + x[r] (u64 wrapping) on device rows (raw pointers: strided views allowed)."""
+        _lib.call("tfhe_mi355_lwe_scalar_mul_add_async", self._h, y_ptr, x_ptr, scalar % (1 << 64), rows, words,
+                  y_stride, x_stride, _stream_ptr(stream))
+
+    def trivial_pbs_async(self, body_ptr: int, rows: int, stride: int, d_lut, stream=None) -> None:
+        _lib.call("tfhe_mi355_trivial_pbs_async", self._h, body_ptr, rows, stride, _dev_ptr(d_lut),
+                  _stream_ptr(stream))
+
     def ks_pbs_scratch_bytes(self, count: int) -> int:
         b = ctypes.c_size_t()
         _lib.call("tfhe_mi355_keyswitch_programmable_bootstrap_scratch", self._h, count, ctypes.byref(b))

@@ -23,7 +23,10 @@ RadixBatch therefore stores the K ciphertexts as one u64 array [K, blocks, lwe_s
 (degree, noise_level) per block, and every PBS layer of the DAG -- across all terms and all K
 pairs -- is handed to the engine as ONE batched keyswitch+PBS launch with per-ciphertext LUT
 indexes (the "PBS-DAG scheduler" of SURVEY.md 8f row f1).  Trivial blocks take the reference's
-trivial-PBS shortcut (shortint/server_key/mod.rs:763-781) on the host.
+trivial-PBS shortcut (shortint/server_key/mod.rs:763-781).  With the GPU engine the batch stays
+resident in HBM between layers (torch tensors for storage; the LWE arithmetic and trivial PBS in
+the engine's lwe_ops kernels); with any other engine object (the oracle, in the tests) it is a
+numpy array on the host -- same DAG, same bits.
 
 Carry propagation uses the Hillis-Steele branch; the reference selects it whenever
 should_hillis_steele_propagation_be_faster (add.rs:44-76) holds, i.e. with >= 16 rayon threads
@@ -57,7 +60,8 @@ class RadixBatch:
         return self.data.shape[1]
 
     def clone(self) -> "RadixBatch":
-        return RadixBatch(self.data.copy(), list(self.degree), list(self.noise))
+        d = self.data.copy() if isinstance(self.data, np.ndarray) else self.data.clone()
+        return RadixBatch(d, list(self.degree), list(self.noise))
 
     def block_carries_are_empty(self, message_modulus: int) -> bool:
         return all(d < message_modulus for d in self.degree)
@@ -94,17 +98,145 @@ class _PbsLayer:
                 luts.append(lut.acc)
             todo.append((rb, j, lut_of[id(lut)]))
         if todo:
-            K = todo[0][0].count
-            x = np.concatenate([rb.data[:, j, :] for rb, j, _ in todo], axis=0)
-            idx = np.repeat(np.asarray([li for _, _, li in todo], dtype=np.uint32), K)
-            out = sk.shortint.engine_ks_pbs(x, np.stack(luts), idx if len(luts) > 1 else None)
-            sk.pbs_count += x.shape[0]
+            n = sk.ops.pbs_rows([(rb, j, li) for rb, j, li in todo], luts)
+            sk.pbs_count += n
             sk.launches += 1
-            for q, (rb, j, _) in enumerate(todo):
-                rb.data[:, j, :] = out[q * K:(q + 1) * K]
+            for rb, j, _ in todo:
                 rb.noise[j] = NOISE_NOMINAL
         for rb, j, lut in reqs:
             rb.degree[j] = lut.degree
+
+
+
+def _is_gpu_engine(engine) -> bool:
+    from .engine import Engine
+
+    return isinstance(engine, Engine)
+
+
+class _HostOps:
+    """numpy arrays on the host; PBS through the engine's host-pointer API (any engine object
+    with keyswitch_programmable_bootstrap, e.g. the oracle's in the tests)."""
+
+    def __init__(self, sk: "ServerKey"):
+        self.sk = sk
+
+    def zeros(self, k, b, s):
+        return np.zeros((k, b, s), dtype=np.uint64)
+
+    def roll(self, data, shift):
+        return np.roll(data, shift, axis=1)
+
+    def to_host(self, data):
+        return data
+
+    def from_host(self, data):
+        return data
+
+    def copy_block(self, dst, j, src, i):
+        dst.data[:, j, :] = src.data[:, i, :]
+
+    def set_trivial(self, rb, j, body):
+        rb.data[:, j, :] = 0
+        rb.data[:, j, -1] = np.uint64(body)
+
+    def mul_add(self, dst, j, scalar, src, i):
+        if scalar != 1:
+            dst.data[:, j, :] *= np.uint64(scalar)
+        if src is not None:
+            dst.data[:, j, :] += src.data[:, i, :]
+
+    def trivial_pbs(self, rb, j, lut):
+        p = self.sk.p
+        modulus_sup = p.message_modulus * p.carry_modulus
+        box = p.polynomial_size // modulus_sup
+        body = lut.acc[p.glwe_dimension * p.polynomial_size:]
+        value = rb.data[:, j, -1] // np.uint64(p.delta)
+        neg = value >= np.uint64(modulus_sup)
+        entry = body[((value % np.uint64(modulus_sup)) * np.uint64(box)).astype(np.int64)]
+        rb.data[:, j, -1] = np.where(neg, np.uint64(0) - entry, entry)
+
+    def pbs_rows(self, todo, luts):
+        K = todo[0][0].count
+        x = np.concatenate([rb.data[:, j, :] for rb, j, _ in todo], axis=0)
+        idx = np.repeat(np.asarray([li for _, _, li in todo], dtype=np.uint32), K)
+        out = self.sk.shortint.engine_ks_pbs(x, np.stack(luts), idx if len(luts) > 1 else None)
+        for q, (rb, j, _) in enumerate(todo):
+            rb.data[:, j, :] = out[q * K:(q + 1) * K]
+        return x.shape[0]
+
+
+class _DeviceOps:
+    """torch int64 tensors resident on the engine's GPU between layers; the LWE arithmetic runs in
+    the engine's own kernels (lwe_ops.hip), torch only allocates, slices and copies."""
+
+    def __init__(self, sk: "ServerKey"):
+        import torch
+
+        self.torch = torch
+        self.sk = sk
+        self.eng = sk.shortint.engine
+        self.device = torch.device("cuda", self.eng.device)
+        self._lut_dev = {}
+        self._scratch = None
+
+    def zeros(self, k, b, s):
+        return self.torch.zeros((k, b, s), dtype=self.torch.int64, device=self.device)
+
+    def roll(self, data, shift):
+        return self.torch.roll(data, shift, dims=1) if shift else data
+
+    def to_host(self, data):
+        return data.cpu().numpy().view(np.uint64)
+
+    def from_host(self, data):
+        return self.torch.from_numpy(np.ascontiguousarray(data).view(np.int64)).to(self.device)
+
+    def copy_block(self, dst, j, src, i):
+        dst.data[:, j, :].copy_(src.data[:, i, :])
+
+    def set_trivial(self, rb, j, body):
+        rb.data[:, j, :].zero_()
+        rb.data[:, j, -1] = int(np.uint64(body).view(np.int64))
+
+    def _row_ptr(self, rb, j, word=0):
+        d = rb.data
+        return d.data_ptr() + 8 * (j * d.shape[2] + word), d.shape[1] * d.shape[2]
+
+    def mul_add(self, dst, j, scalar, src, i):
+        yp, ys = self._row_ptr(dst, j)
+        xp, xs = self._row_ptr(src, i) if src is not None else (None, 0)
+        self.eng.lwe_scalar_mul_add_async(yp, xp, scalar, dst.count, dst.data.shape[2], ys, xs)
+
+    def lut(self, lut):
+        t = self._lut_dev.get(id(lut))
+        if t is None or t[0] is not lut:
+            t = (lut, self.from_host(lut.acc))
+            self._lut_dev[id(lut)] = t
+        return t[1]
+
+    def trivial_pbs(self, rb, j, lut):
+        bp, stride = self._row_ptr(rb, j, rb.data.shape[2] - 1)
+        self.eng.trivial_pbs_async(bp, rb.count, stride, self.lut(lut))
+
+    def pbs_rows(self, todo, luts_np):
+        torch = self.torch
+        K = todo[0][0].count
+        x = torch.cat([rb.data[:, j, :] for rb, j, _ in todo], dim=0)
+        n = x.shape[0]
+        luts = self.from_host(np.stack(luts_np))
+        idx = None
+        if len(luts_np) > 1:
+            idx = torch.from_numpy(np.repeat(np.asarray([li for _, _, li in todo], dtype=np.int32), K)).to(self.device)
+        out = torch.empty_like(x)
+        need = self.eng.ks_pbs_scratch_bytes(n)
+        if self._scratch is None or self._scratch.numel() < need:
+            self._scratch = torch.empty(need, dtype=torch.uint8, device=self.device)
+        self.eng.keyswitch_programmable_bootstrap_async(x, out, luts, len(luts_np), n, self._scratch,
+                                                        d_lut_indexes=idx)
+        for q, (rb, j, _) in enumerate(todo):
+            rb.data[:, j, :].copy_(out[q * K:(q + 1) * K])
+        return n
 
 
 class ServerKey:
@@ -121,6 +253,7 @@ class ServerKey:
         self.lwe_size = p.big_lwe_dimension + 1
         self.pbs_count = 0
         self.launches = 0
+        self.ops = _DeviceOps(self) if _is_gpu_engine(shortint_key.engine) else _HostOps(self)
         m = self.msg
         self.lut_message = self.shortint.generate_lookup_table(lambda x: x % m)
         self.lut_carry = self.shortint.generate_lookup_table(lambda x: x // m)
@@ -143,30 +276,22 @@ class ServerKey:
     # -- block primitives (shortint) -----------------------------------------------------------
     def _trivial_pbs(self, rb: RadixBatch, j: int, lut: LookupTable):
         """trivial_pbs_assign (shortint/server_key/mod.rs:763-781) for every ciphertext of the batch."""
-        p = self.p
-        modulus_sup = p.message_modulus * p.carry_modulus
-        box = p.polynomial_size // modulus_sup
-        body = lut.acc[p.glwe_dimension * p.polynomial_size:]
-        value = rb.data[:, j, -1] // np.uint64(p.delta)
-        neg = value >= np.uint64(modulus_sup)
-        entry = body[((value % np.uint64(modulus_sup)) * np.uint64(box)).astype(np.int64)]
-        rb.data[:, j, -1] = np.where(neg, np.uint64(0) - entry, entry)
+        self.ops.trivial_pbs(rb, j, lut)
 
     def _set_trivial(self, rb: RadixBatch, j: int, value: int = 0):
         """create_trivial_assign (shortint server_key create_trivial)."""
-        rb.data[:, j, :] = 0
-        rb.data[:, j, -1] = np.uint64((value % (self.msg * self.carry)) * self.p.delta)
+        self.ops.set_trivial(rb, j, (value % (self.msg * self.carry)) * self.p.delta)
         rb.degree[j] = value
         rb.noise[j] = NOISE_ZERO
 
     def _add_block(self, dst: RadixBatch, j: int, src: RadixBatch, i: int):
         """shortint unchecked_add_assign: LWE add, degree and noise level add."""
-        dst.data[:, j, :] += src.data[:, i, :]
+        self.ops.mul_add(dst, j, 1, src, i)
         dst.degree[j] += src.degree[i]
         dst.noise[j] += src.noise[i]
 
     def _scalar_mul_block(self, rb: RadixBatch, j: int, s: int):
-        rb.data[:, j, :] *= np.uint64(s)
+        self.ops.mul_add(rb, j, s, None, 0)
         rb.degree[j] *= s
         rb.noise[j] *= s
 
@@ -180,16 +305,15 @@ class ServerKey:
 
     # -- radix helpers -------------------------------------------------------------------------
     def create_trivial_zero(self, count: int, num_blocks: int) -> RadixBatch:
-        rb = RadixBatch(np.zeros((count, num_blocks, self.lwe_size), dtype=np.uint64), [0] * num_blocks,
-                        [NOISE_ZERO] * num_blocks)
-        return rb
+        return RadixBatch(self.ops.zeros(count, num_blocks, self.lwe_size), [0] * num_blocks,
+                          [NOISE_ZERO] * num_blocks)
 
     def blockshift(self, ct: RadixBatch, shift: int) -> RadixBatch:
         """radix/scalar_mul.rs:345-355: rotate_right(shift), low blocks trivial zeros."""
         res = ct.clone()
         nb = ct.num_blocks
         s = shift % nb if nb else 0
-        res.data = np.roll(res.data, s, axis=1)
+        res.data = self.ops.roll(res.data, s)
         res.degree = res.degree[nb - s:] + res.degree[:nb - s]
         res.noise = res.noise[nb - s:] + res.noise[:nb - s]
         for j in range(min(shift, nb)):
@@ -218,7 +342,7 @@ class ServerKey:
                 self._bivariate(layer, step, b, gp, b - space, self.lut_prefix)
             layer.flush()
             for b in range(space, nb):
-                gp.data[:, b, :] = step.data[:, b, :]
+                self.ops.copy_block(gp, b, step, b)
                 gp.degree[b] = step.degree[b]
                 gp.noise[b] = step.noise[b]
             space *= 2
@@ -226,7 +350,7 @@ class ServerKey:
         # swapped out for a trivial zero, then rotate_right(1)
         carries = gp
         self._set_trivial(carries, nb - 1, 0)
-        carries.data = np.roll(carries.data, 1, axis=1)
+        carries.data = self.ops.roll(carries.data, 1)
         carries.degree = carries.degree[-1:] + carries.degree[:-1]
         carries.noise = carries.noise[-1:] + carries.noise[:-1]
         for j in range(nb):
@@ -251,7 +375,7 @@ class ServerKey:
             layer.add(carries, j, self.lut_carry)
         layer.flush()
         self._set_trivial(carries, nb - 1, 0)
-        carries.data = np.roll(carries.data, 1, axis=1)
+        carries.data = self.ops.roll(carries.data, 1)
         carries.degree = carries.degree[-1:] + carries.degree[:-1]
         carries.noise = carries.noise[-1:] + carries.noise[:-1]
         self._unchecked_add_assign_low_latency(ct, carries)
@@ -313,7 +437,7 @@ class ServerKey:
                     self._set_trivial(carry, j, 0)
                 for j in range(end + 1, nb):
                     self._set_trivial(carry, j, 0)
-                carry.data = np.roll(carry.data, 1, axis=1)
+                carry.data = self.ops.roll(carry.data, 1)
                 carry.degree = carry.degree[-1:] + carry.degree[:-1]
                 carry.noise = carry.noise[-1:] + carry.noise[:-1]
                 new += [s, carry]
@@ -329,16 +453,25 @@ class ServerKey:
             layer.add(carry, j, self.lut_carry)
         layer.flush()
         self._set_trivial(carry, nb - 1, 0)
-        carry.data = np.roll(carry.data, 1, axis=1)
+        carry.data = self.ops.roll(carry.data, 1)
         carry.degree = carry.degree[-1:] + carry.degree[:-1]
         carry.noise = carry.noise[-1:] + carry.noise[:-1]
         self.add_assign_parallelized(result, carry)
         assert result.block_carries_are_empty(self.msg)
         return result
 
+    def to_device(self, rb: RadixBatch) -> RadixBatch:
+        """Host RadixBatch (from ClientKey.encrypt) -> this key's residency."""
+        return RadixBatch(self.ops.from_host(rb.data), list(rb.degree), list(rb.noise))
+
+    def to_host(self, rb: RadixBatch) -> RadixBatch:
+        return RadixBatch(self.ops.to_host(rb.data) if not isinstance(rb.data, np.ndarray) else rb.data,
+                          list(rb.degree), list(rb.noise))
+
     # -- multiplication ------------------------------------------------------------------------
     def unchecked_mul(self, lhs: RadixBatch, rhs: RadixBatch) -> RadixBatch:
         """unchecked_mul_assign_parallelized (mul.rs:300-414)."""
+        lhs, rhs = self._resident(lhs), self._resident(rhs)
         if rhs.holds_boolean_value() or lhs.holds_boolean_value():
             raise NotImplementedError("boolean-valued operand (zero_out_if_condition_is_false path)")
         nb = lhs.num_blocks
@@ -362,8 +495,14 @@ class ServerKey:
         out = self.unchecked_sum_ciphertexts_vec(terms)
         return out if out is not None else self.create_trivial_zero(lhs.count, nb)
 
+    def _resident(self, rb: RadixBatch) -> RadixBatch:
+        if isinstance(rb.data, np.ndarray) and isinstance(self.ops, _DeviceOps):
+            return self.to_device(rb)
+        return rb
+
     def mul_parallelized(self, lhs: RadixBatch, rhs: RadixBatch) -> RadixBatch:
         """mul.rs:553-590."""
+        lhs, rhs = self._resident(lhs), self._resident(rhs)
         lhs = lhs.clone()
         if not rhs.block_carries_are_empty(self.msg):
             rhs = rhs.clone()
@@ -395,6 +534,8 @@ class ClientKey:
         p = self.key.parameters
         from . import client
 
+        if not isinstance(rb.data, np.ndarray):
+            rb = RadixBatch(rb.data.cpu().numpy().view(np.uint64), rb.degree, rb.noise)
         bits = int(np.log2(p.message_modulus))
         out = np.zeros(rb.count, dtype=np.uint64)
         for j in range(rb.num_blocks):
