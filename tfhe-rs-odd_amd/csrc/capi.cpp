@@ -84,6 +84,9 @@ struct TfheMi355Context {
     DeviceBuffer fbsk, ksk, std_staging;
     DeviceBuffer io_in, io_out, io_luts, io_idx, io_tmp;
     DeviceBuffer pbs_scratch;  // N = 32768: accumulators + spectra of one chunk of ciphertexts
+    DeviceBuffer ksk_planes;   // int8 byte planes of the KSK for the MFMA keyswitch
+    DeviceBuffer ks_scratch;   // MFMA keyswitch digits
+    bool ksk_planes_ready = false;
     bool fbsk_ready = false, ksk_ready = false;
 
     size_t n() const { return p.lwe_dimension; }
@@ -211,8 +214,39 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
     check(launch_classic_pbs((int)c->N(), (int)c->k(), (int)c->p.pbs_level, a, s), "launch pbs");
 }
 
+bool ks_use_mfma(TfheMi355Context *c) {
+    static const bool disabled = std::getenv("TFHE_MI355_KS_NO_MFMA") != nullptr;
+    return !disabled && ks_mfma_supported((int)c->big_dim(), (int)c->p.ks_level, (int)c->p.ks_base_log);
+}
+
+// KSK -> int8 byte planes (once per key, after the u64 KSK is on the device)
+void repack_ksk(TfheMi355Context *c, hipStream_t s) {
+    c->ksk_planes_ready = false;
+    if (!ks_use_mfma(c)) return;
+    const size_t bytes = 8 * ks_mfma_rows((int)c->big_dim(), (int)c->p.ks_level) * ks_mfma_cols((int)c->n());
+    c->ksk_planes.reserve(bytes);
+    check(launch_ksk_repack((const uint64_t *)c->ksk.ptr, (int8_t *)c->ksk_planes.ptr, (int)c->big_dim(),
+                            (int)c->p.ks_level, (int)c->n(), s),
+          "ksk repack");
+    c->ksk_planes_ready = true;
+}
+
 void launch_ks_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, size_t count, hipStream_t s) {
     require_ksk(c);
+    if (c->ksk_planes_ready && count > 0) {
+        KeyswitchLaunch a;
+        a.lwe_in = d_in;
+        a.lwe_out = d_out;
+        a.ksk = reinterpret_cast<const uint64_t *>(c->ksk.ptr);
+        a.in_dim = (int)c->big_dim();
+        a.out_dim = (int)c->n();
+        a.base_log = (int)c->p.ks_base_log;
+        a.level = (int)c->p.ks_level;
+        a.count = (int)count;
+        c->ks_scratch.reserve(ks_mfma_scratch_bytes(a.in_dim, a.level, a.count));
+        check(launch_keyswitch_mfma(a, (const int8_t *)c->ksk_planes.ptr, c->ks_scratch.ptr, s), "launch mfma keyswitch");
+        return;
+    }
     KeyswitchLaunch a;
     a.lwe_in = d_in;
     a.lwe_out = d_out;
@@ -290,7 +324,8 @@ int tfhe_mi355_context_destroy(TfheMi355Context *ctx) {
         (void)hipSetDevice(ctx->device);
         if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
         for (DeviceBuffer *b : {&ctx->fbsk, &ctx->ksk, &ctx->std_staging, &ctx->io_in, &ctx->io_out,
-                                &ctx->io_luts, &ctx->io_idx, &ctx->io_tmp, &ctx->pbs_scratch})
+                                &ctx->io_luts, &ctx->io_idx, &ctx->io_tmp, &ctx->pbs_scratch,
+                                &ctx->ksk_planes, &ctx->ks_scratch})
             b->release();
         if (ctx->tables.W) (void)hipFree(ctx->tables.W);
         if (ctx->tables.twist) (void)hipFree(ctx->tables.twist);
@@ -360,6 +395,8 @@ int tfhe_mi355_keyswitch_key_upload(TfheMi355Context *ctx, const uint64_t *ksk, 
         if (len != ctx->ksk_len()) fail("keyswitching key has %zu words, expected %zu", len, ctx->ksk_len());
         ctx->ksk.reserve(len * sizeof(uint64_t));
         check(hipMemcpy(ctx->ksk.ptr, ksk, len * sizeof(uint64_t), hipMemcpyHostToDevice), "upload ksk");
+        repack_ksk(ctx, ctx->stream);
+        check(hipStreamSynchronize(ctx->stream), "ksk repack sync");
         ctx->ksk_ready = true;
     });
 }
@@ -374,6 +411,7 @@ int tfhe_mi355_keyswitch_key_upload_async(TfheMi355Context *ctx, const uint64_t 
         ctx->ksk.reserve(len * sizeof(uint64_t));
         check(hipMemcpyAsync(ctx->ksk.ptr, d_ksk, len * sizeof(uint64_t), hipMemcpyDeviceToDevice,
                              (hipStream_t)stream), "copy ksk");
+        repack_ksk(ctx, (hipStream_t)stream);
         ctx->ksk_ready = true;
     });
 }
@@ -395,6 +433,9 @@ int tfhe_mi355_keyswitch_key_set_ready(TfheMi355Context *ctx) {
     return guarded([&] {
         if (!ctx) fail("null ctx");
         if (!ctx->ksk.ptr) fail("no keyswitching key buffer");
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        repack_ksk(ctx, ctx->stream);
+        check(hipStreamSynchronize(ctx->stream), "ksk repack sync");
         ctx->ksk_ready = true;
     });
 }

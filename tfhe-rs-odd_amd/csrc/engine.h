@@ -78,6 +78,13 @@ struct KeyswitchLaunch {
     int count;
 };
 hipError_t launch_keyswitch(const KeyswitchLaunch &a, hipStream_t s);
+// int8-MFMA keyswitch: KSK repacked once into 8 byte planes (ks_mfma_cols x ks_mfma_rows each)
+bool ks_mfma_supported(int in_dim, int level, int base_log);
+size_t ks_mfma_rows(int in_dim, int level);
+size_t ks_mfma_cols(int out_dim);
+size_t ks_mfma_scratch_bytes(int in_dim, int level, int count);
+hipError_t launch_ksk_repack(const uint64_t *ksk, int8_t *kt, int in_dim, int level, int out_dim, hipStream_t s);
+hipError_t launch_keyswitch_mfma(const KeyswitchLaunch &a, const int8_t *kt, void *scratch, hipStream_t s);
 
 // batched LWE linear algebra / trivial PBS (lwe_ops.hip)
 hipError_t launch_lwe_scalar_mul_add(uint64_t *y, const uint64_t *x, uint64_t scalar, size_t rows, size_t words,

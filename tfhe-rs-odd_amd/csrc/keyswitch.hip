@@ -85,6 +85,146 @@ __global__ void __launch_bounds__(256) keyswitch_kernel(KeyswitchLaunch a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Keyswitch as int8 MFMA GEMMs.  With D[c][m] the signed digits (|d| <= 2^(beta-1) <= 64) and
+// the KSK split into byte planes K[m][j] = sum_b 2^(8b) K_b[m][j], K_b in [0, 256):
+//   sum_m D K = sum_b 2^(8b) (D (K_b - 128) + 128 rowsum(D))          (mod 2^64)
+// so each plane is an exact int8 x int8 -> int32 product (v_mfma_i32_32x32x32_i8; |partial| <
+// M 2^(beta-1) 128 < 2^31 is checked), and the u64 result is recombined in the epilogue.
+// KSK planes are repacked once at upload: Kt[b][j][m] = (int8)(byte_b(K[m][j]) - 128), column-
+// major so a lane's 16 consecutive k of one column are one 16-B load.  Layout of the MFMA
+// operands (probed on gfx950, scripts/probes/mfma_i8_probe.hip): lane l, r = l & 31, h = l >> 5
+// holds A[r][16h + j] and B[16h + j][r] (j = 0..15); C/D col = r, row = (reg&3) + 8(reg>>2) + 4h.
+// ---------------------------------------------------------------------------------------
+typedef int ks_v4i __attribute__((ext_vector_type(4)));
+typedef int ks_v16i __attribute__((ext_vector_type(16)));
+
+__global__ void __launch_bounds__(256) ksk_repack_kernel(const uint64_t *__restrict__ ksk, int8_t *__restrict__ kt,
+                                                         size_t rows, size_t cols, size_t mpad, size_t jpad) {
+    const size_t e = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= rows * cols) return;
+    const size_t m = e / cols, j = e % cols;
+    const uint64_t v = ksk[e];
+#pragma unroll
+    for (int b = 0; b < 8; b++) kt[((size_t)b * jpad + j) * mpad + m] = (int8_t)(uint8_t)(((v >> (8 * b)) & 0xff) ^ 0x80);
+}
+
+// one workgroup per ciphertext: digits D[c][i*L + l] (levels L..1 as the KSK rows) and rowsum
+__global__ void __launch_bounds__(256) ks_digits_kernel(KeyswitchLaunch a, int8_t *__restrict__ dig,
+                                                        int *__restrict__ rowsum, size_t mpad) {
+    __shared__ int red[256];
+    const int c = blockIdx.x;
+    const int in_dim = a.in_dim, L = a.level, beta = a.base_log;
+    const uint64_t mask = (1ULL << beta) - 1;
+    const uint64_t *x = a.lwe_in + (size_t)c * (in_dim + 1);
+    int8_t *d = dig + (size_t)c * mpad;
+    int sum = 0;
+    for (int i = threadIdx.x; i < in_dim; i += 256) {
+        uint64_t state = closest_repr(x[i], beta, L) >> (64 - beta * L);
+        for (int l = 0; l < L; l++) {
+            uint64_t res = state & mask;
+            state >>= beta;
+            uint64_t carry = ((res - 1) | state) & res;
+            carry >>= beta - 1;
+            state += carry;
+            const int v = (int)(int64_t)(res - (carry << beta));
+            d[(size_t)i * L + l] = (int8_t)v;
+            sum += v;
+        }
+    }
+    for (size_t m = (size_t)in_dim * L + threadIdx.x; m < mpad; m += 256) d[m] = 0;
+    red[threadIdx.x] = sum;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) rowsum[c] = red[0];
+}
+
+// workgroup tile: 64 ciphertexts x 64 output columns, 4 waves of 32 x 32, 8 byte planes each
+__global__ void __launch_bounds__(256) ks_mfma_kernel(KeyswitchLaunch a, const int8_t *__restrict__ dig,
+                                                      const int *__restrict__ rowsum,
+                                                      const int8_t *__restrict__ kt, size_t mpad, size_t jpad,
+                                                      int cpad) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int c0 = blockIdx.y * 64 + 32 * (wave >> 1);
+    const int j0 = blockIdx.x * 64 + 32 * (wave & 1);
+    const int8_t *pa = dig + (size_t)(c0 + r) * mpad + 16 * h;
+    const int8_t *pb = kt + (size_t)(j0 + r) * mpad + 16 * h;
+    const size_t plane = jpad * mpad;
+    ks_v16i acc[8];
+#pragma unroll
+    for (int b = 0; b < 8; b++)
+#pragma unroll
+        for (int q = 0; q < 16; q++) acc[b][q] = 0;
+    for (size_t k = 0; k < mpad; k += 32) {
+        const ks_v4i av = *reinterpret_cast<const ks_v4i *>(pa + k);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            const ks_v4i bv = *reinterpret_cast<const ks_v4i *>(pb + (size_t)b * plane + k);
+            acc[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv, acc[b], 0, 0, 0);
+        }
+    }
+    const int j = j0 + r;
+    if (j > a.out_dim) return;
+    const size_t in_stride = (size_t)a.in_dim + 1, out_stride = (size_t)a.out_dim + 1;
+    // sum_b 2^(8b) * 128 = 128 * 0x0101010101010101 (mod 2^64)
+    constexpr uint64_t kOffset = 0x8080808080808080ULL;
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int c = c0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (c >= a.count) continue;
+        uint64_t v = (uint64_t)(int64_t)rowsum[c] * kOffset;
+#pragma unroll
+        for (int b = 0; b < 8; b++) v += (uint64_t)(int64_t)acc[b][q] << (8 * b);
+        const uint64_t body = (j == a.out_dim) ? a.lwe_in[(size_t)c * in_stride + a.in_dim] : 0;
+        a.lwe_out[(size_t)c * out_stride + j] = body - v;
+    }
+    (void)cpad;
+}
+
+size_t ks_mfma_rows(int in_dim, int level) { return ((size_t)in_dim * level + 31) / 32 * 32; }
+size_t ks_mfma_cols(int out_dim) { return ((size_t)out_dim + 1 + 63) / 64 * 64; }
+
+bool ks_mfma_supported(int in_dim, int level, int base_log) {
+    // |partial| <= M * 2^(beta-1) * 128 must stay below 2^31
+    return base_log <= 7 && (double)ks_mfma_rows(in_dim, level) * (double)(1 << (base_log - 1)) * 128.0 < 2147483648.0;
+}
+
+size_t ks_mfma_scratch_bytes(int in_dim, int level, int count) {
+    const size_t cp = ((size_t)count + 63) / 64 * 64;
+    return cp * ks_mfma_rows(in_dim, level) + cp * sizeof(int) + 256;
+}
+
+hipError_t launch_ksk_repack(const uint64_t *ksk, int8_t *kt, int in_dim, int level, int out_dim, hipStream_t s) {
+    const size_t rows = (size_t)in_dim * level, cols = (size_t)out_dim + 1;
+    const size_t mpad = ks_mfma_rows(in_dim, level), jpad = ks_mfma_cols(out_dim);
+    hipError_t e = hipMemsetAsync(kt, 0, 8 * mpad * jpad, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(ksk_repack_kernel, dim3((unsigned)((rows * cols + 255) / 256)), dim3(256), 0, s, ksk, kt, rows,
+                       cols, mpad, jpad);
+    return hipGetLastError();
+}
+
+hipError_t launch_keyswitch_mfma(const KeyswitchLaunch &a, const int8_t *kt, void *scratch, hipStream_t s) {
+    if (a.count == 0) return hipSuccess;
+    if (!ks_mfma_supported(a.in_dim, a.level, a.base_log)) return hipErrorInvalidValue;
+    const size_t mpad = ks_mfma_rows(a.in_dim, a.level), jpad = ks_mfma_cols(a.out_dim);
+    const int cpad = (a.count + 63) / 64 * 64;
+    int8_t *dig = reinterpret_cast<int8_t *>(scratch);
+    int *rowsum = reinterpret_cast<int *>(reinterpret_cast<char *>(scratch) + (((size_t)cpad * mpad + 255) / 256) * 256);
+    if (cpad > a.count) {
+        hipError_t e = hipMemsetAsync(dig + (size_t)a.count * mpad, 0, (size_t)(cpad - a.count) * mpad, s);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(ks_digits_kernel, dim3(a.count), dim3(256), 0, s, a, dig, rowsum, mpad);
+    hipLaunchKernelGGL(ks_mfma_kernel, dim3((unsigned)(jpad / 64), (unsigned)(cpad / 64)), dim3(256), 0, s, a, dig,
+                       rowsum, kt, mpad, jpad, cpad);
+    return hipGetLastError();
+}
+
 hipError_t launch_keyswitch(const KeyswitchLaunch &a, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
     if (a.level > KS_MAXL || a.base_log * a.level >= 64 || a.base_log > 7) return hipErrorInvalidValue;
