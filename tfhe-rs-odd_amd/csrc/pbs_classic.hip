@@ -33,18 +33,31 @@ namespace tfhe_mi355 {
 #ifndef PBS_CPW
 #define PBS_CPW 1
 #endif
-template <int N>
+#ifndef PBS_GGSW_LDS
+#define PBS_GGSW_LDS 0  // measured 2% slower than streaming from L2 (CPW=2 couples 4 waves); kept as an option
+#endif
+template <int N, int K, int L>
 struct PbsConfig {
-    static constexpr int CPW = PBS_CPW;  // ciphertexts per workgroup
+    static constexpr int M = N / 2;
+    static constexpr size_t GGSW_ELEMS = (size_t)L * (K + 1) * (K + 1) * M;  // double2 per GGSW
+    // GGSW_i staged in LDS by async global->LDS loads and shared by the workgroup's ciphertexts;
+    // fits next to the tables and 2 x (k+1) exchange buffers when it is <= 64 KiB
+    static constexpr bool STAGE = PBS_GGSW_LDS && GGSW_ELEMS * 16 <= 65536;
+    static constexpr int CPW = STAGE ? 2 : PBS_CPW;  // ciphertexts per workgroup
+    static constexpr size_t lds_bytes() {
+        return PbsLds<M>::bytes((K + 1) * CPW) + (STAGE ? GGSW_ELEMS * 16 : 0);
+    }
 };
 
 template <int N, int K, int L>
-__global__ void __launch_bounds__(64 * (K + 1) * PbsConfig<N>::CPW, PBS_WAVES_PER_EU)
+__global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), PBS_WAVES_PER_EU)
     pbs_classic_kernel(ClassicPbsLaunch a) {
     constexpr int M = N / 2;
     constexpr int V = M / 64;
     constexpr int LOG2N = ilog2(N);
-    constexpr int CPW = PbsConfig<N>::CPW;
+    using Cfg = PbsConfig<N, K, L>;
+    constexpr int CPW = Cfg::CPW;
+    constexpr bool STAGE = Cfg::STAGE;
     using Fft = WaveFft<M>;
     using Lay = PbsLds<M>;
     constexpr int XL = Lay::XL;
@@ -87,6 +100,10 @@ __global__ void __launch_bounds__(64 * (K + 1) * PbsConfig<N>::CPW, PBS_WAVES_PE
     cx *xb = xct + wave * XL;
     uint64_t *xb64 = reinterpret_cast<uint64_t *>(xb);
     const uint64_t *in = a.lwe_in + (size_t)ct * (n + 1);
+    // the input row is read-only for the whole launch: constant address space -> s_load
+    const __attribute__((address_space(4))) uint64_t *in_s = (const __attribute__((address_space(4))) uint64_t *)(
+        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)in >> 32)) << 32) |
+        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)in));
     const uint32_t li = a.lut_indexes ? a.lut_indexes[ct] : 0u;
     const uint64_t *lut = a.luts + (size_t)li * (K + 1) * N + (size_t)wave * N;
 
@@ -108,6 +125,31 @@ __global__ void __launch_bounds__(64 * (K + 1) * PbsConfig<N>::CPW, PBS_WAVES_PE
 
     constexpr size_t ggsw_stride = (size_t)L * (K + 1) * (K + 1) * M;
     const double2 *gcol = a.fbsk + (size_t)wave * M + lane;  // column c = wave, this lane
+    // staged GGSW: LDS image identical to the global one (lane-linear 1 KiB chunks)
+    double2 *s_ggsw = lds + Lay::xbuf_off + (size_t)CPW * (K + 1) * XL;
+    // The LDS-DMA is issued from inline asm: issued through the builtin, hipcc makes every later
+    // LDS read wait vmcnt(0) (it cannot prove the DMA target disjoint), which drains the prefetch
+    // at the first FFT twiddle read.  Hidden from it, the copy is retired explicitly before the
+    // barrier that precedes its reader (stage_ggsw_wait); the loop issues no other vector loads.
+    const uint32_t s_ggsw_addr = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char *)(s_ggsw));
+    auto stage_ggsw = [&](int i) {
+        const double2 *src = a.fbsk + (size_t)i * ggsw_stride + lane0;
+        for (int q = wid; q < (int)(ggsw_stride / 64); q += CPW * (K + 1)) {
+            const uint32_t dst = __builtin_amdgcn_readfirstlane(s_ggsw_addr + (uint32_t)q * 1024u);
+            uint32_t keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\t"
+                "s_mov_b32 m0, %2\n\t"
+                "s_nop 0\n\t"
+                "global_load_lds_dwordx4 %1, off\n\t"
+                "s_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(src + q * 64), "s"(dst)
+                : "memory");
+        }
+    };
+    auto stage_ggsw_wait = [&]() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+    if constexpr (STAGE) stage_ggsw(0);  // drained by the first spectrum-publish barrier
 
     for (int i = 0; i < n; i++) {
         // Every LDS/GGSW address below is a function of the lane only (loop invariant); hoisted
@@ -115,10 +157,12 @@ __global__ void __launch_bounds__(64 * (K + 1) * PbsConfig<N>::CPW, PBS_WAVES_PE
         // lane id makes them cheap per-iteration recomputations instead.
         int lane = lane0;
         asm volatile("" : "+v"(lane));
-        const uint32_t at = pbs_modulus_switch<LOG2N>(in[i]);
+        // mask element through the scalar unit: an s_load waits on lgkmcnt, never on the vmcnt
+        // that the GGSW LDS-DMA occupies
+        const uint32_t at = pbs_modulus_switch<LOG2N>(in_s[i]);
         const bool full_odd = (at / N) & 1;
         const int rem = at % N;
-        const double2 *ggsw = gcol + (size_t)i * ggsw_stride;
+        const double2 *ggsw = STAGE ? s_ggsw + (size_t)wave * M + lane : gcol + (size_t)i * ggsw_stride;
 
         // ct1 = X^{a~} ct0 - ct0 (polynomial_algorithms.rs:425-490) through the LDS buffer
         // (wave-private: the other waves' last reads of it ended at the post-MAC barrier)
@@ -166,6 +210,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PbsConfig<N>::CPW, PBS_WAVES_PE
 #pragma unroll
             for (int s = 0; s < V; s++)
                 reinterpret_cast<double2 *>(xb)[s * 64 + lane] = make_double2(v[s].re, v[s].im);
+            if constexpr (STAGE) stage_ggsw_wait();  // this wave's part of GGSW_i has landed
             sync();
             // output column c = wave: sum_r F_r * G[lvl][r][c]   (ggsw.rs:524-567, update_with_fmadd)
             const double2 *lm = ggsw + (size_t)(lvl - 1) * (K + 1) * (K + 1) * M;
@@ -195,7 +240,12 @@ __global__ void __launch_bounds__(64 * (K + 1) * PbsConfig<N>::CPW, PBS_WAVES_PE
                 if constexpr (L > 1) acc[s] = o;
                 else v[s] = o;
             }
-            sync();  // every wave is done reading the published spectra before xb is reused
+            sync();  // every wave is done reading the published spectra (and the staged GGSW)
+            if constexpr (STAGE) {
+                // prefetch GGSW_{i+1} into LDS: overlaps the inverse FFT, the rotation and the
+                // forward FFT; the next publish barrier (its vmcnt(0)) retires it
+                if (lvl == 1 && i + 1 < n) stage_ggsw(i + 1);
+            }
             if constexpr (L == 1) {
                 Fft::inverse(v, xb, tw, lane, wsync);
 #pragma unroll
@@ -232,8 +282,8 @@ __global__ void __launch_bounds__(64 * (K + 1) * PbsConfig<N>::CPW, PBS_WAVES_PE
 template <int N, int K, int L>
 static hipError_t launch_pbs_t(const ClassicPbsLaunch &a, hipStream_t s) {
     constexpr int M = N / 2;
-    constexpr int CPW = PbsConfig<N>::CPW;
-    const size_t lds = PbsLds<M>::bytes((K + 1) * CPW);
+    constexpr int CPW = PbsConfig<N, K, L>::CPW;
+    const size_t lds = PbsConfig<N, K, L>::lds_bytes();
     if (a.count == 0) return hipSuccess;
     const int blocks = (a.count + CPW - 1) / CPW;
     hipLaunchKernelGGL((pbs_classic_kernel<N, K, L>), dim3(blocks), dim3(64 * (K + 1) * CPW), lds, s, a);
