@@ -281,7 +281,6 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), PBS_
 
 template <int N, int K, int L>
 static hipError_t launch_pbs_t(const ClassicPbsLaunch &a, hipStream_t s) {
-    constexpr int M = N / 2;
     constexpr int CPW = PbsConfig<N, K, L>::CPW;
     const size_t lds = PbsConfig<N, K, L>::lds_bytes();
     if (a.count == 0) return hipSuccess;
