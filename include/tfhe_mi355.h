@@ -108,6 +108,41 @@ int tfhe_mi355_programmable_bootstrap_async(TfheMi355Context *ctx, const uint64_
                                             size_t lut_count, const uint32_t *d_lut_indexes,
                                             size_t count, void *stream);
 
+/* Batched blind rotation WITHOUT sample extraction: glwe_out[c] = the rotated accumulator
+ * ((k+1)*N words, GLWE layout) of lwe_in[c] with LUT luts[lut_indexes ? lut_indexes[c] : 0].
+ * Replaces the fork's FourierLweBootstrapKeyView::bootstrap_without_sample_extract
+ * (fft64/crypto/bootstrap.rs:383-412), the first step of its multi-value bootstrapping.
+ * Classic and multi-bit contexts with N <= 2048. */
+int tfhe_mi355_blind_rotate(TfheMi355Context *ctx, const uint64_t *lwe_in, uint64_t *glwe_out,
+                            const uint64_t *luts, size_t lut_count, const uint32_t *lut_indexes, size_t count);
+int tfhe_mi355_blind_rotate_async(TfheMi355Context *ctx, const uint64_t *d_lwe_in, uint64_t *d_glwe_out,
+                                  const uint64_t *d_luts, size_t lut_count, const uint32_t *d_lut_indexes,
+                                  size_t count, void *stream);
+
+/* LWE -> GLWE packing keyswitch of the fork's tree bootstrapping (gadget ServerKey
+ * lwe_packing_keyswitch_key, gadget/engine/bootstrapping.rs:345-352, used at :713,:744).
+ * Key layout [k*N][level][(k+1)*N] (levels stored L..1), input key = the big LWE key.
+ * Replaces keyswitch_lwe_ciphertext_into_glwe_ciphertext (lwe_packing_keyswitch.rs:102-186):
+ * lwe_in count x (k*N+1) -> glwe_out count x (k+1)*N. */
+int tfhe_mi355_packing_keyswitch_key_upload(TfheMi355Context *ctx, const uint64_t *pksk, size_t len,
+                                            uint32_t base_log, uint32_t level);
+int tfhe_mi355_packing_keyswitch(TfheMi355Context *ctx, const uint64_t *lwe_in, uint64_t *glwe_out, size_t count);
+int tfhe_mi355_packing_keyswitch_async(TfheMi355Context *ctx, const uint64_t *d_lwe_in, uint64_t *d_glwe_out,
+                                       size_t count, void *stream);
+
+/* GLWE x plaintext-polynomial products over (Z/2^64)[X]/(X^N+1):
+ *   out[c][i] = sum_{j < glwe_per_item} glwe_in[c][j] * polys[i][j]   (each GLWE polynomial)
+ * glwe_in [count][glwe_per_item][(k+1)N], polys [npoly][glwe_per_item][N],
+ * out [count][npoly][(k+1)N], or [count][npoly][k*N+1] when extract != 0 (degree-0 sample
+ * extraction of each product).  Replaces the fork's MVB products v0 * v_i + extraction
+ * (gadget/engine/bootstrapping.rs:567-620, polynomial_karatsuba_wrapping_mul at
+ * polynomial_algorithms.rs:683-742) and the window sums of pack_into_new_accumulator (:690-773). */
+int tfhe_mi355_glwe_poly_mul(TfheMi355Context *ctx, const uint64_t *glwe_in, size_t glwe_per_item,
+                             const uint64_t *polys, size_t npoly, size_t count, int extract, uint64_t *out);
+int tfhe_mi355_glwe_poly_mul_async(TfheMi355Context *ctx, const uint64_t *d_glwe_in, size_t glwe_per_item,
+                                   const uint64_t *d_polys, size_t npoly, size_t count, int extract,
+                                   uint64_t *d_out, void *stream);
+
 /* Batched LWE keyswitch (big key -> small key): lwe_in count x (k*N+1) -> lwe_out count x (n+1).
  * Replaces keyswitch_lwe_ciphertext (lwe_keyswitch.rs:96-170). */
 int tfhe_mi355_keyswitch(TfheMi355Context *ctx, const uint64_t *lwe_in, uint64_t *lwe_out, size_t count);
@@ -169,6 +204,11 @@ int tfhe_mi355_client_gen_multi_bit_bootstrap_key(uint64_t seed, const uint64_t 
 int tfhe_mi355_client_gen_keyswitch_key(uint64_t seed, const uint64_t *in_sk, uint32_t in_dim,
                                         const uint64_t *out_sk, uint32_t out_dim, uint32_t base_log,
                                         uint32_t level, double std_dev, uint64_t *ksk);
+/* packing KSK [in_dim][level][(k+1)N] (lwe_packing_keyswitch_key_generation.rs:74-149) */
+int tfhe_mi355_client_gen_packing_keyswitch_key(uint64_t seed, const uint64_t *in_sk, uint32_t in_dim,
+                                                const uint64_t *glwe_sk, uint32_t k, uint32_t N,
+                                                uint32_t base_log, uint32_t level, double std_dev,
+                                                uint64_t *pksk, uint32_t threads);
 int tfhe_mi355_client_lwe_encrypt(uint64_t seed, const uint64_t *sk, uint32_t n, const uint64_t *plaintexts,
                                   size_t count, double std_dev, uint64_t *cts);
 int tfhe_mi355_client_lwe_decrypt(const uint64_t *sk, uint32_t n, const uint64_t *cts, size_t count,

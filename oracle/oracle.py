@@ -69,11 +69,19 @@ def lib():
         L.orc_fbsk_copy.argtypes = [ctypes.c_void_p, f64p]
         L.orc_pbs_batch.argtypes = [ctypes.c_void_p, u64p, u64p, u64p, u32p, ctypes.c_size_t,
                                     ctypes.c_int]
+        L.orc_blind_rotate_batch.argtypes = [ctypes.c_void_p, u64p, u64p, u64p, u32p, ctypes.c_size_t,
+                                             ctypes.c_int]
         L.orc_keyswitch_batch.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, u64p, u64p, ctypes.c_size_t]
         L.orc_mono_spectrum.argtypes = [ctypes.c_int, ctypes.c_uint32, f64p]
         L.orc_fft_forward_integer.argtypes = [ctypes.c_int, u64p, f64p]
         L.orc_pos_freq.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.orc_gen_pksk.argtypes = [ctypes.c_uint64, u64p, ctypes.c_int, u64p, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_int, ctypes.c_double, u64p]
+        L.orc_packing_keyswitch_batch.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                  ctypes.c_int, u64p, u64p, ctypes.c_size_t]
+        L.orc_glwe_poly_mul.argtypes = [ctypes.c_int, ctypes.c_int, u64p, ctypes.c_size_t, u64p,
+                                        ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, u64p]
         if hasattr(L, "orc_mb_pbs_batch"):
             L.orc_mb_fbsk_create.restype = ctypes.c_void_p
             L.orc_mb_fbsk_create.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -281,11 +289,55 @@ class MultiBitFourierBsk:
         return out
 
 
+def _fbsk_blind_rotate(self, lwe_in, luts, lut_idx=None, threads=8) -> np.ndarray:
+    lwe_in = _u64(lwe_in).reshape(-1, self.n + 1)
+    luts = _u64(luts)
+    cnt = lwe_in.shape[0]
+    out = np.zeros((cnt, (self.k + 1) * self.N), dtype=np.uint64)
+    idx = None if lut_idx is None else np.ascontiguousarray(lut_idx, dtype=np.uint32)
+    lib().orc_blind_rotate_batch(self.h, _p(lwe_in), _p(out), _p(luts),
+                                 idx.ctypes.data_as(u32p) if idx is not None else None, cnt, threads)
+    return out
+
+
+FourierBsk.blind_rotate = _fbsk_blind_rotate
+
+
 def keyswitch(ksk, in_dim, out_dim, base_log, level, lwe_in) -> np.ndarray:
     lwe_in = _u64(lwe_in).reshape(-1, in_dim + 1)
     out = np.zeros((lwe_in.shape[0], out_dim + 1), dtype=np.uint64)
     lib().orc_keyswitch_batch(_p(_u64(ksk)), in_dim, out_dim, base_log, level, _p(lwe_in),
                               _p(out), lwe_in.shape[0])
+    return out
+
+
+def gen_pksk(seed, in_sk, glwe_sk, k, N, base_log, level, std) -> np.ndarray:
+    in_sk, glwe_sk = _u64(in_sk), _u64(glwe_sk)
+    out = np.zeros(len(in_sk) * level * (k + 1) * N, dtype=np.uint64)
+    lib().orc_gen_pksk(seed, _p(in_sk), len(in_sk), _p(glwe_sk), k, N, base_log, level, std, _p(out))
+    return out
+
+
+def packing_keyswitch(pksk, in_dim, k, N, base_log, level, lwe_in) -> np.ndarray:
+    x = _u64(lwe_in).reshape(-1, in_dim + 1)
+    out = np.zeros((len(x), (k + 1) * N), dtype=np.uint64)
+    lib().orc_packing_keyswitch_batch(_p(_u64(pksk)), in_dim, k, N, base_log, level, _p(x), _p(out), len(x))
+    return out
+
+
+def glwe_poly_mul(k, N, glwe_in, polys, extract: bool) -> np.ndarray:
+    """glwe_in [count][J][(k+1)N], polys [npoly][J][N] -> [count][npoly][(k+1)N or kN+1]."""
+    g = _u64(glwe_in)
+    v = _u64(polys)
+    if g.ndim == 2:
+        g = g.reshape(g.shape[0], 1, -1)
+    if v.ndim == 2:
+        v = v.reshape(v.shape[0], 1, -1)
+    count, J = g.shape[0], g.shape[1]
+    npoly = v.shape[0]
+    assert v.shape[1] == J and v.shape[2] == N and g.shape[2] == (k + 1) * N
+    out = np.zeros((count, npoly, k * N + 1 if extract else (k + 1) * N), dtype=np.uint64)
+    lib().orc_glwe_poly_mul(k, N, _p(g), J, _p(v), npoly, count, int(extract), _p(out))
     return out
 
 
@@ -321,3 +373,21 @@ class OracleEngine:
 
     def keyswitch_programmable_bootstrap(self, x, luts, lut_indexes=None):
         return self.fb.pbs(self.keyswitch(x), luts, lut_indexes, threads=self.threads)
+
+    def programmable_bootstrap(self, x, luts, lut_indexes=None):
+        return self.fb.pbs(x, luts, lut_indexes, threads=self.threads)
+
+    def blind_rotate(self, x, luts, lut_indexes=None):
+        return self.fb.blind_rotate(x, luts, lut_indexes, threads=self.threads)
+
+    def upload_packing_keyswitch_key(self, pksk, base_log, level):
+        self.pksk, self.pks = np.ascontiguousarray(pksk, dtype=np.uint64), (base_log, level)
+
+    def packing_keyswitch(self, x):
+        p = self.p
+        return packing_keyswitch(self.pksk, p.big_lwe_dimension, p.glwe_dimension, p.polynomial_size,
+                                 self.pks[0], self.pks[1], x)
+
+    def glwe_poly_mul(self, glwe_in, polys, extract=False):
+        p = self.p
+        return glwe_poly_mul(p.glwe_dimension, p.polynomial_size, glwe_in, polys, extract)

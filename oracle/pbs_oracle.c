@@ -739,6 +739,81 @@ void orc_gen_ksk(uint64_t seed, const uint64_t *in_sk, int in_dim, const uint64_
     }
 }
 
+/* LWE -> GLWE packing KSK (lwe_packing_keyswitch_key_generation.rs:74-149): block i, level
+ * lvl = L..1 is a GLWE encryption of the constant polynomial in_sk[i] * 2^(64 - base_log*lvl);
+ * layout [in][L][(k+1)N]; input coefficient i draws from RNG stream 0x5000000 + i. */
+void orc_gen_pksk(uint64_t seed, const uint64_t *in_sk, int in_dim, const uint64_t *glwe_sk, int k, int N,
+                  int base_log, int level, double std, uint64_t *pksk) {
+    size_t glwe_len = (size_t)(k + 1) * N;
+    for (int i = 0; i < in_dim; i++) {
+        orc_rng r;
+        rng_seed(&r, seed, 0x5000000ULL + (uint64_t)i);
+        for (int l = 0; l < level; l++) {
+            int lvl = level - l;
+            uint64_t *g = pksk + ((size_t)i * level + l) * glwe_len;
+            memset(g + (size_t)k * N, 0, sizeof(uint64_t) * N);
+            g[(size_t)k * N] = in_sk[i] << (64 - base_log * lvl);
+            glwe_encrypt_assign(&r, g, glwe_sk, k, N, std);
+        }
+    }
+}
+
+/* keyswitch_lwe_ciphertext_into_glwe_ciphertext (lwe_packing_keyswitch.rs:102-186): output
+ * zeroed, GLWE body[0] = LWE body, then minus sum of signed digits times the key GLWEs. */
+void orc_packing_keyswitch_batch(const uint64_t *pksk, int in_dim, int k, int N, int base_log, int level,
+                                 const uint64_t *in, uint64_t *out, size_t count) {
+    uint64_t mask = (1ULL << base_log) - 1;
+    size_t glwe_len = (size_t)(k + 1) * N;
+    for (size_t c = 0; c < count; c++) {
+        const uint64_t *x = in + c * (size_t)(in_dim + 1);
+        uint64_t *o = out + c * glwe_len;
+        memset(o, 0, sizeof(uint64_t) * glwe_len);
+        o[(size_t)k * N] = x[in_dim];
+        for (int i = 0; i < in_dim; i++) {
+            uint64_t state = orc_closest_representable(x[i], base_log, level) >> (64 - base_log * level);
+            for (int l = 0; l < level; l++) {
+                uint64_t d = decompose_one_level(base_log, &state, mask);
+                if (!d) continue;
+                const uint64_t *row = pksk + ((size_t)i * level + l) * glwe_len;
+                for (size_t j = 0; j < glwe_len; j++) o[j] -= d * row[j];
+            }
+        }
+    }
+}
+
+/* out[c][i] = sum_j glwe_in[c][j] * polys[i][j] per GLWE polynomial (schoolbook negacyclic
+ * product, polynomial_wrapping_add_mul_assign semantics), then optionally
+ * extract_lwe_sample_from_glwe_ciphertext at degree 0. */
+void orc_glwe_poly_mul(int k, int N, const uint64_t *glwe_in, size_t J, const uint64_t *polys, size_t npoly,
+                       size_t count, int extract, uint64_t *out) {
+    size_t glwe_len = (size_t)(k + 1) * N;
+    size_t out_len = extract ? (size_t)k * N + 1 : glwe_len;
+    uint64_t *acc = malloc(sizeof(uint64_t) * glwe_len);
+    for (size_t c = 0; c < count; c++)
+        for (size_t i = 0; i < npoly; i++) {
+            memset(acc, 0, sizeof(uint64_t) * glwe_len);
+            for (size_t j = 0; j < J; j++) {
+                const uint64_t *g = glwe_in + (c * J + j) * glwe_len;
+                const uint64_t *v = polys + (i * J + j) * (size_t)N;
+                for (int t = 0; t < N; t++) {
+                    if (!v[t]) continue;
+                    for (int p = 0; p <= k; p++) {
+                        const uint64_t *a = g + (size_t)p * N;
+                        uint64_t *o = acc + (size_t)p * N;
+                        for (int m = 0; m < t; m++) o[m] -= v[t] * a[m - t + N];
+                        for (int m = t; m < N; m++) o[m] += v[t] * a[m - t];
+                    }
+                }
+            }
+            uint64_t *dst = out + (c * npoly + i) * out_len;
+            if (extract)
+                sample_extract0(acc, dst, k, N);
+            else
+                memcpy(dst, acc, sizeof(uint64_t) * glwe_len);
+        }
+    free(acc);
+}
+
 void orc_lwe_encrypt_batch(uint64_t seed, const uint64_t *sk, int n, const uint64_t *pts, size_t count,
                            double std, uint64_t *cts) {
     orc_rng r;
@@ -885,7 +960,7 @@ static void external_product_add(const orc_fbsk *b, const cplx *ggsw, uint64_t *
  * bootstrap (bootstrap.rs:346-380) = blind_rotate_assign (bootstrap.rs:243-344, without the
  * fork's PATTERN noise dump) + sample extract at degree 0. */
 static void pbs_one(const orc_fbsk *b, const uint64_t *lwe_in, uint64_t *lwe_out, const uint64_t *lut,
-                    uint64_t *acc, pbs_scratch *s) {
+                    uint64_t *acc, pbs_scratch *s, int glwe_out) {
     int n = b->n, k = b->k, N = b->N, M = N / 2;
     int log2N = 0;
     while ((1 << log2N) < N) log2N++;
@@ -899,7 +974,10 @@ static void pbs_one(const orc_fbsk *b, const uint64_t *lwe_in, uint64_t *lwe_out
             monomial_mul_sub(s->ct1 + (size_t)p * N, acc + (size_t)p * N, N, at);
         external_product_add(b, b->fourier + (size_t)i * ggsw_len, acc, s->ct1, s);
     }
-    sample_extract0(acc, lwe_out, k, N);
+    if (glwe_out) /* bootstrap_without_sample_extract (fork, bootstrap.rs:383-412) */
+        memcpy(lwe_out, acc, sizeof(uint64_t) * (size_t)(k + 1) * N);
+    else
+        sample_extract0(acc, lwe_out, k, N);
 }
 
 typedef struct {
@@ -910,6 +988,7 @@ typedef struct {
     size_t count;
     size_t next;
     pthread_mutex_t mu;
+    int glwe_out;
 } pbs_job;
 
 static void *pbs_worker(void *arg) {
@@ -925,8 +1004,9 @@ static void *pbs_worker(void *arg) {
         pthread_mutex_unlock(&J->mu);
         if (c >= J->count) break;
         size_t li = J->lut_idx ? J->lut_idx[c] : 0;
-        pbs_one(b, J->in + c * (size_t)(b->n + 1), J->out + c * (size_t)(k * N + 1),
-                J->luts + li * (size_t)(k + 1) * N, acc, &s);
+        const size_t out_len = J->glwe_out ? (size_t)(k + 1) * N : (size_t)(k * N + 1);
+        pbs_one(b, J->in + c * (size_t)(b->n + 1), J->out + c * out_len, J->luts + li * (size_t)(k + 1) * N, acc, &s,
+                J->glwe_out);
     }
     free(acc);
     scratch_free(&s);
@@ -934,9 +1014,10 @@ static void *pbs_worker(void *arg) {
 }
 
 /* Batched PBS, one ciphertext per thread (mirrors pbs_bench.rs:430-549 par_iter). */
-void orc_pbs_batch(const void *fbsk, const uint64_t *in, uint64_t *out, const uint64_t *luts,
-                   const uint32_t *lut_idx, size_t count, int threads) {
+static void pbs_batch(const void *fbsk, const uint64_t *in, uint64_t *out, const uint64_t *luts,
+                      const uint32_t *lut_idx, size_t count, int threads, int glwe_out) {
     pbs_job J = {fbsk, in, luts, lut_idx, out, count, 0};
+    J.glwe_out = glwe_out;
     pthread_mutex_init(&J.mu, NULL);
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;
@@ -944,6 +1025,17 @@ void orc_pbs_batch(const void *fbsk, const uint64_t *in, uint64_t *out, const ui
     for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, pbs_worker, &J);
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
     pthread_mutex_destroy(&J.mu);
+}
+
+void orc_pbs_batch(const void *fbsk, const uint64_t *in, uint64_t *out, const uint64_t *luts,
+                   const uint32_t *lut_idx, size_t count, int threads) {
+    pbs_batch(fbsk, in, out, luts, lut_idx, count, threads, 0);
+}
+
+/* blind rotation without sample extraction: out = [count][(k+1)N] */
+void orc_blind_rotate_batch(const void *fbsk, const uint64_t *in, uint64_t *out, const uint64_t *luts,
+                            const uint32_t *lut_idx, size_t count, int threads) {
+    pbs_batch(fbsk, in, out, luts, lut_idx, count, threads, 1);
 }
 
 /* ------------------------------------------------------------------------------------ */

@@ -88,6 +88,10 @@ struct TfheMi355Context {
     DeviceBuffer ks_scratch;   // MFMA keyswitch digits
     bool ksk_planes_ready = false;
     bool fbsk_ready = false, ksk_ready = false;
+    // LWE -> GLWE packing keyswitching key of the gadget layer (big LWE key -> GLWE key)
+    DeviceBuffer pksk, pksk_planes;
+    uint32_t pks_base_log = 0, pks_level = 0;
+    bool pksk_ready = false, pksk_planes_ready = false;
 
     size_t n() const { return p.lwe_dimension; }
     size_t k() const { return p.glwe_dimension; }
@@ -105,6 +109,7 @@ struct TfheMi355Context {
         return ggsw_count() * p.pbs_level * (k() + 1) * (k() + 1) * (N() / 2) * sizeof(double2);
     }
     size_t ksk_len() const { return big_dim() * p.ks_level * (n() + 1); }
+    size_t pksk_len(uint32_t level) const { return big_dim() * level * glwe_len(); }
 };
 
 namespace {
@@ -153,7 +158,7 @@ hipError_t convert_bsk(TfheMi355Context *c, const uint64_t *d_std, size_t npoly,
 }
 
 void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, const uint64_t *d_luts,
-                    size_t lut_count, const uint32_t *d_idx, size_t count, hipStream_t s) {
+                    size_t lut_count, const uint32_t *d_idx, size_t count, hipStream_t s, bool glwe_out = false) {
     require_fbsk(c);
     if (lut_count == 0) fail("lut_count must be >= 1");
     if (count > 0x7fffffff) fail("batch too large");
@@ -166,14 +171,17 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
         a.fbsk = reinterpret_cast<const double2 *>(c->fbsk.ptr);
         a.W = c->tables.W;
         a.twist = c->tables.twist;
+        a.twist_inv = c->tables.twist_inv;
         a.n = (int)c->n();
         a.base_log = (int)c->p.pbs_base_log;
         a.count = (int)count;
+        a.glwe_out = glwe_out;
         check(launch_multibit_pbs((int)c->N(), (int)c->k(), (int)c->p.pbs_level, (int)c->p.grouping_factor, a, s),
               "launch multi-bit pbs");
         return;
     }
     if (large_pbs_supported((int)c->N(), (int)c->k(), (int)c->p.pbs_level)) {
+        if (glwe_out) fail("blind rotation without sample extraction is not available at N = %zu", c->N());
         // ciphertexts per pass: the chunk's accumulators + spectra (1.5 MiB per ciphertext at 4_4)
         // should stay resident in the 256 MiB Infinity Cache across the two launches of a CMUX
         static const size_t kChunk = [] {
@@ -211,6 +219,7 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
     a.n = (int)c->n();
     a.base_log = (int)c->p.pbs_base_log;
     a.count = (int)count;
+    a.glwe_out = glwe_out;
     check(launch_classic_pbs((int)c->N(), (int)c->k(), (int)c->p.pbs_level, a, s), "launch pbs");
 }
 
@@ -257,6 +266,54 @@ void launch_ks_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, s
     a.level = (int)c->p.ks_level;
     a.count = (int)count;
     check(launch_keyswitch(a, s), "launch keyswitch");
+}
+
+// LWE -> GLWE packing keyswitch (lwe_packing_keyswitch.rs:102-186): the LWE keyswitch GEMM with
+// (k+1)N-word GLWE rows and the input body landing on the GLWE body's constant term
+KeyswitchLaunch packing_ks_args(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, size_t count) {
+    KeyswitchLaunch a;
+    a.lwe_in = d_in;
+    a.lwe_out = d_out;
+    a.ksk = reinterpret_cast<const uint64_t *>(c->pksk.ptr);
+    a.in_dim = (int)c->big_dim();
+    a.out_dim = (int)c->glwe_len() - 1;
+    a.body_col = (int)c->big_dim();
+    a.base_log = (int)c->pks_base_log;
+    a.level = (int)c->pks_level;
+    a.count = (int)count;
+    return a;
+}
+
+void launch_packing_ks_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, size_t count, hipStream_t s) {
+    if (!c->pksk_ready) fail("packing keyswitching key not uploaded");
+    if (count == 0) return;
+    if (count > 0x7fffffffu) fail("count too large");
+    KeyswitchLaunch a = packing_ks_args(c, d_in, d_out, count);
+    if (c->pksk_planes_ready) {
+        c->ks_scratch.reserve(ks_mfma_scratch_bytes(a.in_dim, a.level, a.count));
+        check(launch_keyswitch_mfma(a, (const int8_t *)c->pksk_planes.ptr, c->ks_scratch.ptr, s),
+              "launch mfma packing keyswitch");
+    } else {
+        check(launch_keyswitch(a, s), "launch packing keyswitch");
+    }
+}
+
+void launch_glwe_poly_mul_dev(TfheMi355Context *c, const uint64_t *d_glwe, size_t glwe_per_item,
+                              const uint64_t *d_polys, size_t npoly, size_t count, bool extract, uint64_t *d_out,
+                              hipStream_t s) {
+    if (glwe_per_item == 0 || glwe_per_item > 0xffff) fail("glwe_per_item out of range");
+    if (npoly > 0x7fffffffu) fail("npoly too large");
+    GlwePolyMulLaunch a;
+    a.glwe_in = d_glwe;
+    a.polys = d_polys;
+    a.out = d_out;
+    a.k = (int)c->k();
+    a.N = (int)c->N();
+    a.J = (int)glwe_per_item;
+    a.npoly = (int)npoly;
+    a.count = count;
+    a.extract = extract;
+    check(launch_glwe_poly_mul(a, s), "launch glwe poly mul");
 }
 
 void validate_lut_indexes(const uint32_t *idx, size_t count, size_t lut_count) {
@@ -325,7 +382,7 @@ int tfhe_mi355_context_destroy(TfheMi355Context *ctx) {
         if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
         for (DeviceBuffer *b : {&ctx->fbsk, &ctx->ksk, &ctx->std_staging, &ctx->io_in, &ctx->io_out,
                                 &ctx->io_luts, &ctx->io_idx, &ctx->io_tmp, &ctx->pbs_scratch,
-                                &ctx->ksk_planes, &ctx->ks_scratch})
+                                &ctx->ksk_planes, &ctx->ks_scratch, &ctx->pksk, &ctx->pksk_planes})
             b->release();
         if (ctx->tables.W) (void)hipFree(ctx->tables.W);
         if (ctx->tables.twist) (void)hipFree(ctx->tables.twist);
@@ -476,6 +533,136 @@ int tfhe_mi355_programmable_bootstrap_async(TfheMi355Context *ctx, const uint64_
         if (!ctx || (!d_in && count) || (!d_out && count) || !d_luts) fail("null argument");
         check(hipSetDevice(ctx->device), "hipSetDevice");
         launch_pbs_dev(ctx, d_in, d_out, d_luts, lut_count, d_idx, count, (hipStream_t)stream);
+    });
+}
+
+int tfhe_mi355_blind_rotate(TfheMi355Context *ctx, const uint64_t *lwe_in, uint64_t *glwe_out, const uint64_t *luts,
+                            size_t lut_count, const uint32_t *lut_indexes, size_t count) {
+    return guarded([&] {
+        if (!ctx || (!lwe_in && count) || (!glwe_out && count) || !luts) fail("null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        require_fbsk(ctx);
+        if (count == 0) return;
+        validate_lut_indexes(lut_indexes, count, lut_count);
+        const size_t in_b = count * (ctx->n() + 1) * 8, out_b = count * ctx->glwe_len() * 8;
+        const size_t lut_b = lut_count * ctx->glwe_len() * 8;
+        ctx->io_in.reserve(in_b);
+        ctx->io_out.reserve(out_b);
+        ctx->io_luts.reserve(lut_b);
+        if (lut_indexes) ctx->io_idx.reserve(count * 4);
+        hipStream_t s = ctx->stream;
+        check(hipMemcpyAsync(ctx->io_in.ptr, lwe_in, in_b, hipMemcpyHostToDevice, s), "H2D in");
+        check(hipMemcpyAsync(ctx->io_luts.ptr, luts, lut_b, hipMemcpyHostToDevice, s), "H2D luts");
+        if (lut_indexes)
+            check(hipMemcpyAsync(ctx->io_idx.ptr, lut_indexes, count * 4, hipMemcpyHostToDevice, s), "H2D idx");
+        launch_pbs_dev(ctx, (const uint64_t *)ctx->io_in.ptr, (uint64_t *)ctx->io_out.ptr,
+                       (const uint64_t *)ctx->io_luts.ptr, lut_count,
+                       lut_indexes ? (const uint32_t *)ctx->io_idx.ptr : nullptr, count, s, true);
+        check(hipMemcpyAsync(glwe_out, ctx->io_out.ptr, out_b, hipMemcpyDeviceToHost, s), "D2H out");
+        check(hipStreamSynchronize(s), "blind rotate sync");
+    });
+}
+
+int tfhe_mi355_blind_rotate_async(TfheMi355Context *ctx, const uint64_t *d_in, uint64_t *d_glwe_out,
+                                  const uint64_t *d_luts, size_t lut_count, const uint32_t *d_lut_indexes,
+                                  size_t count, void *stream) {
+    return guarded([&] {
+        if (!ctx || (!d_in && count) || (!d_glwe_out && count) || !d_luts) fail("null argument");
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        launch_pbs_dev(ctx, d_in, d_glwe_out, d_luts, lut_count, d_lut_indexes, count, (hipStream_t)stream, true);
+    });
+}
+
+int tfhe_mi355_packing_keyswitch_key_upload(TfheMi355Context *ctx, const uint64_t *pksk, size_t len,
+                                            uint32_t base_log, uint32_t level) {
+    return guarded([&] {
+        if (!ctx || !pksk) fail("null argument");
+        if (level == 0 || base_log == 0 || base_log * level >= 64) fail("invalid packing ks decomposition");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        if (len != ctx->pksk_len(level))
+            fail("packing keyswitching key has %zu words, expected %zu", len, ctx->pksk_len(level));
+        ctx->pksk_ready = ctx->pksk_planes_ready = false;
+        ctx->pksk.reserve(len * sizeof(uint64_t));
+        check(hipMemcpy(ctx->pksk.ptr, pksk, len * sizeof(uint64_t), hipMemcpyHostToDevice), "upload pksk");
+        ctx->pks_base_log = base_log;
+        ctx->pks_level = level;
+        const int in_dim = (int)ctx->big_dim(), out_dim = (int)ctx->glwe_len() - 1;
+        const char *no_mfma = std::getenv("TFHE_MI355_KS_NO_MFMA");
+        if (!(no_mfma && *no_mfma && *no_mfma != '0') && ks_mfma_supported(in_dim, (int)level, (int)base_log)) {
+            ctx->pksk_planes.reserve(8 * ks_mfma_rows(in_dim, (int)level) * ks_mfma_cols(out_dim));
+            check(launch_ksk_repack((const uint64_t *)ctx->pksk.ptr, (int8_t *)ctx->pksk_planes.ptr, in_dim,
+                                    (int)level, out_dim, ctx->stream),
+                  "pksk repack");
+            ctx->pksk_planes_ready = true;
+        }
+        check(hipStreamSynchronize(ctx->stream), "pksk repack sync");
+        ctx->pksk_ready = true;
+    });
+}
+
+int tfhe_mi355_packing_keyswitch(TfheMi355Context *ctx, const uint64_t *lwe_in, uint64_t *glwe_out, size_t count) {
+    return guarded([&] {
+        if (!ctx || (!lwe_in && count) || (!glwe_out && count)) fail("null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        if (!ctx->pksk_ready) fail("packing keyswitching key not uploaded");
+        if (count == 0) return;
+        const size_t in_b = count * (ctx->big_dim() + 1) * 8, out_b = count * ctx->glwe_len() * 8;
+        ctx->io_in.reserve(in_b);
+        ctx->io_out.reserve(out_b);
+        hipStream_t s = ctx->stream;
+        check(hipMemcpyAsync(ctx->io_in.ptr, lwe_in, in_b, hipMemcpyHostToDevice, s), "H2D in");
+        launch_packing_ks_dev(ctx, (const uint64_t *)ctx->io_in.ptr, (uint64_t *)ctx->io_out.ptr, count, s);
+        check(hipMemcpyAsync(glwe_out, ctx->io_out.ptr, out_b, hipMemcpyDeviceToHost, s), "D2H out");
+        check(hipStreamSynchronize(s), "packing ks sync");
+    });
+}
+
+int tfhe_mi355_packing_keyswitch_async(TfheMi355Context *ctx, const uint64_t *d_lwe_in, uint64_t *d_glwe_out,
+                                       size_t count, void *stream) {
+    return guarded([&] {
+        if (!ctx || (!d_lwe_in && count) || (!d_glwe_out && count)) fail("null argument");
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        launch_packing_ks_dev(ctx, d_lwe_in, d_glwe_out, count, (hipStream_t)stream);
+    });
+}
+
+int tfhe_mi355_glwe_poly_mul(TfheMi355Context *ctx, const uint64_t *glwe_in, size_t glwe_per_item,
+                             const uint64_t *polys, size_t npoly, size_t count, int extract, uint64_t *out) {
+    return guarded([&] {
+        if (!ctx || (!glwe_in && count) || (!polys && npoly) || (!out && count && npoly)) fail("null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        if (count == 0 || npoly == 0) return;
+        const size_t out_words = extract ? ctx->big_dim() + 1 : ctx->glwe_len();
+        const size_t in_b = count * glwe_per_item * ctx->glwe_len() * 8;
+        const size_t poly_b = npoly * glwe_per_item * ctx->N() * 8, out_b = count * npoly * out_words * 8;
+        ctx->io_in.reserve(in_b);
+        ctx->io_luts.reserve(poly_b);
+        ctx->io_out.reserve(out_b);
+        hipStream_t s = ctx->stream;
+        check(hipMemcpyAsync(ctx->io_in.ptr, glwe_in, in_b, hipMemcpyHostToDevice, s), "H2D glwe");
+        check(hipMemcpyAsync(ctx->io_luts.ptr, polys, poly_b, hipMemcpyHostToDevice, s), "H2D polys");
+        launch_glwe_poly_mul_dev(ctx, (const uint64_t *)ctx->io_in.ptr, glwe_per_item,
+                                 (const uint64_t *)ctx->io_luts.ptr, npoly, count, extract != 0,
+                                 (uint64_t *)ctx->io_out.ptr, s);
+        check(hipMemcpyAsync(out, ctx->io_out.ptr, out_b, hipMemcpyDeviceToHost, s), "D2H out");
+        check(hipStreamSynchronize(s), "glwe poly mul sync");
+    });
+}
+
+int tfhe_mi355_glwe_poly_mul_async(TfheMi355Context *ctx, const uint64_t *d_glwe_in, size_t glwe_per_item,
+                                   const uint64_t *d_polys, size_t npoly, size_t count, int extract,
+                                   uint64_t *d_out, void *stream) {
+    return guarded([&] {
+        if (!ctx || (!d_glwe_in && count) || (!d_polys && npoly) || (!d_out && count && npoly))
+            fail("null argument");
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        if (count == 0 || npoly == 0) return;
+        launch_glwe_poly_mul_dev(ctx, d_glwe_in, glwe_per_item, d_polys, npoly, count, extract != 0, d_out,
+                                 (hipStream_t)stream);
     });
 }
 

@@ -266,6 +266,40 @@ int tfhe_mi355_client_gen_keyswitch_key(uint64_t seed, const uint64_t *in_sk, ui
     });
 }
 
+// LWE -> GLWE packing keyswitching key [in_dim][level][(k+1)N], levels stored L..1: GLWE
+// encryptions of the constant polynomial in_sk[i] * 2^(64 - base_log*lvl)
+// (lwe_packing_keyswitch_key_generation.rs:74-149); input coefficient i draws from its own stream.
+int tfhe_mi355_client_gen_packing_keyswitch_key(uint64_t seed, const uint64_t *in_sk, uint32_t in_dim,
+                                                const uint64_t *glwe_sk, uint32_t k, uint32_t N,
+                                                uint32_t base_log, uint32_t level, double std, uint64_t *pksk,
+                                                uint32_t threads) {
+    return guard([&] {
+        if (!in_sk || !glwe_sk || !pksk) throw std::invalid_argument("null argument");
+        if (level == 0 || base_log == 0 || base_log * level >= 64) throw std::invalid_argument("invalid decomposition");
+        const size_t glwe_len = (size_t)(k + 1) * N;
+        std::atomic<uint32_t> next{0};
+        auto work = [&] {
+            for (;;) {
+                const uint32_t i = next++;
+                if (i >= in_dim) break;
+                Rng r(seed, 0x5000000ULL + i);
+                for (uint32_t l = 0; l < level; l++) {
+                    const uint32_t lvl = level - l;
+                    uint64_t *g = pksk + ((size_t)i * level + l) * glwe_len;
+                    std::memset(g + (size_t)k * N, 0, sizeof(uint64_t) * N);
+                    g[(size_t)k * N] = in_sk[i] << (64 - base_log * lvl);
+                    glwe_encrypt_assign(r, g, glwe_sk, (int)k, (int)N, std);
+                }
+            }
+        };
+        uint32_t nt = threads ? threads : std::max(1u, std::thread::hardware_concurrency());
+        std::vector<std::thread> th;
+        for (uint32_t t = 1; t < nt; t++) th.emplace_back(work);
+        work();
+        for (auto &t : th) t.join();
+    });
+}
+
 int tfhe_mi355_client_lwe_encrypt(uint64_t seed, const uint64_t *sk, uint32_t n, const uint64_t *pts,
                                   size_t count, double std, uint64_t *cts) {
     return guard([&] {

@@ -24,6 +24,7 @@ struct ClassicPbsLaunch {
     int n;
     int base_log;
     int count;
+    int glwe_out;                // 1: write the rotated accumulator [count][(k+1)N] (no sample extract)
 };
 
 // Returns false if (N, k, L) has no compiled specialisation.
@@ -36,10 +37,11 @@ struct MultiBitPbsLaunch {
     const uint64_t *luts;        // [lut_count][(k+1)*N]
     const uint32_t *lut_indexes; // [count] or null
     const double2 *fbsk;         // [n/g][2^g][L][k+1][k+1] polys, engine Fourier layout
-    const double2 *W, *twist;
+    const double2 *W, *twist, *twist_inv;
     int n;
     int base_log;
     int count;
+    int glwe_out;                // 1: write the rotated accumulator [count][(k+1)N] (no sample extract)
 };
 bool multibit_pbs_supported(int N, int k, int L, int g);
 hipError_t launch_multibit_pbs(int N, int k, int L, int g, const MultiBitPbsLaunch &a, hipStream_t s);
@@ -76,6 +78,10 @@ struct KeyswitchLaunch {
     const uint64_t *ksk;     // [in_dim][level][out_dim+1]
     int in_dim, out_dim, base_log, level;
     int count;
+    // output column receiving the input body: out_dim for an LWE keyswitch, k*N for the LWE ->
+    // GLWE packing keyswitch (lwe_packing_keyswitch.rs:159-161, the GLWE body's constant term)
+    int body_col = -1;
+    __host__ __device__ int body() const { return body_col < 0 ? out_dim : body_col; }
 };
 hipError_t launch_keyswitch(const KeyswitchLaunch &a, hipStream_t s);
 // int8-MFMA keyswitch: KSK repacked once into 8 byte planes (ks_mfma_cols x ks_mfma_rows each)
@@ -91,5 +97,20 @@ hipError_t launch_lwe_scalar_mul_add(uint64_t *y, const uint64_t *x, uint64_t sc
                                      size_t y_stride, size_t x_stride, hipStream_t s);
 hipError_t launch_trivial_pbs(uint64_t *body, size_t rows, size_t stride, const uint64_t *lut_body, uint64_t delta,
                               uint64_t modulus_sup, uint64_t box, hipStream_t s);
+
+// GLWE x plaintext-polynomial products (glwe_ops.hip):
+//   out[c][i] = sum_{j<J} glwe_in[c][j] * polys[i][j]   in (Z/2^64)[X]/(X^N+1), per GLWE polynomial,
+// optionally sample-extracted at degree 0.  Serves the fork's MVB products v0 * v_i
+// (gadget/engine/bootstrapping.rs:567-620) and the window sums of the tree-bootstrapping packing
+// (:690-773).  Cost scales with the polys' nonzero count.
+struct GlwePolyMulLaunch {
+    const uint64_t *glwe_in;  // [count][J][(k+1)N]
+    const uint64_t *polys;    // [npoly][J][N]
+    uint64_t *out;            // [count][npoly][(k+1)N], or [count][npoly][kN+1] when extract
+    int k, N, J, npoly;
+    size_t count;
+    bool extract;
+};
+hipError_t launch_glwe_poly_mul(const GlwePolyMulLaunch &a, hipStream_t s);
 
 }  // namespace tfhe_mi355

@@ -4,7 +4,9 @@
 // with the signed decomposer (commons/math/decomposition/decomposer.rs:99-153, iter.rs:134-141)
 // and slice_wrapping_sub_scalar_mul_assign (algorithms/slice_algorithms.rs:363).
 //
-// Shape: out[c][j] = (j == out_dim ? in[c][in_dim] : 0) - sum_{i,l} d[c][i][l] * KSK[i][l][j]
+// Shape: out[c][j] = (j == body ? in[c][in_dim] : 0) - sum_{i,l} d[c][i][l] * KSK[i][l][j]
+// (body = out_dim for an LWE output; k*N for the LWE -> GLWE packing keyswitch,
+// lwe_packing_keyswitch.rs:102-186, whose rows are (k+1)N-word GLWEs)
 // i.e. a [count x in_dim*L] x [in_dim*L x (out_dim+1)] product over Z/2^64 with tiny signed
 // digits.  A workgroup owns a 64-ciphertext x 64-column tile; every KSK row segment it loads
 // (512 B, coalesced) is reused by its 64 ciphertexts, the digits are staged in LDS per chunk
@@ -80,7 +82,7 @@ __global__ void __launch_bounds__(256) keyswitch_kernel(KeyswitchLaunch a) {
     for (int t = 0; t < KS_CPT; t++) {
         const int c = c0 + tg * KS_CPT + t;
         if (c >= a.count) break;
-        uint64_t body = (j == out_dim) ? a.lwe_in[(size_t)c * in_stride + in_dim] : 0;
+        uint64_t body = (j == a.body()) ? a.lwe_in[(size_t)c * in_stride + in_dim] : 0;
         a.lwe_out[(size_t)c * out_stride + j] = body + acc[t];
     }
 }
@@ -179,7 +181,7 @@ __global__ void __launch_bounds__(256) ks_mfma_kernel(KeyswitchLaunch a, const i
         uint64_t v = (uint64_t)(int64_t)rowsum[c] * kOffset;
 #pragma unroll
         for (int b = 0; b < 8; b++) v += (uint64_t)(int64_t)acc[b][q] << (8 * b);
-        const uint64_t body = (j == a.out_dim) ? a.lwe_in[(size_t)c * in_stride + a.in_dim] : 0;
+        const uint64_t body = (j == a.body()) ? a.lwe_in[(size_t)c * in_stride + a.in_dim] : 0;
         a.lwe_out[(size_t)c * out_stride + j] = body - v;
     }
     (void)cpad;

@@ -42,11 +42,13 @@ struct PbsConfig {
     static constexpr size_t GGSW_ELEMS = (size_t)L * (K + 1) * (K + 1) * M;  // double2 per GGSW
     // GGSW_i staged in LDS by async global->LDS loads and shared by the workgroup's ciphertexts;
     // fits next to the tables and 2 x (k+1) exchange buffers when it is <= 64 KiB
-    static constexpr bool STAGE = PBS_GGSW_LDS && GGSW_ELEMS * 16 <= 65536;
+    // (only without the twist/M table: both do not fit next to four exchange buffers)
+    static constexpr bool STAGE = PBS_GGSW_LDS && !PBS_TWIST_INV_LDS && GGSW_ELEMS * 16 <= 65536;
     static constexpr int CPW = STAGE ? 2 : PBS_CPW;  // ciphertexts per workgroup
     static constexpr size_t lds_bytes() {
         return PbsLds<M>::bytes((K + 1) * CPW) + (STAGE ? GGSW_ELEMS * 16 : 0);
     }
+    static_assert(lds_bytes() <= 160 * 1024, "LDS per workgroup exceeds a CU");
 };
 
 template <int N, int K, int L>
@@ -91,7 +93,11 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), PBS_
 #endif
 
     // twiddles and twist -> LDS (once per workgroup)
-    for (int e = threadIdx.x; e < M; e += blockDim.x) lds[Lay::twist_off + e] = a.twist[e];
+    for (int e = threadIdx.x; e < M; e += blockDim.x) {
+        lds[Lay::twist_off + e] = a.twist[e];
+        if (PBS_TWIST_INV_LDS) lds[Lay::twinv_off + e] = a.twist_inv[e];
+    }
+    const double2 *s_twinv = lds + Lay::twinv_off;
     Fft::Lds::template fill<M>(lds + Lay::s1_off, lds + Lay::s2_off, a.W, threadIdx.x, blockDim.x);
     const typename Fft::Lds tw{lds + Lay::s1_off, lds + Lay::s2_off};
     sync();  // tables visible to every wave (the CMUX loop itself only syncs wave-locally)
@@ -250,8 +256,9 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), PBS_
                 Fft::inverse(v, xb, tw, lane, wsync);
 #pragma unroll
                 for (int b = 0; b < V; b++) {
-                    const double2 w = s_twist[lane + 64 * b];
-                    backward_add(v[b], cx{norm * w.x, norm * w.y}, c0[b], c0[V + b]);
+                    const double2 w = PBS_TWIST_INV_LDS ? s_twinv[lane + 64 * b] : s_twist[lane + 64 * b];
+                    const cx ws = PBS_TWIST_INV_LDS ? cx{w.x, w.y} : cx{norm * w.x, norm * w.y};
+                    backward_add(v[b], ws, c0[b], c0[V + b]);
                 }
             }
         }
@@ -259,12 +266,20 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), PBS_
             Fft::inverse(acc, xb, tw, lane, wsync);
 #pragma unroll
             for (int b = 0; b < V; b++) {
-                const double2 w = s_twist[lane + 64 * b];
-                backward_add(acc[b], cx{norm * w.x, norm * w.y}, c0[b], c0[V + b]);
+                const double2 w = PBS_TWIST_INV_LDS ? s_twinv[lane + 64 * b] : s_twist[lane + 64 * b];
+                const cx ws = PBS_TWIST_INV_LDS ? cx{w.x, w.y} : cx{norm * w.x, norm * w.y};
+                backward_add(acc[b], ws, c0[b], c0[V + b]);
             }
         }
     }
 
+    if (a.glwe_out) {  // bootstrap_without_sample_extract (fork, bootstrap.rs:383-412)
+        if (!active) return;
+        uint64_t *g = a.lwe_out + ((size_t)ct * (K + 1) + wave) * N;
+#pragma unroll
+        for (int h = 0; h < 2 * V; h++) g[lane + 64 * h] = c0[h];
+        return;
+    }
     // sample extract at degree 0 (glwe_sample_extraction.rs:91-147)
     wsync();
 #pragma unroll

@@ -32,7 +32,7 @@ __global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU)
     constexpr int LOG2M = LOG2N - 1;
     constexpr int NSEL = 1 << G;
     using Fft = WaveFft<M>;
-    using Lay = PbsLds<M>;
+    using Lay = PbsLds<M, PBS_MB_TWIST_INV_LDS>;
     constexpr int XL = Lay::XL;
     static_assert(sizeof(cx) * XL >= sizeof(uint64_t) * N, "exchange buffer holds one polynomial");
 
@@ -54,7 +54,11 @@ __global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU)
     BlockSync sync;
     WaveLocalSync wsync;
 
-    for (int e = threadIdx.x; e < M; e += blockDim.x) lds[Lay::twist_off + e] = a.twist[e];
+    for (int e = threadIdx.x; e < M; e += blockDim.x) {
+        lds[Lay::twist_off + e] = a.twist[e];
+        if (PBS_MB_TWIST_INV_LDS) lds[Lay::twinv_off + e] = a.twist_inv[e];
+    }
+    const double2 *s_twinv = lds + Lay::twinv_off;
     Fft::Lds::template fill<M>(lds + Lay::s1_off, lds + Lay::s2_off, a.W, threadIdx.x, blockDim.x);
     const typename Fft::Lds tw{lds + Lay::s1_off, lds + Lay::s2_off};
     sync();
@@ -204,8 +208,9 @@ __global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU)
                 Fft::inverse(v, xb, tw, lane, wsync);
 #pragma unroll
                 for (int b = 0; b < V; b++) {
-                    const double2 w = s_twist[lane + 64 * b];
-                    backward_convert(v[b], cx{norm * w.x, norm * w.y}, c0[b], c0[V + b]);
+                    const double2 w = PBS_MB_TWIST_INV_LDS ? s_twinv[lane + 64 * b] : s_twist[lane + 64 * b];
+                    const cx ws = PBS_MB_TWIST_INV_LDS ? cx{w.x, w.y} : cx{norm * w.x, norm * w.y};
+                    backward_convert(v[b], ws, c0[b], c0[V + b]);
                 }
             }
         }
@@ -213,12 +218,19 @@ __global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU)
             Fft::inverse(acc, xb, tw, lane, wsync);
 #pragma unroll
             for (int b = 0; b < V; b++) {
-                const double2 w = s_twist[lane + 64 * b];
-                backward_convert(acc[b], cx{norm * w.x, norm * w.y}, c0[b], c0[V + b]);
+                const double2 w = PBS_MB_TWIST_INV_LDS ? s_twinv[lane + 64 * b] : s_twist[lane + 64 * b];
+                const cx ws = PBS_MB_TWIST_INV_LDS ? cx{w.x, w.y} : cx{norm * w.x, norm * w.y};
+                backward_convert(acc[b], ws, c0[b], c0[V + b]);
             }
         }
     }
 
+    if (a.glwe_out) {  // bootstrap_without_sample_extract (fork, bootstrap.rs:383-412)
+        uint64_t *g = a.lwe_out + ((size_t)ct * (K + 1) + wave) * N;
+#pragma unroll
+        for (int h = 0; h < 2 * V; h++) g[lane + 64 * h] = c0[h];
+        return;
+    }
     // sample extract at degree 0 (glwe_sample_extraction.rs:91-147)
     wsync();
 #pragma unroll
@@ -235,7 +247,7 @@ __global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU)
 template <int N, int K, int L, int G>
 static hipError_t launch_mb_t(const MultiBitPbsLaunch &a, hipStream_t s) {
     constexpr int M = N / 2;
-    const size_t lds = PbsLds<M>::bytes(K + 1);
+    const size_t lds = PbsLds<M, PBS_MB_TWIST_INV_LDS>::bytes(K + 1);
     if (a.count == 0) return hipSuccess;
     if (a.n % G) return hipErrorInvalidValue;
     hipLaunchKernelGGL((pbs_multibit_kernel<N, K, L, G>), dim3(a.count), dim3(64 * (K + 1)), lds, s, a);

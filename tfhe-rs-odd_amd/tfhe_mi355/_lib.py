@@ -62,6 +62,9 @@ SIGNATURES = [
     ("tfhe_mi355_client_gen_bootstrap_key", ctypes.c_int,
      [ctypes.c_uint64, u64p, ctypes.c_uint32, u64p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
       ctypes.c_uint32, ctypes.c_double, u64p, ctypes.c_uint32]),
+    ("tfhe_mi355_blind_rotate", ctypes.c_int, [vp, u64p, u64p, u64p, ctypes.c_size_t, u32p, ctypes.c_size_t]),
+    ("tfhe_mi355_blind_rotate_async", ctypes.c_int,
+     [vp, vp, vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, vp]),
     ("tfhe_mi355_lwe_scalar_mul_add_async", ctypes.c_int,
      [vp, vp, vp, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, vp]),
     ("tfhe_mi355_trivial_pbs_async", ctypes.c_int, [vp, vp, ctypes.c_size_t, ctypes.c_size_t, vp, vp]),
@@ -71,6 +74,14 @@ SIGNATURES = [
     ("tfhe_mi355_client_gen_keyswitch_key", ctypes.c_int,
      [ctypes.c_uint64, u64p, ctypes.c_uint32, u64p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
       ctypes.c_double, u64p]),
+    ("tfhe_mi355_packing_keyswitch_key_upload", ctypes.c_int, [vp, u64p, sz, ctypes.c_uint32, ctypes.c_uint32]),
+    ("tfhe_mi355_packing_keyswitch", ctypes.c_int, [vp, u64p, u64p, sz]),
+    ("tfhe_mi355_packing_keyswitch_async", ctypes.c_int, [vp, vp, vp, sz, vp]),
+    ("tfhe_mi355_glwe_poly_mul", ctypes.c_int, [vp, u64p, sz, u64p, sz, sz, ctypes.c_int, u64p]),
+    ("tfhe_mi355_glwe_poly_mul_async", ctypes.c_int, [vp, vp, sz, vp, sz, sz, ctypes.c_int, vp, vp]),
+    ("tfhe_mi355_client_gen_packing_keyswitch_key", ctypes.c_int,
+     [ctypes.c_uint64, u64p, ctypes.c_uint32, u64p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+      ctypes.c_uint32, ctypes.c_double, u64p, ctypes.c_uint32]),
     ("tfhe_mi355_client_lwe_encrypt", ctypes.c_int,
      [ctypes.c_uint64, u64p, ctypes.c_uint32, u64p, sz, ctypes.c_double, u64p]),
     ("tfhe_mi355_client_lwe_decrypt", ctypes.c_int, [u64p, ctypes.c_uint32, u64p, sz, u64p]),

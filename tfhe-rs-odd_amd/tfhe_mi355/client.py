@@ -60,6 +60,18 @@ def gen_keyswitch_key(seed, in_sk, out_sk, base_log, level, std_dev) -> np.ndarr
     return ksk
 
 
+def gen_packing_keyswitch_key(seed, in_sk, glwe_sk, glwe_dimension, polynomial_size, base_log, level, std_dev,
+                              threads: int = 0) -> np.ndarray:
+    """LWE -> GLWE packing KSK [in][level][(k+1)N] (lwe_packing_keyswitch_key_generation.rs:74-149)."""
+    in_sk = np.ascontiguousarray(in_sk, dtype=np.uint64)
+    glwe_sk = np.ascontiguousarray(glwe_sk, dtype=np.uint64)
+    k, N = glwe_dimension, polynomial_size
+    out = np.empty(len(in_sk) * level * (k + 1) * N, dtype=np.uint64)
+    _lib.call("tfhe_mi355_client_gen_packing_keyswitch_key", seed, _ptr(in_sk), len(in_sk), _ptr(glwe_sk), k, N,
+              base_log, level, std_dev, _ptr(out), threads)
+    return out
+
+
 def lwe_encrypt(seed, sk, plaintexts, std_dev) -> np.ndarray:
     sk = np.ascontiguousarray(sk, dtype=np.uint64)
     pts = np.ascontiguousarray(plaintexts, dtype=np.uint64).ravel()

@@ -150,6 +150,16 @@ class Engine:
                   idxp, x.shape[0])
         return out
 
+    def blind_rotate(self, lwe_in, luts, lut_indexes=None) -> np.ndarray:
+        """bootstrap_without_sample_extract (fork, fft64/crypto/bootstrap.rs:383-412): the rotated
+        accumulators, [count][(k+1)N]."""
+        x = _u64(lwe_in).reshape(-1, self.n + 1)
+        L = self._luts(luts)
+        idx, idxp = self._idx(lut_indexes, x.shape[0], L.shape[0])
+        out = np.empty((x.shape[0], self.glwe_len), dtype=np.uint64)
+        _lib.call("tfhe_mi355_blind_rotate", self._h, _ptr(x), _ptr(out), _ptr(L), L.shape[0], idxp, x.shape[0])
+        return out
+
     def keyswitch(self, lwe_in) -> np.ndarray:
         x = _u64(lwe_in).reshape(-1, self.big_dim + 1)
         out = np.empty((x.shape[0], self.n + 1), dtype=np.uint64)
@@ -172,6 +182,34 @@ class Engine:
         out = np.empty((x.shape[0], self.n + 1), dtype=np.uint64)
         _lib.call("tfhe_mi355_programmable_bootstrap_keyswitch", self._h, _ptr(x), _ptr(out), _ptr(L),
                   L.shape[0], idxp, x.shape[0])
+        return out
+
+    def upload_packing_keyswitch_key(self, pksk: np.ndarray, base_log: int, level: int) -> None:
+        k = _u64(pksk)
+        _lib.call("tfhe_mi355_packing_keyswitch_key_upload", self._h, _ptr(k), k.size, base_log, level)
+
+    def packing_keyswitch(self, lwe_in) -> np.ndarray:
+        """keyswitch_lwe_ciphertext_into_glwe_ciphertext (lwe_packing_keyswitch.rs:102-186), batched."""
+        x = _u64(lwe_in).reshape(-1, self.big_dim + 1)
+        out = np.empty((x.shape[0], self.glwe_len), dtype=np.uint64)
+        _lib.call("tfhe_mi355_packing_keyswitch", self._h, _ptr(x), _ptr(out), x.shape[0])
+        return out
+
+    def glwe_poly_mul(self, glwe_in, polys, extract: bool = False) -> np.ndarray:
+        """out[c][i] = sum_j glwe_in[c][j] * polys[i][j] (negacyclic, wrapping), optionally sample-
+        extracted: glwe_in [count][J][(k+1)N], polys [npoly][J][N]."""
+        N = self.params.polynomial_size
+        g = _u64(glwe_in)
+        if g.ndim == 2:
+            g = g.reshape(g.shape[0], 1, -1)
+        v = _u64(polys)
+        if v.ndim == 2:
+            v = v.reshape(v.shape[0], 1, -1)
+        count, J = g.shape[0], g.shape[1]
+        if g.shape[2] != self.glwe_len or v.shape[1] != J or v.shape[2] != N:
+            raise ValueError("glwe_poly_mul: shape mismatch")
+        out = np.empty((count, v.shape[0], self.big_dim + 1 if extract else self.glwe_len), dtype=np.uint64)
+        _lib.call("tfhe_mi355_glwe_poly_mul", self._h, _ptr(g), J, _ptr(v), v.shape[0], count, int(extract), _ptr(out))
         return out
 
     # -- device (torch) async ops -------------------------------------------------------
@@ -199,6 +237,15 @@ class Engine:
     def trivial_pbs_async(self, body_ptr: int, rows: int, stride: int, d_lut, stream=None) -> None:
         _lib.call("tfhe_mi355_trivial_pbs_async", self._h, body_ptr, rows, stride, _dev_ptr(d_lut),
                   _stream_ptr(stream))
+
+    def packing_keyswitch_async(self, d_in, d_out, count: int, stream=None) -> None:
+        _lib.call("tfhe_mi355_packing_keyswitch_async", self._h, _dev_ptr(d_in), _dev_ptr(d_out), count,
+                  _stream_ptr(stream))
+
+    def glwe_poly_mul_async(self, d_glwe, glwe_per_item: int, d_polys, npoly: int, count: int, extract: bool,
+                            d_out, stream=None) -> None:
+        _lib.call("tfhe_mi355_glwe_poly_mul_async", self._h, _dev_ptr(d_glwe), glwe_per_item, _dev_ptr(d_polys),
+                  npoly, count, int(extract), _dev_ptr(d_out), _stream_ptr(stream))
 
     def ks_pbs_scratch_bytes(self, count: int) -> int:
         b = ctypes.c_size_t()
