@@ -377,6 +377,9 @@ class OracleEngine:
     def programmable_bootstrap(self, x, luts, lut_indexes=None):
         return self.fb.pbs(x, luts, lut_indexes, threads=self.threads)
 
+    def programmable_bootstrap_keyswitch(self, x, luts, lut_indexes=None):
+        return self.keyswitch(self.fb.pbs(x, luts, lut_indexes, threads=self.threads))
+
     def blind_rotate(self, x, luts, lut_indexes=None):
         return self.fb.blind_rotate(x, luts, lut_indexes, threads=self.threads)
 

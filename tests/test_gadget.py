@@ -233,3 +233,18 @@ def test_gadget_tree_bootstrapping_cpu(gadget_cpu):
     for (x0, x1), (r1, r0) in zip(pairs, res):
         X = x1 + o * x0
         assert ck.decrypt(r0) == f(X) % o and ck.decrypt(r1) == f(X) // o, (x0, x1)
+
+
+@pytest.mark.parametrize("name", ["GADGET_ZAMA_TRIVIUM_PARAMETERS", "GADGET_SIMON_PARAMETERS_40"])
+def test_gadget_apply_lut_gadget_params_cpu(orc, name):
+    """k = 3, N = 512 sets through the oracle engine: Small key (PBS -> KS) and Big key (KS -> PBS)."""
+    from tfhe_mi355 import gadget
+    from tfhe_mi355.parameters import ALL
+
+    P = ALL[name]
+    ck = gadget.ClientKey(P, seed=4)
+    sk = gadget.ServerKey(ck, engine=OracleEngine(P))
+    enc = gadget.Encoding.new_trivial(3)
+    cts = ck.encrypt_arithmetic_many([0, 1, 2, 2, 1], enc)
+    res = sk.apply_lut_batch(cts, enc, lambda x: (x + 1) % 3)
+    assert ck.decrypt_many(res) == [1, 2, 0, 0, 2]

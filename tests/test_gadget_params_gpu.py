@@ -1,0 +1,65 @@
+"""The classic PBS at the fork's gadget parameter sets (k = 2, 3; N = 512, 1024; levels 1-4;
+gadget/parameters/mod.rs:84-222), bit-exact against the oracle, plus one gadget evaluation per
+PBS order (KS -> PBS for Big-key sets, PBS -> KS for Small-key sets) checked by decryption.
+"""
+import numpy as np
+import pytest
+
+from conftest import KeySet, OracleEngine
+
+pytestmark = pytest.mark.gpu
+
+
+def _supported():
+    from tfhe_mi355.parameters import GADGET_ALL
+
+    return [p for p in GADGET_ALL if p.polynomial_size >= 512]
+
+
+@pytest.mark.parametrize("params", _supported(), ids=lambda p: p.name)
+def test_gadget_params_pbs_bit_exact(orc, params):
+    from tfhe_mi355 import Engine
+
+    keys = KeySet(orc, params, seed=7)
+    p = params
+    eng = Engine(p, 0)
+    eng.upload_bootstrap_key(keys.bsk)
+    rng = np.random.default_rng(p.lwe_dimension)
+    cts = rng.integers(0, 2 ** 64, (19, p.lwe_dimension + 1), dtype=np.uint64)
+    cts[0, :-1] = 0                                        # skipped CMUXes only
+    luts = rng.integers(0, 2 ** 64, (2, (p.glwe_dimension + 1) * p.polynomial_size), dtype=np.uint64)
+    idx = (np.arange(19) % 2).astype(np.uint32)
+    exp = keys.fbsk.pbs(cts, luts, idx, threads=8)
+    got = eng.programmable_bootstrap(cts, luts, idx)
+    assert np.array_equal(got, exp), f"{np.count_nonzero(got != exp)} words differ"
+    exp = keys.fbsk.blind_rotate(cts, luts, idx, threads=8)
+    got = eng.blind_rotate(cts, luts, idx)
+    assert np.array_equal(got, exp)
+
+
+def test_gadget_params_unsupported_n256_fails_loudly():
+    from tfhe_mi355 import Engine
+    from tfhe_mi355._lib import EngineError
+    from tfhe_mi355.parameters import GADGET_SHA3_PARAMETERS_40
+
+    with pytest.raises(EngineError, match="no kernel"):
+        Engine(GADGET_SHA3_PARAMETERS_40, 0)
+
+
+@pytest.mark.parametrize("name", ["GADGET_ASCON_PARAMETERS_40", "GADGET_ZAMA_TRIVIUM_PARAMETERS"])
+def test_gadget_apply_lut_both_orders(name):
+    """Big-key set (KS -> PBS) and Small-key set (PBS -> KS) end to end, GPU vs oracle engine."""
+    from tfhe_mi355 import gadget
+    from tfhe_mi355.parameters import ALL
+
+    P = ALL[name]
+    ck = gadget.ClientKey(P, seed=3)
+    gpu = gadget.ServerKey(ck, device=0)
+    cpu = gadget.ServerKey(ck, engine=OracleEngine(P))
+    enc = gadget.Encoding.new_trivial(3)
+    cts = ck.encrypt_arithmetic_many([x % 3 for x in range(12)], enc)
+    f = lambda x: (2 * x + 1) % 3  # noqa: E731
+    a = gpu.apply_lut_batch(cts, enc, f)
+    b = cpu.apply_lut_batch(cts, enc, f)
+    assert all(np.array_equal(x.ct, y.ct) for x, y in zip(a, b))
+    assert ck.decrypt_many(a) == [f(x % 3) for x in range(12)]

@@ -458,6 +458,130 @@ struct WaveFft<512> {
     }
 };
 
+// ---------------------------------------------------------------------------------------
+// M = 256 (N = 512): radices [16, 16]; 64 lanes x 4 values.  A 16-point DFT is spread over the
+// four 16-lane rows: row A holds its column (v[A], v[A+4], v[A+8], v[A+12]), runs the first
+// radix-4 and the internal twiddles omega_16^{A q} (A is per row, so selected at run time), a
+// cross-row register transpose hands row c the values u[0..3][c], and the second radix-4 leaves
+// X[c + 4q] in slot q.  Same operations as dft16_fwd/inv, distributed.
+//   natural layout  : lane a, slot b  <->  position a + 64 b
+//   stage 1 (a' = lane & 15 = butterfly, row i): position a' + 16 (i + 4 b): column A = i
+//   fourier layout  : lane L, slot q  <->  position 16 (L & 15) + (L >> 4) + 4 q
+// One LDS exchange per transform (between the two stages).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void tw16_fwd_row(int A, cx &y1, cx &y2, cx &y3) {
+    if (A == 1) {
+        y1 = tw16_fwd<1>(y1);
+        y2 = tw16_fwd<2>(y2);
+        y3 = tw16_fwd<3>(y3);
+    } else if (A == 2) {
+        y1 = tw16_fwd<2>(y1);
+        y2 = tw16_fwd<4>(y2);
+        y3 = tw16_fwd<6>(y3);
+    } else if (A == 3) {
+        y1 = tw16_fwd<3>(y1);
+        y2 = tw16_fwd<6>(y2);
+        y3 = tw16_fwd<9>(y3);
+    }
+}
+__device__ __forceinline__ void tw16_inv_row(int A, cx &y1, cx &y2, cx &y3) {
+    if (A == 1) {
+        y1 = tw16_inv<1>(y1);
+        y2 = tw16_inv<2>(y2);
+        y3 = tw16_inv<3>(y3);
+    } else if (A == 2) {
+        y1 = tw16_inv<2>(y1);
+        y2 = tw16_inv<4>(y2);
+        y3 = tw16_inv<6>(y3);
+    } else if (A == 3) {
+        y1 = tw16_inv<3>(y1);
+        y2 = tw16_inv<6>(y2);
+        y3 = tw16_inv<9>(y3);
+    }
+}
+// dft16_fwd across rows: in  row A slot j = v[A + 4j];  out  row c slot q = X[c + 4q]
+__device__ __forceinline__ void dft16_fwd_rows(cx *v, int row) {
+    r4_fwd(v[0], v[1], v[2], v[3]);
+    tw16_fwd_row(row, v[1], v[2], v[3]);
+    transpose_rows4(v[0], v[1], v[2], v[3]);
+    r4_fwd(v[0], v[1], v[2], v[3]);
+}
+// dft16_inv across rows: in  row c slot q = X[c + 4q];  out  row A slot j = v[A + 4j]
+__device__ __forceinline__ void dft16_inv_rows(cx *v, int row) {
+    r4_inv(v[0], v[1], v[2], v[3]);
+    transpose_rows4(v[0], v[1], v[2], v[3]);
+    tw16_inv_row(row, v[1], v[2], v[3]);
+    r4_inv(v[0], v[1], v[2], v[3]);
+}
+// stage-1 twiddles W[a' C] (a' < 16, C = 1..15): LDS table [C-1][a']
+struct LdsTwiddles256 {
+    const double2 *t1, *t2;
+    __device__ __forceinline__ cx s1(int c, int a) const {
+        double2 t = t1[(c - 1) * 16 + a];
+        return {t.x, t.y};
+    }
+    static constexpr int s1_len = 15 * 16;
+    static constexpr int s2_len = 0;
+    template <int M>
+    __device__ static void fill(double2 *t1, double2 *, const double2 *__restrict__ W, int tid, int nthreads) {
+        for (int e = tid; e < s1_len; e += nthreads) t1[e] = W[(e & 15) * ((e >> 4) + 1)];
+    }
+};
+
+template <>
+struct WaveFft<256> {
+    static constexpr int M = 256;
+    static constexpr int V = 4;
+    static constexpr int XL = xbuf_len(256);
+    using Lds = LdsTwiddles256;
+
+    template <class TW, class Sync>
+    __device__ __forceinline__ static void forward(cx *v, cx *xb, const TW &tw, int lane, Sync sync) {
+        // stage 1: L = 256, R = 16, m = 16; butterfly a' = lane & 15
+        const int ap = lane & 15, row = lane >> 4;
+        dft16_fwd_rows(v, row);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int C = row + 4 * q;
+            if (C) {
+                cx w = tw.s1(C, ap);
+                v[q] = cmulw(v[q], w.re, w.im);
+            }
+        }
+        sync();
+#pragma unroll
+        for (int q = 0; q < 4; q++) lds_st(xb, ap + 16 * (row + 4 * q), v[q]);  // position a' + 16C
+        sync();
+        // stage 2: blocks of 16 (C = lane & 15), R = 16, m = 1, no twiddles; column A = row
+#pragma unroll
+        for (int j = 0; j < 4; j++) v[j] = lds_ld(xb, 16 * ap + row + 4 * j);
+        dft16_fwd_rows(v, row);
+    }
+
+    template <class TW, class Sync>
+    __device__ __forceinline__ static void inverse(cx *v, cx *xb, const TW &tw, int lane, Sync sync) {
+        const int ap = lane & 15, row = lane >> 4;
+        // block DFTs (stage 2 of the forward), lane (c2, C) slot q = X_C[c2 + 4q]
+        dft16_inv_rows(v, row);
+        sync();
+#pragma unroll
+        for (int j = 0; j < 4; j++) lds_st(xb, 16 * ap + row + 4 * j, v[j]);
+        sync();
+        // stage 1: butterfly a' = lane & 15, column c = row: z[a' + 16 (c + 4q)] * conj(W[a' (c + 4q)])
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int C = row + 4 * q;
+            cx y = lds_ld(xb, ap + 16 * C);
+            if (C) {
+                cx w = tw.s1(C, ap);
+                y = cmulw(y, w.re, -w.im);
+            }
+            v[q] = y;
+        }
+        dft16_inv_rows(v, row);
+    }
+};
+
 // exact u64 (mod 2^64) of an integral double |v| <= 2^63: v = hi * 2^32 + lo with hi, lo
 // exact in f64; same value as the reference's f64 -> i64 bit twiddle (x86.rs:28-81).
 __device__ __forceinline__ uint64_t f64_int_to_u64(double v) {

@@ -304,18 +304,28 @@ static hipError_t launch_pbs_t(const ClassicPbsLaunch &a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// Instantiated shapes: the shortint sets (k = 1, N = 2048 / 1024) and the fork's gadget sets
+// (gadget/parameters/mod.rs:84-235: k = 2, 3 at N = 512 / 1024, levels 1-4).
+#define PBS_CLASSIC_SHAPES(X) \
+    X(2048, 1, 1) X(2048, 1, 2) \
+    X(1024, 1, 1) X(1024, 1, 2) X(1024, 1, 3) X(1024, 1, 4) \
+    X(1024, 2, 1) X(1024, 2, 2) X(1024, 2, 3) X(1024, 2, 4) \
+    X(1024, 3, 1) X(1024, 3, 2) X(1024, 3, 3) \
+    X(512, 1, 1) X(512, 1, 2) X(512, 1, 3) X(512, 1, 4) \
+    X(512, 2, 1) X(512, 2, 2) X(512, 2, 3) X(512, 2, 4) \
+    X(512, 3, 1) X(512, 3, 2) X(512, 3, 3) X(512, 3, 4)
+
 bool classic_pbs_supported(int N, int k, int L) {
-    if (k != 1) return false;
-    if (N == 2048) return L == 1 || L == 2;
-    if (N == 1024) return L == 1 || L == 2;
+#define PBS_SUPPORTED(n_, k_, l_) if (N == n_ && k == k_ && L == l_) return true;
+    PBS_CLASSIC_SHAPES(PBS_SUPPORTED)
+#undef PBS_SUPPORTED
     return false;
 }
 
 hipError_t launch_classic_pbs(int N, int k, int L, const ClassicPbsLaunch &a, hipStream_t s) {
-    if (k == 1 && N == 2048 && L == 1) return launch_pbs_t<2048, 1, 1>(a, s);
-    if (k == 1 && N == 2048 && L == 2) return launch_pbs_t<2048, 1, 2>(a, s);
-    if (k == 1 && N == 1024 && L == 1) return launch_pbs_t<1024, 1, 1>(a, s);
-    if (k == 1 && N == 1024 && L == 2) return launch_pbs_t<1024, 1, 2>(a, s);
+#define PBS_LAUNCH(n_, k_, l_) if (N == n_ && k == k_ && L == l_) return launch_pbs_t<n_, k_, l_>(a, s);
+    PBS_CLASSIC_SHAPES(PBS_LAUNCH)
+#undef PBS_LAUNCH
     return hipErrorInvalidValue;
 }
 
@@ -361,6 +371,9 @@ hipError_t launch_bsk_to_fourier(int N, const uint64_t *std_polys, double2 *four
     } else if (N == 1024) {
         hipLaunchKernelGGL(bsk_to_fourier_kernel<1024>, dim3(npoly), dim3(64),
                            sizeof(cx) * WaveFft<512>::XL, s, std_polys, fourier, npoly, t.W, t.twist);
+    } else if (N == 512) {
+        hipLaunchKernelGGL(bsk_to_fourier_kernel<512>, dim3(npoly), dim3(64),
+                           sizeof(cx) * WaveFft<256>::XL, s, std_polys, fourier, npoly, t.W, t.twist);
     } else {
         return hipErrorInvalidValue;
     }

@@ -6,6 +6,8 @@ authoritative -- see SURVEY.md 0.4 for the BASELINE.json annotation mismatch).
   PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS   shortint/parameters/multi_bit.rs:173-190
   PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS   shortint/parameters/multi_bit.rs:115-132
   MANTICORE_PARAMETERS (fork)      gadget/parameters/mod.rs:224-235
+  GADGET_* (fork)                  gadget/parameters/mod.rs:84-222 (DEFAULT, SIMON_40,
+                                   ZAMA_TRIVIUM, ASCON_40, SHA3_40, AES_40, AES_23, TFHE_LIB)
   TEST_PARAMS_4_BITS_NATIVE_U64    core_crypto/algorithms/test/mod.rs:56-73
 """
 from __future__ import annotations
@@ -84,8 +86,38 @@ MANTICORE_PARAMETERS = ClassicPBSParameters(
     pbs_base_log=15, pbs_level=2, ks_base_log=4, ks_level=3,
     message_modulus=2, carry_modulus=2, name="MANTICORE_PARAMETERS")
 
+
+
+def _gadget(name, n, k, N, lwe_std, glwe_std, pbs_bl, pbs_l, ks_bl, ks_l, choice):
+    return ClassicPBSParameters(lwe_dimension=n, glwe_dimension=k, polynomial_size=N, lwe_modular_std_dev=lwe_std,
+                                glwe_modular_std_dev=glwe_std, pbs_base_log=pbs_bl, pbs_level=pbs_l,
+                                ks_base_log=ks_bl, ks_level=ks_l, message_modulus=2, carry_modulus=2,
+                                encryption_key_choice=choice, name=name)
+
+
+# the fork's other GadgetParameters (k = 2, 3, 5 at N = 256..1024)
+GADGET_DEFAULT_PARAMETERS = _gadget("GADGET_DEFAULT_PARAMETERS", 722, 2, 512, 0.000013071021089943935,
+                                    0.00000004990272175010415, 6, 3, 3, 4, "Small")
+GADGET_SIMON_PARAMETERS_40 = _gadget("GADGET_SIMON_PARAMETERS_40", 684, 3, 512, 1.52587890625e-05,
+                                     9.313225746154785e-10, 10, 2, 3, 4, "Big")
+GADGET_ZAMA_TRIVIUM_PARAMETERS = _gadget("GADGET_ZAMA_TRIVIUM_PARAMETERS", 684, 3, 512, 0.0000204378,
+                                         0.000000000000345253, 18, 1, 4, 3, "Small")
+GADGET_ASCON_PARAMETERS_40 = _gadget("GADGET_ASCON_PARAMETERS_40", 740, 2, 1024, 1.9073486328125e-06,
+                                     9.313225746154785e-10, 7, 3, 5, 3, "Big")
+GADGET_SHA3_PARAMETERS_40 = _gadget("GADGET_SHA3_PARAMETERS_40", 676, 5, 256, 0.0009765625,
+                                    0.0000000000000000008673617379884035, 14, 1, 4, 3, "Big")
+GADGET_AES_PARAMETERS_40 = _gadget("GADGET_AES_PARAMETERS_40", 708, 3, 512, 3.0517578125e-05,
+                                   9.313225746154785e-10, 6, 4, 2, 7, "Big")
+GADGET_AES_PARAMETERS_23 = _gadget("GADGET_AES_PARAMETERS_23", 672, 3, 512, 0.0000000010797982869590127,
+                                   0.0000000000000000008673617379884035, 7, 3, 3, 4, "Big")
+GADGET_TFHE_LIB_PARAMETERS = _gadget("GADGET_TFHE_LIB_PARAMETERS", 830, 2, 1024, 0.000001412290588219445,
+                                     0.00000000000000029403601535432533, 23, 1, 5, 3, "Small")
+GADGET_ALL = [GADGET_DEFAULT_PARAMETERS, GADGET_SIMON_PARAMETERS_40, GADGET_ZAMA_TRIVIUM_PARAMETERS,
+              GADGET_ASCON_PARAMETERS_40, GADGET_SHA3_PARAMETERS_40, GADGET_AES_PARAMETERS_40,
+              GADGET_AES_PARAMETERS_23, GADGET_TFHE_LIB_PARAMETERS]
+
 TEST_PARAMS_4_BITS_NATIVE_U64 = PARAM_MESSAGE_2_CARRY_2_KS_PBS.with_(name="TEST_PARAMS_4_BITS_NATIVE_U64")
 
 ALL = {p.name: p for p in [PARAM_MESSAGE_2_CARRY_2_KS_PBS, PARAM_MESSAGE_4_CARRY_4_KS_PBS,
                            PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS,
-                           PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS, MANTICORE_PARAMETERS]}
+                           PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS, MANTICORE_PARAMETERS] + GADGET_ALL}
