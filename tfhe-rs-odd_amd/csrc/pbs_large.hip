@@ -8,8 +8,8 @@
 // Why a different structure (DESIGN.md "Kernels"): at N = 32768 one ciphertext's accumulator is
 // (k+1) N u64 = 512 KiB and one spectrum M = 16384 c64 = 256 KiB -- neither fits a CU (160 KiB
 // LDS), so the accumulator lives in HBM scratch and each CMUX is two batch-wide launches:
-//   large_fwd  : one workgroup per (ciphertext, row r, level): ct1 = X^{a~} acc_r - acc_r,
-//                decompose, twist, FFT -> spectrum F[ct][lvl][r]   (global)
+//   large_fwd  : one workgroup per (ciphertext, row r): ct1 = X^{a~} acc_r - acc_r, decompose,
+//                then per level: twist, FFT -> spectrum F[ct][lvl][r]   (global)
 //   large_inv  : one workgroup per (ciphertext, column c): sum_{lvl,r} F * GGSW[lvl][r][c],
 //                inverse FFT, acc_c += rounded result                  (global)
 // The M = 16384 FFT is the oracle's [16, 16, 16, 4] DAG: the top radix-16 stage runs across the
@@ -111,6 +111,7 @@ __device__ __forceinline__ void large_forward(const LargeCtx &c, cx (&u)[2][16])
         dft16_fwd(u[h]);
 #pragma unroll
         for (int q = 1; q < 16; q++) {
+            if (q % 4 == 1) __builtin_amdgcn_sched_barrier(0);  // bound twiddle loads in flight
             const cx w = gld(c.W + a * q);
             u[h][q] = cmulw(u[h][q], w.re, w.im);
         }
@@ -166,13 +167,17 @@ __global__ void __launch_bounds__(256) large_init_kernel(LargePbsLaunch a, int c
     a.acc[e] = (wrap != (bool)(full & 1)) ? 0 - v : v;
 }
 
+// One workgroup per (ciphertext, row r): the rotation and the decomposition are done once for all
+// levels; level L's digits go straight into the FFT input, level L-1's (L = 2) are parked as int16
+// pairs in the not-yet-written level-(L-1) spectrum buffer (64 KiB of its 256 KiB; L2-resident)
+// and transformed second.  Halves the accumulator reads and the decomposition work of a
+// per-(row, level) split, and the workgroup count.
 template <int K, int L>
 __global__ void __launch_bounds__(LT) large_fwd_kernel(LargePbsLaunch a, int ct0, int i) {
+    static_assert(L == 1 || L == 2, "levels L and L-1 only");
     const LargeCtx c = large_setup(a.W);
-    const int blk = blockIdx.x;
-    const int lvl = L - blk % L;                 // level of this workgroup's digits
-    const int r = (blk / L) % (K + 1);
-    const int cl = blk / (L * (K + 1));
+    const int r = blockIdx.x % (K + 1);
+    const int cl = blockIdx.x / (K + 1);
     const uint64_t *in = a.lwe_in + (size_t)(ct0 + cl) * (a.n + 1);
     const uint32_t at = pbs_modulus_switch<15>(in[i]);
     const bool full_odd = (at / LN) & 1;
@@ -180,6 +185,8 @@ __global__ void __launch_bounds__(LT) large_fwd_kernel(LargePbsLaunch a, int ct0
     const uint64_t *acc = a.acc + ((size_t)cl * (K + 1) + r) * LN;
     const int beta = a.base_log;
     const uint32_t dmask = (1u << beta) - 1;
+    auto spectrum = [&](int lvl) { return a.spectra + (((size_t)cl * L + (lvl - 1)) * (K + 1) + r) * LM; };
+    uint32_t *stash = reinterpret_cast<uint32_t *>(spectrum(L - 1 > 0 ? L - 1 : 1));
 
     cx u[2][16];
 #pragma unroll
@@ -187,7 +194,7 @@ __global__ void __launch_bounds__(LT) large_fwd_kernel(LargePbsLaunch a, int ct0
 #pragma unroll
         for (int b = 0; b < 16; b++) {
             const int j = c.t + 512 * h + 1024 * b;
-            int32_t dg[2];
+            int32_t dg[2], dl[2];
 #pragma unroll
             for (int half = 0; half < 2; half++) {
                 // ct1 = X^{a~} acc - acc  (polynomial_wrapping_monic_monomial_mul_and_subtract)
@@ -196,24 +203,44 @@ __global__ void __launch_bounds__(LT) large_fwd_kernel(LargePbsLaunch a, int ct0
                 const uint64_t x = acc[(unsigned)jj & (unsigned)(LN - 1)];
                 const uint64_t d = (neg ? 0 - x : x) - acc[j + half * LM];
                 uint32_t st = decomp_state32_hi<L>((uint32_t)(d >> 32), beta);
-                int32_t dig = 0;
-#pragma unroll
-                for (int l = L; l >= 1; l--) {
-                    const int32_t v = decomp_digit32(st, beta, dmask);
-                    if (l == lvl) dig = v;
-                }
-                dg[half] = dig;
+                dg[half] = decomp_digit32(st, beta, dmask);                  // level L
+                dl[half] = L == 2 ? decomp_digit32(st, beta, dmask) : 0;     // level L-1
             }
+            if constexpr (L == 2)
+                stash[(h * 16 + b) * LT + c.t] = ((uint32_t)dl[0] & 0xffffu) | ((uint32_t)dl[1] << 16);
             const cx tw = gld(a.twist + j);
             u[h][b] = cmulw(cx{(double)dg[0], (double)dg[1]}, tw.re, tw.im);
         }
     }
+    auto store = [&](int lvl) {
+        double2 *F = spectrum(lvl);
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+            for (int s = 0; s < 16; s++)
+                F[spec_off(c.wave, h, s, c.lane)] = make_double2(u[h][s].re, u[h][s].im);
+    };
     large_forward(c, u);
-    double2 *F = a.spectra + (((size_t)cl * L + (lvl - 1)) * (K + 1) + r) * LM;
+    store(L);
+    if constexpr (L == 2) {
+        __builtin_amdgcn_sched_barrier(0);
+        // own stash entries only (written by this thread); the spectrum writes below come after
+        // the FFT's first workgroup barrier, so every thread has read its entries by then
 #pragma unroll
-    for (int h = 0; h < 2; h++)
+        for (int h = 0; h < 2; h++)
 #pragma unroll
-        for (int s = 0; s < 16; s++) F[spec_off(c.wave, h, s, c.lane)] = make_double2(u[h][s].re, u[h][s].im);
+            for (int b = 0; b < 16; b++) {
+                int t = c.t;
+                asm volatile("" : "+v"(t));  // per-use address: no block of hoisted addresses
+                const int j = t + 512 * h + 1024 * b;
+                const uint32_t pk = stash[(h * 16 + b) * LT + t];
+                const int32_t d0 = (int32_t)(int16_t)(pk & 0xffffu), d1 = (int32_t)pk >> 16;
+                const cx tw = gld(a.twist + j);
+                u[h][b] = cmulw(cx{(double)d0, (double)d1}, tw.re, tw.im);
+            }
+        large_forward(c, u);
+        store(L - 1);
+    }
 }
 
 template <int K, int L>
@@ -334,7 +361,7 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
         hipLaunchKernelGGL(large_init_kernel<K>, dim3((unsigned)((init_elems + 255) / 256)), dim3(256), 0, s, a,
                            ct0, cnt);
         for (int i = 0; i < a.n; i++) {
-            hipLaunchKernelGGL((large_fwd_kernel<K, L>), dim3(cnt * (K + 1) * L), dim3(LT), LARGE_LDS, s, a, ct0, i);
+            hipLaunchKernelGGL((large_fwd_kernel<K, L>), dim3(cnt * (K + 1)), dim3(LT), LARGE_LDS, s, a, ct0, i);
             hipLaunchKernelGGL((large_inv_kernel<K, L>), dim3(cnt * (K + 1)), dim3(LT), LARGE_LDS, s, a, ct0, i);
         }
         const size_t out_elems = (size_t)cnt * (K * LN + 1);
