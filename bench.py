@@ -50,6 +50,22 @@ PARAMS = {  # --params choice -> (parameter set name, workload text, kernel name
     "mb2": ("PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS",
             "batch of 4096 independent multi-bit (grouping 2) PBS per GPU, identity LUT",
             "pbs_multibit_kernel<2048,1,1,2>"),
+    # the fork's gadget parameter sets (gadget/parameters/mod.rs), same PBS workload
+    "manticore": ("MANTICORE_PARAMETERS",
+                  "batch of 4096 independent classic PBS per GPU at the fork's MANTICORE_PARAMETERS",
+                  "pbs_classic_kernel<1024,1,2>"),
+    "ascon": ("GADGET_ASCON_PARAMETERS_40",
+              "batch of 4096 independent classic PBS per GPU at the fork's ASCON_PARAMETERS_40",
+              "pbs_classic_kernel<1024,2,3>"),
+    "simon": ("GADGET_SIMON_PARAMETERS_40",
+              "batch of 4096 independent classic PBS per GPU at the fork's SIMON_PARAMETERS_40",
+              "pbs_classic_kernel<512,3,2>"),
+    "tfhelib": ("GADGET_TFHE_LIB_PARAMETERS",
+                "batch of 4096 independent classic PBS per GPU at the fork's TFHE_LIB_PARAMETERS",
+                "pbs_classic_kernel<1024,2,1>"),
+    "aes40": ("GADGET_AES_PARAMETERS_40",
+              "batch of 4096 independent classic PBS per GPU at the fork's AES_PARAMETERS_40",
+              "pbs_classic_kernel<512,3,4>"),
 }
 
 

@@ -49,10 +49,13 @@ struct PbsConfig {
         return PbsLds<M>::bytes((K + 1) * CPW) + (STAGE ? GGSW_ELEMS * 16 : 0);
     }
     static_assert(lds_bytes() <= 160 * 1024, "LDS per workgroup exceeds a CU");
+    // register budget: 1 wave/SIMD at N = 2048 (the headline shape needs ~360 VGPR+AGPR);
+    // smaller N fit 2 (N = 1024: <= 256) or 3 (N = 512: <= 168) waves per SIMD
+    static constexpr int WPE = PBS_WAVES_PER_EU > 0 ? PBS_WAVES_PER_EU : (N >= 2048 ? 1 : N == 1024 ? 2 : 3);
 };
 
 template <int N, int K, int L>
-__global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), PBS_WAVES_PER_EU)
+__global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (PbsConfig<N, K, L>::WPE))
     pbs_classic_kernel(ClassicPbsLaunch a) {
     constexpr int M = N / 2;
     constexpr int V = M / 64;
@@ -156,6 +159,22 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), PBS_
     };
     auto stage_ggsw_wait = [&]() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
     if constexpr (STAGE) stage_ggsw(0);  // drained by the first spectrum-publish barrier
+    // L = 1: this wave's GGSW column for the next CMUX is loaded into registers right after the
+    // current MAC, so its L2/MALL latency hides behind the inverse FFT, the rotation and the
+    // forward FFT (the vmcnt wait lands at the MAC; no other vector loads in the loop).
+    constexpr bool PREF = PBS_GGSW_PREFETCH && L == 1 && !STAGE;
+    double2 gpre[PREF ? V * (K + 1) : 1];
+    auto prefetch = [&](int ii) {
+        const double2 *g = gcol + (size_t)ii * ggsw_stride;
+#pragma unroll
+        for (int s = 0; s < V; s++)
+#pragma unroll
+            for (int r = 0; r <= K; r++) gpre[s * (K + 1) + r] = g[(size_t)r * (K + 1) * M + s * 64];
+    };
+    if constexpr (PREF) {
+        prefetch(0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
 
     for (int i = 0; i < n; i++) {
         // Every LDS/GGSW address below is a function of the lane only (loop invariant); hoisted
@@ -193,7 +212,9 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), PBS_
         }
 
         cx acc[L > 1 ? V : 1];
-#pragma unroll
+        // L > 1: a runtime level loop (one copy of the FFT/MAC code); unrolled, the compiler
+        // overlaps consecutive levels and the register demand grows by ~(K+1)*V*4 per level
+#pragma unroll 1
         for (int lvl = L; lvl >= 1; lvl--) {
             cx v[V];
 #pragma unroll
@@ -226,7 +247,7 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), PBS_
                 cx o = (L > 1 && lvl != L) ? acc[L > 1 ? s : 0] : cx{0.0, 0.0};
 #pragma unroll
                 for (int r = 0; r <= K; r++) {
-                    const double2 gg = lm[(size_t)r * (K + 1) * M + s * 64];
+                    const double2 gg = PREF ? gpre[PREF ? s * (K + 1) + r : 0] : lm[(size_t)r * (K + 1) * M + s * 64];
                     double2 ff;
                     if (PBS_MAC_FROM_LDS) {  // every row from LDS: no wave-dependent branch
                         ff = reinterpret_cast<const double2 *>(xct + r * XL)[s * 64 + lane];
@@ -247,6 +268,11 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), PBS_
                 else v[s] = o;
             }
             sync();  // every wave is done reading the published spectra (and the staged GGSW)
+            if constexpr (PREF) {
+                __builtin_amdgcn_sched_barrier(0);
+                if (i + 1 < n) prefetch(i + 1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
             if constexpr (STAGE) {
                 // prefetch GGSW_{i+1} into LDS: overlaps the inverse FFT, the rotation and the
                 // forward FFT; the next publish barrier (its vmcnt(0)) retires it

@@ -14,11 +14,14 @@
 #ifndef PBS_MAC_SB
 #define PBS_MAC_SB 4  // MAC slots per scheduling region
 #endif
+#ifndef PBS_GGSW_PREFETCH
+#define PBS_GGSW_PREFETCH 0  // L = 1: GGSW_{i+1} column into registers during CMUX i's inverse FFT (measured 8% slower: AGPR shuffles)
+#endif
 #ifndef PBS_MAC_FROM_LDS
 #define PBS_MAC_FROM_LDS 0
 #endif
 #ifndef PBS_WAVES_PER_EU
-#define PBS_WAVES_PER_EU 1
+#define PBS_WAVES_PER_EU 0  // 0: per-shape default (PbsConfig::WPE); the multi-bit kernel uses 1
 #endif
 
 namespace tfhe_mi355 {

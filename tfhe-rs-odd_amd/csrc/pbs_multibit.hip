@@ -24,7 +24,7 @@
 namespace tfhe_mi355 {
 
 template <int N, int K, int L, int G>
-__global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU)
+__global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU > 0 ? PBS_WAVES_PER_EU : 1)
     pbs_multibit_kernel(MultiBitPbsLaunch a) {
     constexpr int M = N / 2;
     constexpr int V = M / 64;
