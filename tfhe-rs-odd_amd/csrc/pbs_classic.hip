@@ -11,7 +11,7 @@
 //   par_convert_polynomials_list_to_fourier           fft64/math/fft/mod.rs:719-764
 // The fork's PATTERN msgpack dump (bootstrap.rs:340-342) is deliberately not reproduced.
 //
-// Design (DESIGN.md "Kernels"): a workgroup bootstraps CPW ciphertexts (CPW = 1 by default),
+// Design (DESIGN.md "Kernels"): a workgroup bootstraps CPW ciphertexts (4 at 2_2, else 1),
 // one wavefront per GLWE polynomial ((k+1) waves per ciphertext).  Each wave keeps its
 // accumulator polynomial in registers (u64), rotates it through its LDS buffer, decomposes and
 // forward-FFTs it (row r = its polynomial); the (k+1) spectra of a ciphertext are exchanged
@@ -31,7 +31,7 @@
 namespace tfhe_mi355 {
 
 #ifndef PBS_CPW
-#define PBS_CPW 1
+#define PBS_CPW 0  // ciphertexts per workgroup; 0: per-shape default
 #endif
 #ifndef PBS_GGSW_LDS
 #define PBS_GGSW_LDS 0  // measured 2% slower than streaming from L2 (CPW=2 couples 4 waves); kept as an option
@@ -40,18 +40,26 @@ template <int N, int K, int L>
 struct PbsConfig {
     static constexpr int M = N / 2;
     static constexpr size_t GGSW_ELEMS = (size_t)L * (K + 1) * (K + 1) * M;  // double2 per GGSW
+    // 2_2 shape (N = 2048, k = 1, L = 1): 4 ciphertexts per workgroup at 2 waves/SIMD.  The MAC
+    // reads every row spectrum back from LDS (the own row's 64 VGPRs are free by then: 226
+    // VGPRs, no spills) and the twist/M table is dropped, so 31 KiB of tables + 8 x 16 KiB
+    // exchange buffers fill the CU's LDS (159 KiB): 8 waves per CU instead of 4, 77.5k -> 96.9k PBS/s.
+    static constexpr bool PACK4 = N == 2048 && K == 1 && L == 1;
+    static constexpr bool TWINV = PACK4 ? false : (bool)PBS_TWIST_INV_LDS;
+    static constexpr bool MAC_LDS = PACK4 ? true : (bool)PBS_MAC_FROM_LDS;
     // GGSW_i staged in LDS by async global->LDS loads and shared by the workgroup's ciphertexts;
     // fits next to the tables and 2 x (k+1) exchange buffers when it is <= 64 KiB
     // (only without the twist/M table: both do not fit next to four exchange buffers)
-    static constexpr bool STAGE = PBS_GGSW_LDS && !PBS_TWIST_INV_LDS && GGSW_ELEMS * 16 <= 65536;
-    static constexpr int CPW = STAGE ? 2 : PBS_CPW;  // ciphertexts per workgroup
+    static constexpr bool STAGE = PBS_GGSW_LDS && !TWINV && !PACK4 && GGSW_ELEMS * 16 <= 65536;
+    static constexpr int CPW = PBS_CPW > 0 ? PBS_CPW : STAGE ? 2 : PACK4 ? 4 : 1;
     static constexpr size_t lds_bytes() {
-        return PbsLds<M>::bytes((K + 1) * CPW) + (STAGE ? GGSW_ELEMS * 16 : 0);
+        return PbsLds<M, TWINV>::bytes((K + 1) * CPW) + (STAGE ? GGSW_ELEMS * 16 : 0);
     }
     static_assert(lds_bytes() <= 160 * 1024, "LDS per workgroup exceeds a CU");
-    // register budget: 1 wave/SIMD at N = 2048 (the headline shape needs ~360 VGPR+AGPR);
-    // smaller N fit 2 (N = 1024: <= 256) or 3 (N = 512: <= 168) waves per SIMD
-    static constexpr int WPE = PBS_WAVES_PER_EU > 0 ? PBS_WAVES_PER_EU : (N >= 2048 ? 1 : N == 1024 ? 2 : 3);
+    // register budget per wave: 2 waves/SIMD for the packed 2_2 shape and N = 1024 (<= 256),
+    // 3 at N = 512 (<= 168), 1 for the other N = 2048 shapes (~430 VGPR+AGPR at L = 2)
+    static constexpr int WPE = PBS_WAVES_PER_EU > 0 ? PBS_WAVES_PER_EU
+                                                    : (PACK4 ? 2 : N >= 2048 ? 1 : N == 1024 ? 2 : 3);
 };
 
 template <int N, int K, int L>
@@ -64,7 +72,7 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
     constexpr int CPW = Cfg::CPW;
     constexpr bool STAGE = Cfg::STAGE;
     using Fft = WaveFft<M>;
-    using Lay = PbsLds<M>;
+    using Lay = PbsLds<M, Cfg::TWINV>;
     constexpr int XL = Lay::XL;
     static_assert(sizeof(cx) * XL >= sizeof(uint64_t) * N, "exchange buffer holds one polynomial");
 
@@ -98,7 +106,7 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
     // twiddles and twist -> LDS (once per workgroup)
     for (int e = threadIdx.x; e < M; e += blockDim.x) {
         lds[Lay::twist_off + e] = a.twist[e];
-        if (PBS_TWIST_INV_LDS) lds[Lay::twinv_off + e] = a.twist_inv[e];
+        if (Cfg::TWINV) lds[Lay::twinv_off + e] = a.twist_inv[e];
     }
     const double2 *s_twinv = lds + Lay::twinv_off;
     Fft::Lds::template fill<M>(lds + Lay::s1_off, lds + Lay::s2_off, a.W, threadIdx.x, blockDim.x);
@@ -249,7 +257,7 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
                 for (int r = 0; r <= K; r++) {
                     const double2 gg = PREF ? gpre[PREF ? s * (K + 1) + r : 0] : lm[(size_t)r * (K + 1) * M + s * 64];
                     double2 ff;
-                    if (PBS_MAC_FROM_LDS) {  // every row from LDS: no wave-dependent branch
+                    if (Cfg::MAC_LDS) {  // every row from LDS: no wave-dependent branch
                         ff = reinterpret_cast<const double2 *>(xct + r * XL)[s * 64 + lane];
                     } else if (r == wave) {
                         ff = make_double2(v[s].re, v[s].im);
@@ -282,8 +290,8 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
                 Fft::inverse(v, xb, tw, lane, wsync);
 #pragma unroll
                 for (int b = 0; b < V; b++) {
-                    const double2 w = PBS_TWIST_INV_LDS ? s_twinv[lane + 64 * b] : s_twist[lane + 64 * b];
-                    const cx ws = PBS_TWIST_INV_LDS ? cx{w.x, w.y} : cx{norm * w.x, norm * w.y};
+                    const double2 w = Cfg::TWINV ? s_twinv[lane + 64 * b] : s_twist[lane + 64 * b];
+                    const cx ws = Cfg::TWINV ? cx{w.x, w.y} : cx{norm * w.x, norm * w.y};
                     backward_add(v[b], ws, c0[b], c0[V + b]);
                 }
             }
@@ -292,8 +300,8 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
             Fft::inverse(acc, xb, tw, lane, wsync);
 #pragma unroll
             for (int b = 0; b < V; b++) {
-                const double2 w = PBS_TWIST_INV_LDS ? s_twinv[lane + 64 * b] : s_twist[lane + 64 * b];
-                const cx ws = PBS_TWIST_INV_LDS ? cx{w.x, w.y} : cx{norm * w.x, norm * w.y};
+                const double2 w = Cfg::TWINV ? s_twinv[lane + 64 * b] : s_twist[lane + 64 * b];
+                const cx ws = Cfg::TWINV ? cx{w.x, w.y} : cx{norm * w.x, norm * w.y};
                 backward_add(acc[b], ws, c0[b], c0[V + b]);
             }
         }
