@@ -23,9 +23,25 @@
 
 namespace tfhe_mi355 {
 
+// Ciphertexts per workgroup and register budget.  As the classic 2_2 kernel: 4 ciphertexts per
+// workgroup at 2 waves/SIMD (31 KiB of tables + 8 x 16 KiB exchange buffers = 159 KiB of LDS),
+// the MAC reading every row spectrum from LDS and a one-slot issue window for the GGSW loads so
+// the wave fits 256 registers.
+#ifndef PBS_MB_CPW
+#define PBS_MB_CPW 4
+#endif
+#ifndef PBS_MB_WINDOW
+#define PBS_MB_WINDOW 4  // MAC slots whose GGSW loads may be in flight (4: 234 VGPRs at g = 3; 8 spills)
+#endif
+#ifndef PBS_MB_MAC_LDS
+#define PBS_MB_MAC_LDS 1
+#endif
+constexpr int mb_wpe() { return PBS_WAVES_PER_EU > 0 ? PBS_WAVES_PER_EU : (PBS_MB_CPW >= 4 ? 2 : 1); }
+
 template <int N, int K, int L, int G>
-__global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU > 0 ? PBS_WAVES_PER_EU : 1)
+__global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
     pbs_multibit_kernel(MultiBitPbsLaunch a) {
+    constexpr int CPW = PBS_MB_CPW;
     constexpr int M = N / 2;
     constexpr int V = M / 64;
     constexpr int LOG2N = ilog2(N);
@@ -40,10 +56,14 @@ __global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU > 0 ? PBS_WAVES
     double2 *lds = reinterpret_cast<double2 *>(smem);
     const double2 *s_twist = lds + Lay::twist_off;
 
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // polynomial / column
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wave = wid % (K + 1);  // polynomial / column
+    const int slot = wid / (K + 1);  // ciphertext slot in the workgroup
     const int lane0 = threadIdx.x & 63;
     int lane = lane0;
-    const int ct = blockIdx.x;
+    const int ct_raw = blockIdx.x * CPW + slot;
+    const bool active = ct_raw < a.count;  // idle slots compute on a valid ct, store nothing
+    const int ct = active ? ct_raw : a.count - 1;
     const int n = a.n;
     const int beta = a.base_log;
     const uint32_t dmask = (1u << beta) - 1;
@@ -63,7 +83,7 @@ __global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU > 0 ? PBS_WAVES
     const typename Fft::Lds tw{lds + Lay::s1_off, lds + Lay::s2_off};
     sync();
 
-    cx *xct = reinterpret_cast<cx *>(lds + Lay::xbuf_off);
+    cx *xct = reinterpret_cast<cx *>(lds + Lay::xbuf_off) + (size_t)slot * (K + 1) * XL;  // this ct's buffers
     cx *xb = xct + wave * XL;
     uint64_t *xb64 = reinterpret_cast<uint64_t *>(xb);
     const uint64_t *in = a.lwe_in + (size_t)ct * (n + 1);
@@ -153,8 +173,8 @@ __global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU > 0 ? PBS_WAVES
                 // Issue window: slot s's GGSW loads and monomial reads take their addresses from
                 // an opaque copy that depends on the result of slot s-2, so at most two slots of
                 // operands are in flight (hoisted all at once they need ~1 KiB/lane and spill).
-                if (s >= 2) {
-                    const double dep = (L > 1) ? acc[L > 1 ? s - 2 : 0].re : v[s - 2].re;
+                if (s >= PBS_MB_WINDOW) {
+                    const double dep = (L > 1) ? acc[L > 1 ? s - PBS_MB_WINDOW : 0].re : v[s - PBS_MB_WINDOW].re;
                     asm volatile("" : "+v"(lm) : "v"(dep));
 #pragma unroll
                     for (int sel = 1; sel < NSEL; sel++) asm volatile("" : "+v"(tb[sel]) : "v"(dep));
@@ -185,7 +205,7 @@ __global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU > 0 ? PBS_WAVES
                         kb.y = fma(gg.x, mono[sel].im, fma(gg.y, mono[sel].re, kb.y));
                     }
                     double2 ff;
-                    if (PBS_MAC_FROM_LDS) {  // every row from LDS: no wave-dependent branch
+                    if (PBS_MB_MAC_LDS) {  // every row from LDS: no wave-dependent branch
                         ff = reinterpret_cast<const double2 *>(xct + r * XL)[s * 64 + lane];
                     } else if (r == wave) {
                         ff = make_double2(v[s].re, v[s].im);
@@ -226,6 +246,7 @@ __global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU > 0 ? PBS_WAVES
     }
 
     if (a.glwe_out) {  // bootstrap_without_sample_extract (fork, bootstrap.rs:383-412)
+        if (!active) return;
         uint64_t *g = a.lwe_out + ((size_t)ct * (K + 1) + wave) * N;
 #pragma unroll
         for (int h = 0; h < 2 * V; h++) g[lane + 64 * h] = c0[h];
@@ -236,6 +257,7 @@ __global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU > 0 ? PBS_WAVES
 #pragma unroll
     for (int h = 0; h < 2 * V; h++) xb64[lane + 64 * h] = c0[h];
     wsync();
+    if (!active) return;
     uint64_t *out = a.lwe_out + (size_t)ct * (K * N + 1);
     if (wave < K) {
         for (int j = lane; j < N; j += 64) out[wave * N + j] = j == 0 ? xb64[0] : 0 - xb64[N - j];
@@ -247,10 +269,12 @@ __global__ void __launch_bounds__(64 * (K + 1), PBS_WAVES_PER_EU > 0 ? PBS_WAVES
 template <int N, int K, int L, int G>
 static hipError_t launch_mb_t(const MultiBitPbsLaunch &a, hipStream_t s) {
     constexpr int M = N / 2;
-    const size_t lds = PbsLds<M, PBS_MB_TWIST_INV_LDS>::bytes(K + 1);
+    constexpr size_t lds = PbsLds<M, PBS_MB_TWIST_INV_LDS>::bytes((K + 1) * PBS_MB_CPW);
+    static_assert(lds <= 160 * 1024, "LDS per workgroup exceeds a CU");
     if (a.count == 0) return hipSuccess;
     if (a.n % G) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((pbs_multibit_kernel<N, K, L, G>), dim3(a.count), dim3(64 * (K + 1)), lds, s, a);
+    const int blocks = (a.count + PBS_MB_CPW - 1) / PBS_MB_CPW;
+    hipLaunchKernelGGL((pbs_multibit_kernel<N, K, L, G>), dim3(blocks), dim3(64 * (K + 1) * PBS_MB_CPW), lds, s, a);
     return hipGetLastError();
 }
 
