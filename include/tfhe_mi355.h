@@ -119,6 +119,22 @@ int tfhe_mi355_blind_rotate_async(TfheMi355Context *ctx, const uint64_t *d_lwe_i
                                   const uint64_t *d_luts, size_t lut_count, const uint32_t *d_lut_indexes,
                                   size_t count, void *stream);
 
+/* Seeded (compressed) keys: the reference's SeededLweBootstrapKey / SeededLweKeyswitchKey
+ * (shortint CompressedServerKey) hold only the bodies and a CompressionSeed (u128 = hi:lo); every
+ * mask is regenerated on the GPU from the concrete-csprng AES-CTR stream of that seed.
+ * Replace decompress_seeded_lwe_bootstrap_key (seeded_lwe_bootstrap_key_decompression.rs) +
+ * the Fourier conversion, and decompress_seeded_lwe_keyswitch_key
+ * (seeded_lwe_keyswitch_key_decompression.rs).  bodies: BSK [ggsw_count][L][k+1][N] (multi-bit:
+ * ggsw_count = (n/g) 2^g, grouped as the standard key), KSK [k*N][ks_level]. */
+int tfhe_mi355_bootstrap_key_upload_seeded(TfheMi355Context *ctx, const uint64_t *bodies, size_t len,
+                                           uint64_t seed_lo, uint64_t seed_hi);
+int tfhe_mi355_keyswitch_key_upload_seeded(TfheMi355Context *ctx, const uint64_t *bodies, size_t len,
+                                           uint64_t seed_lo, uint64_t seed_hi);
+/* the raw mask stream on the device: word w = little-endian bytes [1 + 8w, 9 + 8w) of the
+ * AES-CTR table of the seed (concrete-csprng generators/aes_ctr, started at TableIndex::SECOND) */
+int tfhe_mi355_csprng_mask_words(TfheMi355Context *ctx, uint64_t seed_lo, uint64_t seed_hi, uint64_t *out,
+                                 size_t words);
+
 /* LWE -> GLWE packing keyswitch of the fork's tree bootstrapping (gadget ServerKey
  * lwe_packing_keyswitch_key, gadget/engine/bootstrapping.rs:345-352, used at :713,:744).
  * Key layout [k*N][level][(k+1)*N] (levels stored L..1), input key = the big LWE key.
@@ -209,6 +225,17 @@ int tfhe_mi355_client_gen_packing_keyswitch_key(uint64_t seed, const uint64_t *i
                                                 const uint64_t *glwe_sk, uint32_t k, uint32_t N,
                                                 uint32_t base_log, uint32_t level, double std_dev,
                                                 uint64_t *pksk, uint32_t threads);
+/* seeded keys (masks from the AES-CTR stream of mask_seed, noise from noise_seed); bodies only */
+int tfhe_mi355_client_gen_seeded_bootstrap_key(uint64_t noise_seed, uint64_t mask_seed_lo, uint64_t mask_seed_hi,
+                                               const uint64_t *lwe_sk, uint32_t n, const uint64_t *glwe_sk,
+                                               uint32_t k, uint32_t N, uint32_t base_log, uint32_t level,
+                                               double std_dev, uint64_t *bodies, uint32_t threads);
+int tfhe_mi355_client_gen_seeded_keyswitch_key(uint64_t noise_seed, uint64_t mask_seed_lo, uint64_t mask_seed_hi,
+                                               const uint64_t *in_sk, uint32_t in_dim, const uint64_t *out_sk,
+                                               uint32_t out_dim, uint32_t base_log, uint32_t level, double std_dev,
+                                               uint64_t *bodies);
+int tfhe_mi355_client_csprng_mask_words(uint64_t seed_lo, uint64_t seed_hi, uint64_t first_word, size_t count,
+                                        uint64_t *out);
 int tfhe_mi355_client_lwe_encrypt(uint64_t seed, const uint64_t *sk, uint32_t n, const uint64_t *plaintexts,
                                   size_t count, double std_dev, uint64_t *cts);
 int tfhe_mi355_client_lwe_decrypt(const uint64_t *sk, uint32_t n, const uint64_t *cts, size_t count,

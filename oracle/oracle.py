@@ -82,6 +82,16 @@ def lib():
                                                   ctypes.c_int, u64p, u64p, ctypes.c_size_t]
         L.orc_glwe_poly_mul.argtypes = [ctypes.c_int, ctypes.c_int, u64p, ctypes.c_size_t, u64p,
                                         ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, u64p]
+        L.orc_aes128_expand.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint8)]
+        L.orc_aes128_encrypt.argtypes = [ctypes.POINTER(ctypes.c_uint8), ctypes.c_char_p,
+                                         ctypes.POINTER(ctypes.c_uint8)]
+        L.orc_csprng_bytes.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t,
+                                       ctypes.POINTER(ctypes.c_uint8)]
+        L.orc_seeded_mask_words.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, u64p]
+        L.orc_decompress_seeded_bsk.argtypes = [ctypes.c_uint64, ctypes.c_uint64, u64p, ctypes.c_size_t,
+                                                ctypes.c_int, ctypes.c_int, ctypes.c_int, u64p]
+        L.orc_decompress_seeded_ksk.argtypes = [ctypes.c_uint64, ctypes.c_uint64, u64p, ctypes.c_size_t,
+                                                ctypes.c_int, ctypes.c_int, u64p]
         if hasattr(L, "orc_mb_pbs_batch"):
             L.orc_mb_fbsk_create.restype = ctypes.c_void_p
             L.orc_mb_fbsk_create.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -338,6 +348,51 @@ def glwe_poly_mul(k, N, glwe_in, polys, extract: bool) -> np.ndarray:
     assert v.shape[1] == J and v.shape[2] == N and g.shape[2] == (k + 1) * N
     out = np.zeros((count, npoly, k * N + 1 if extract else (k + 1) * N), dtype=np.uint64)
     lib().orc_glwe_poly_mul(k, N, _p(g), J, _p(v), npoly, count, int(extract), _p(out))
+    return out
+
+
+# ---- seeded keys (csprng_oracle.c) ----------------------------------------------------------
+def aes128_encrypt(key: bytes, block: bytes) -> bytes:
+    rk = (ctypes.c_uint8 * 176)()
+    out = (ctypes.c_uint8 * 16)()
+    lib().orc_aes128_expand(key, rk)
+    lib().orc_aes128_encrypt(rk, block, out)
+    return bytes(out)
+
+
+def aes128_round_keys(key: bytes) -> bytes:
+    rk = (ctypes.c_uint8 * 176)()
+    lib().orc_aes128_expand(key, rk)
+    return bytes(rk)
+
+
+def _seed(seed: int):
+    return seed & 0xFFFFFFFFFFFFFFFF, (seed >> 64) & 0xFFFFFFFFFFFFFFFF
+
+
+def csprng_bytes(seed: int, offset: int, count: int) -> bytes:
+    out = (ctypes.c_uint8 * count)()
+    lib().orc_csprng_bytes(*_seed(seed), offset, count, out)
+    return bytes(out)
+
+
+def seeded_mask_words(seed: int, first_word: int, count: int) -> np.ndarray:
+    out = np.zeros(count, dtype=np.uint64)
+    lib().orc_seeded_mask_words(*_seed(seed), first_word, count, _p(out))
+    return out
+
+
+def decompress_seeded_bsk(seed: int, bodies, n_ggsw: int, level: int, k: int, N: int) -> np.ndarray:
+    b = _u64(bodies)
+    out = np.zeros(n_ggsw * level * (k + 1) * (k + 1) * N, dtype=np.uint64)
+    lib().orc_decompress_seeded_bsk(*_seed(seed), _p(b), n_ggsw, level, k, N, _p(out))
+    return out
+
+
+def decompress_seeded_ksk(seed: int, bodies, in_dim: int, level: int, out_dim: int) -> np.ndarray:
+    b = _u64(bodies)
+    out = np.zeros(in_dim * level * (out_dim + 1), dtype=np.uint64)
+    lib().orc_decompress_seeded_ksk(*_seed(seed), _p(b), in_dim, level, out_dim, _p(out))
     return out
 
 

@@ -410,6 +410,92 @@ int tfhe_mi355_bootstrap_key_upload(TfheMi355Context *ctx, const uint64_t *bsk, 
     });
 }
 
+namespace {
+// AES tables of a compression seed on the device (a few KiB, one per call)
+void upload_aes_tables(TfheMi355Context *c, uint64_t seed_lo, uint64_t seed_hi, DeviceBuffer &d) {
+    std::vector<unsigned char> host(aes_tables_bytes());
+    aes_tables_build(seed_lo, seed_hi, host.data());
+    d.reserve(host.size());
+    check(hipMemcpyAsync(d.ptr, host.data(), host.size(), hipMemcpyHostToDevice, c->stream), "upload aes tables");
+    check(hipStreamSynchronize(c->stream), "aes tables sync");
+}
+}  // namespace
+
+int tfhe_mi355_bootstrap_key_upload_seeded(TfheMi355Context *ctx, const uint64_t *bodies, size_t len,
+                                           uint64_t seed_lo, uint64_t seed_hi) {
+    return guarded([&] {
+        if (!ctx || !bodies) fail("null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        const size_t rows = ctx->ggsw_count() * ctx->p.pbs_level * (ctx->k() + 1);
+        if (len != rows * ctx->N()) fail("seeded bootstrapping key has %zu body words, expected %zu", len, rows * ctx->N());
+        DeviceBuffer tab;
+        upload_aes_tables(ctx, seed_lo, seed_hi, tab);
+        DeviceBuffer d_bodies;
+        d_bodies.reserve(len * sizeof(uint64_t));
+        check(hipMemcpyAsync(d_bodies.ptr, bodies, len * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream),
+              "upload bodies");
+        ctx->std_staging.reserve(ctx->std_bsk_len() * sizeof(uint64_t));
+        check(launch_seeded_decompress(tab.ptr, (const uint64_t *)d_bodies.ptr, rows, ctx->k() * ctx->N(), ctx->N(),
+                                       (uint64_t *)ctx->std_staging.ptr, ctx->stream),
+              "seeded bsk decompression");
+        ctx->fbsk.reserve(ctx->fourier_bsk_bytes());
+        check(convert_bsk(ctx, (const uint64_t *)ctx->std_staging.ptr, ctx->std_bsk_len() / ctx->N(), ctx->stream),
+              "bsk conversion");
+        check(hipStreamSynchronize(ctx->stream), "seeded bsk sync");
+        ctx->std_staging.release();
+        d_bodies.release();
+        tab.release();
+        ctx->fbsk_ready = true;
+    });
+}
+
+int tfhe_mi355_keyswitch_key_upload_seeded(TfheMi355Context *ctx, const uint64_t *bodies, size_t len,
+                                           uint64_t seed_lo, uint64_t seed_hi) {
+    return guarded([&] {
+        if (!ctx || !bodies) fail("null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        const size_t rows = ctx->big_dim() * ctx->p.ks_level;
+        if (len != rows) fail("seeded keyswitching key has %zu body words, expected %zu", len, rows);
+        DeviceBuffer tab;
+        upload_aes_tables(ctx, seed_lo, seed_hi, tab);
+        DeviceBuffer d_bodies;
+        d_bodies.reserve(len * sizeof(uint64_t));
+        check(hipMemcpyAsync(d_bodies.ptr, bodies, len * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream),
+              "upload bodies");
+        ctx->ksk_ready = false;
+        ctx->ksk.reserve(ctx->ksk_len() * sizeof(uint64_t));
+        check(launch_seeded_decompress(tab.ptr, (const uint64_t *)d_bodies.ptr, rows, ctx->n(), 1,
+                                       (uint64_t *)ctx->ksk.ptr, ctx->stream),
+              "seeded ksk decompression");
+        repack_ksk(ctx, ctx->stream);
+        check(hipStreamSynchronize(ctx->stream), "seeded ksk sync");
+        d_bodies.release();
+        tab.release();
+        ctx->ksk_ready = true;
+    });
+}
+
+int tfhe_mi355_csprng_mask_words(TfheMi355Context *ctx, uint64_t seed_lo, uint64_t seed_hi, uint64_t *out,
+                                 size_t words) {
+    return guarded([&] {
+        if (!ctx || (!out && words)) fail("null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        if (words == 0) return;
+        DeviceBuffer tab;
+        upload_aes_tables(ctx, seed_lo, seed_hi, tab);
+        ctx->io_out.reserve(words * sizeof(uint64_t));
+        check(launch_seeded_decompress(tab.ptr, nullptr, 1, words, 0, (uint64_t *)ctx->io_out.ptr, ctx->stream),
+              "csprng");
+        check(hipMemcpyAsync(out, ctx->io_out.ptr, words * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream),
+              "D2H words");
+        check(hipStreamSynchronize(ctx->stream), "csprng sync");
+        tab.release();
+    });
+}
+
 int tfhe_mi355_bootstrap_key_convert_async(TfheMi355Context *ctx, const uint64_t *d_bsk, size_t len,
                                            void *stream) {
     return guarded([&] {

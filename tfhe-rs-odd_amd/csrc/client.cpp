@@ -6,8 +6,9 @@
 //                                         (commons/math/torus/mod.rs:71-78)
 //   GGSW rows of the BSK                 (algorithms/ggsw_encryption.rs:116-150, 300-331)
 //   KSK levels stored L..1               (algorithms/lwe_keyswitch_key_generation.rs:60-135)
-// The randomness source is a seeded xoshiro256** (the reference's AES-CTR CSPRNG is not part of
-// the GPU path); keys are deterministic per (seed, index) whatever the thread count.
+// The randomness source is a seeded xoshiro256**; keys are deterministic per (seed, index)
+// whatever the thread count.  Seeded keys take their masks from the reference's AES-CTR mask
+// stream of the compression seed (csprng.hip), so that the GPU can regenerate them.
 #include <cmath>
 #include <complex>
 #include <cstdint>
@@ -20,6 +21,13 @@
 #include <thread>
 #include <vector>
 #include <atomic>
+#include <algorithm>
+
+namespace tfhe_mi355 {  // csprng.hip (host side): AES-128 tables / block function
+size_t aes_tables_bytes();
+void aes_tables_build(uint64_t seed_lo, uint64_t seed_hi, void *host_tables);
+void aes128_encrypt_host(const void *host_tables, uint32_t s[4]);
+}  // namespace tfhe_mi355
 
 #include "../../include/tfhe_mi355.h"
 #include "errors.h"
@@ -148,17 +156,47 @@ void negacyclic_binary_add(uint64_t *body, const uint64_t *a, const uint64_t *s,
     }
 }
 
-void glwe_encrypt_assign(Rng &r, uint64_t *glwe, const uint64_t *key, int k, int N, double std) {
+// AES-CTR mask words of a compression seed (csprng.hip; the reference's seeded-key mask stream:
+// word w = little-endian bytes [1 + 8w, 9 + 8w) of the AES-CTR table)
+struct SeededMask {
+    std::vector<unsigned char> tables;
+    SeededMask(uint64_t lo, uint64_t hi) : tables(tfhe_mi355::aes_tables_bytes()) {
+        tfhe_mi355::aes_tables_build(lo, hi, tables.data());
+    }
+    void words(uint64_t first, size_t count, uint64_t *out) const {
+        uint64_t cur = UINT64_MAX;
+        unsigned char blk[16];
+        unsigned char *dst = reinterpret_cast<unsigned char *>(out);
+        for (size_t i = 0; i < 8 * count; i++) {
+            const uint64_t g = 1 + 8 * first + i, a = g / 16;
+            if (a != cur) {
+                uint32_t st[4] = {(uint32_t)a, (uint32_t)(a >> 32), 0u, 0u};
+                tfhe_mi355::aes128_encrypt_host(tables.data(), st);
+                std::memcpy(blk, st, 16);
+                cur = a;
+            }
+            dst[i] = blk[g % 16];
+        }
+    }
+};
+
+void glwe_encrypt_assign(Rng &r, uint64_t *glwe, const uint64_t *key, int k, int N, double std,
+                         const SeededMask *mask = nullptr, uint64_t mask_first_word = 0) {
     uint64_t *body = glwe + (size_t)k * N;
-    for (size_t i = 0; i < (size_t)k * N; i++) glwe[i] = r.next();
+    if (mask)
+        mask->words(mask_first_word, (size_t)k * N, glwe);
+    else
+        for (size_t i = 0; i < (size_t)k * N; i++) glwe[i] = r.next();
     for (int j = 0; j < N; j++) body[j] += r.gaussian_torus(std);
     for (int p = 0; p < k; p++) negacyclic_binary_add(body, glwe + (size_t)p * N, key + (size_t)p * N, N);
 }
 
-void lwe_encrypt(Rng &r, const uint64_t *sk, int n, uint64_t pt, double std, uint64_t *ct) {
+void lwe_encrypt(Rng &r, const uint64_t *sk, int n, uint64_t pt, double std, uint64_t *ct,
+                 const SeededMask *mask = nullptr, uint64_t mask_first_word = 0) {
     uint64_t b = pt + r.gaussian_torus(std);
+    if (mask) mask->words(mask_first_word, (size_t)n, ct);
     for (int i = 0; i < n; i++) {
-        ct[i] = r.next();
+        if (!mask) ct[i] = r.next();
         b += ct[i] * sk[i];
     }
     ct[n] = b;
@@ -181,10 +219,11 @@ int tfhe_mi355_client_gen_binary_key(uint64_t seed, uint64_t stream, uint64_t *k
 namespace {
 // GGSW list generation shared by the classic and multi-bit keys: GGSW i encrypts the constant
 // plaintext msg(i) (ggsw_encryption.rs:116-150,300-331), with its own RNG stream.
+// mask: optional seeded mask stream (GLWE row j of the list takes mask words [j kN, (j+1) kN))
 template <class Msg>
 void gen_ggsw_list(uint64_t seed, uint64_t stream_base, uint32_t items, const uint64_t *glwe_sk, uint32_t k,
                    uint32_t N, uint32_t base_log, uint32_t level, double std, uint64_t *out, uint32_t threads,
-                   Msg msg) {
+                   Msg msg, const SeededMask *mask = nullptr) {
     const size_t glwe_len = (size_t)(k + 1) * N, ggsw_len = (size_t)level * (k + 1) * glwe_len;
     std::atomic<uint32_t> next{0};
     auto work = [&] {
@@ -205,7 +244,8 @@ void gen_ggsw_list(uint64_t seed, uint64_t stream_base, uint32_t items, const ui
                         std::memset(body, 0, sizeof(uint64_t) * N);
                         body[0] = 0 - factor;
                     }
-                    glwe_encrypt_assign(r, g, glwe_sk, (int)k, (int)N, std);
+                    const uint64_t row_index = ((uint64_t)i * level + (lvl - 1)) * (k + 1) + row;
+                    glwe_encrypt_assign(r, g, glwe_sk, (int)k, (int)N, std, mask, row_index * k * N);
                 }
             }
         }
@@ -297,6 +337,54 @@ int tfhe_mi355_client_gen_packing_keyswitch_key(uint64_t seed, const uint64_t *i
         for (uint32_t t = 1; t < nt; t++) th.emplace_back(work);
         work();
         for (auto &t : th) t.join();
+    });
+}
+
+// Seeded keys (the reference's SeededLweBootstrapKey / SeededLweKeyswitchKey with a
+// CompressionSeed, seeded_lwe_bootstrap_key_generation.rs, seeded_lwe_keyswitch_key_generation.rs):
+// masks from the AES-CTR stream of (mask_seed_lo, mask_seed_hi), noise from the engine's own RNG;
+// only the bodies are returned -- [n][L][k+1][N] and [in_dim][L].
+int tfhe_mi355_client_gen_seeded_bootstrap_key(uint64_t noise_seed, uint64_t mask_seed_lo, uint64_t mask_seed_hi,
+                                               const uint64_t *lwe_sk, uint32_t n, const uint64_t *glwe_sk,
+                                               uint32_t k, uint32_t N, uint32_t base_log, uint32_t level, double std,
+                                               uint64_t *bodies, uint32_t threads) {
+    return guard([&] {
+        if (!lwe_sk || !glwe_sk || !bodies) throw std::invalid_argument("null argument");
+        const SeededMask mask(mask_seed_lo, mask_seed_hi);
+        const size_t glwe = (size_t)(k + 1) * N, rows = (size_t)n * level * (k + 1);
+        std::vector<uint64_t> full(glwe * rows);
+        gen_ggsw_list(noise_seed, 0x6000000ULL, n, glwe_sk, k, N, base_log, level, std, full.data(), threads,
+                      [&](uint32_t i) { return lwe_sk[i]; }, &mask);
+        for (size_t row = 0; row < rows; row++)
+            std::memcpy(bodies + row * N, full.data() + row * glwe + (size_t)k * N, sizeof(uint64_t) * N);
+    });
+}
+
+int tfhe_mi355_client_gen_seeded_keyswitch_key(uint64_t noise_seed, uint64_t mask_seed_lo, uint64_t mask_seed_hi,
+                                               const uint64_t *in_sk, uint32_t in_dim, const uint64_t *out_sk,
+                                               uint32_t out_dim, uint32_t base_log, uint32_t level, double std,
+                                               uint64_t *bodies) {
+    return guard([&] {
+        if (!in_sk || !out_sk || !bodies) throw std::invalid_argument("null argument");
+        const SeededMask mask(mask_seed_lo, mask_seed_hi);
+        Rng r(noise_seed, 0x7000000ULL);
+        std::vector<uint64_t> ct((size_t)out_dim + 1);
+        for (uint32_t i = 0; i < in_dim; i++)
+            for (uint32_t l = 0; l < level; l++) {
+                const uint32_t lvl = level - l;
+                const uint64_t j = (uint64_t)i * level + l;
+                lwe_encrypt(r, out_sk, (int)out_dim, in_sk[i] << (64 - base_log * lvl), std, ct.data(), &mask,
+                            j * out_dim);
+                bodies[j] = ct[out_dim];
+            }
+    });
+}
+
+int tfhe_mi355_client_csprng_mask_words(uint64_t seed_lo, uint64_t seed_hi, uint64_t first_word, size_t count,
+                                        uint64_t *out) {
+    return guard([&] {
+        if (!out && count) throw std::invalid_argument("null argument");
+        SeededMask(seed_lo, seed_hi).words(first_word, count, out);
     });
 }
 

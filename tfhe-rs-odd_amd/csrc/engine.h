@@ -113,4 +113,12 @@ struct GlwePolyMulLaunch {
 };
 hipError_t launch_glwe_poly_mul(const GlwePolyMulLaunch &a, hipStream_t s);
 
+// seeded-key decompression (csprng.hip): AES-CTR mask stream of the compression seed written as
+// `row_words` mask words per row, followed by `body_words` copied from d_bodies, for `rows` rows
+size_t aes_tables_bytes();
+void aes_tables_build(uint64_t seed_lo, uint64_t seed_hi, void *host_tables);
+void aes128_encrypt_host(const void *host_tables, uint32_t s[4]);
+hipError_t launch_seeded_decompress(const void *d_tables, const uint64_t *d_bodies, size_t rows, size_t row_words,
+                                    size_t body_words, uint64_t *d_out, hipStream_t s);
+
 }  // namespace tfhe_mi355

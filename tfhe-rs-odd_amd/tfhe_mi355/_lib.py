@@ -82,6 +82,17 @@ SIGNATURES = [
     ("tfhe_mi355_client_gen_packing_keyswitch_key", ctypes.c_int,
      [ctypes.c_uint64, u64p, ctypes.c_uint32, u64p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
       ctypes.c_uint32, ctypes.c_double, u64p, ctypes.c_uint32]),
+    ("tfhe_mi355_bootstrap_key_upload_seeded", ctypes.c_int, [vp, u64p, sz, ctypes.c_uint64, ctypes.c_uint64]),
+    ("tfhe_mi355_keyswitch_key_upload_seeded", ctypes.c_int, [vp, u64p, sz, ctypes.c_uint64, ctypes.c_uint64]),
+    ("tfhe_mi355_csprng_mask_words", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64, u64p, sz]),
+    ("tfhe_mi355_client_gen_seeded_bootstrap_key", ctypes.c_int,
+     [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u64p, ctypes.c_uint32, u64p, ctypes.c_uint32,
+      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double, u64p, ctypes.c_uint32]),
+    ("tfhe_mi355_client_gen_seeded_keyswitch_key", ctypes.c_int,
+     [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u64p, ctypes.c_uint32, u64p, ctypes.c_uint32,
+      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double, u64p]),
+    ("tfhe_mi355_client_csprng_mask_words", ctypes.c_int,
+     [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, sz, u64p]),
     ("tfhe_mi355_client_lwe_encrypt", ctypes.c_int,
      [ctypes.c_uint64, u64p, ctypes.c_uint32, u64p, sz, ctypes.c_double, u64p]),
     ("tfhe_mi355_client_lwe_decrypt", ctypes.c_int, [u64p, ctypes.c_uint32, u64p, sz, u64p]),

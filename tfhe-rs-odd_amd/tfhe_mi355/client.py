@@ -72,6 +72,43 @@ def gen_packing_keyswitch_key(seed, in_sk, glwe_sk, glwe_dimension, polynomial_s
     return out
 
 
+def _seed_parts(seed: int):
+    return seed & 0xFFFFFFFFFFFFFFFF, (seed >> 64) & 0xFFFFFFFFFFFFFFFF
+
+
+def csprng_mask_words(compression_seed: int, first_word: int, count: int) -> np.ndarray:
+    """Mask words of a seeded key: word w = LE u64 of AES-CTR stream bytes [1 + 8w, 9 + 8w)."""
+    out = np.empty(count, dtype=np.uint64)
+    lo, hi = _seed_parts(compression_seed)
+    _lib.call("tfhe_mi355_client_csprng_mask_words", lo, hi, first_word, count, _ptr(out))
+    return out
+
+
+def gen_seeded_bootstrap_key(noise_seed, compression_seed: int, lwe_sk, glwe_sk, glwe_dimension, polynomial_size,
+                             base_log, level, std_dev, threads: int = 0) -> np.ndarray:
+    """SeededLweBootstrapKey bodies [n][L][k+1][N]; masks = the AES-CTR stream of compression_seed."""
+    lwe_sk = np.ascontiguousarray(lwe_sk, dtype=np.uint64)
+    glwe_sk = np.ascontiguousarray(glwe_sk, dtype=np.uint64)
+    k, N = glwe_dimension, polynomial_size
+    out = np.empty(len(lwe_sk) * level * (k + 1) * N, dtype=np.uint64)
+    lo, hi = _seed_parts(compression_seed)
+    _lib.call("tfhe_mi355_client_gen_seeded_bootstrap_key", noise_seed, lo, hi, _ptr(lwe_sk), len(lwe_sk),
+              _ptr(glwe_sk), k, N, base_log, level, std_dev, _ptr(out), threads)
+    return out
+
+
+def gen_seeded_keyswitch_key(noise_seed, compression_seed: int, in_sk, out_sk, base_log, level,
+                             std_dev) -> np.ndarray:
+    """SeededLweKeyswitchKey bodies [in_dim][L]."""
+    in_sk = np.ascontiguousarray(in_sk, dtype=np.uint64)
+    out_sk = np.ascontiguousarray(out_sk, dtype=np.uint64)
+    out = np.empty(len(in_sk) * level, dtype=np.uint64)
+    lo, hi = _seed_parts(compression_seed)
+    _lib.call("tfhe_mi355_client_gen_seeded_keyswitch_key", noise_seed, lo, hi, _ptr(in_sk), len(in_sk),
+              _ptr(out_sk), len(out_sk), base_log, level, std_dev, _ptr(out))
+    return out
+
+
 def lwe_encrypt(seed, sk, plaintexts, std_dev) -> np.ndarray:
     sk = np.ascontiguousarray(sk, dtype=np.uint64)
     pts = np.ascontiguousarray(plaintexts, dtype=np.uint64).ravel()

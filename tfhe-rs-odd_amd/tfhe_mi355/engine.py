@@ -184,6 +184,24 @@ class Engine:
                   L.shape[0], idxp, x.shape[0])
         return out
 
+    def upload_seeded_bootstrap_key(self, bodies: np.ndarray, compression_seed: int) -> None:
+        """decompress_seeded_lwe_bootstrap_key on the GPU + Fourier conversion."""
+        b = _u64(bodies)
+        _lib.call("tfhe_mi355_bootstrap_key_upload_seeded", self._h, _ptr(b), b.size,
+                  compression_seed & 0xFFFFFFFFFFFFFFFF, (compression_seed >> 64) & 0xFFFFFFFFFFFFFFFF)
+
+    def upload_seeded_keyswitch_key(self, bodies: np.ndarray, compression_seed: int) -> None:
+        """decompress_seeded_lwe_keyswitch_key on the GPU."""
+        b = _u64(bodies)
+        _lib.call("tfhe_mi355_keyswitch_key_upload_seeded", self._h, _ptr(b), b.size,
+                  compression_seed & 0xFFFFFFFFFFFFFFFF, (compression_seed >> 64) & 0xFFFFFFFFFFFFFFFF)
+
+    def csprng_mask_words(self, compression_seed: int, count: int) -> np.ndarray:
+        out = np.empty(count, dtype=np.uint64)
+        _lib.call("tfhe_mi355_csprng_mask_words", self._h, compression_seed & 0xFFFFFFFFFFFFFFFF,
+                  (compression_seed >> 64) & 0xFFFFFFFFFFFFFFFF, _ptr(out), count)
+        return out
+
     def upload_packing_keyswitch_key(self, pksk: np.ndarray, base_log: int, level: int) -> None:
         k = _u64(pksk)
         _lib.call("tfhe_mi355_packing_keyswitch_key_upload", self._h, _ptr(k), k.size, base_log, level)
