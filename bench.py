@@ -66,6 +66,9 @@ PARAMS = {  # --params choice -> (parameter set name, workload text, kernel name
     "aes40": ("GADGET_AES_PARAMETERS_40",
               "batch of 4096 independent classic PBS per GPU at the fork's AES_PARAMETERS_40",
               "pbs_classic_kernel<512,3,4>"),
+    "sha3": ("GADGET_SHA3_PARAMETERS_40",
+             "batch of 4096 independent classic PBS per GPU at the fork's SHA3_PARAMETERS_40",
+             "pbs_classic_kernel<256,5,1>"),
 }
 
 

@@ -1,5 +1,5 @@
 """The classic PBS at the fork's gadget parameter sets (k = 2, 3; N = 512, 1024; levels 1-4;
-gadget/parameters/mod.rs:84-222), bit-exact against the oracle, plus one gadget evaluation per
+gadget/parameters/mod.rs:84-222; SHA3_40 at k = 5, N = 256), bit-exact against the oracle, plus one gadget evaluation per
 PBS order (KS -> PBS for Big-key sets, PBS -> KS for Small-key sets) checked by decryption.
 """
 import numpy as np
@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 def _supported():
     from tfhe_mi355.parameters import GADGET_ALL
 
-    return [p for p in GADGET_ALL if p.polynomial_size >= 512]
+    return list(GADGET_ALL)
 
 
 @pytest.mark.parametrize("params", _supported(), ids=lambda p: p.name)
@@ -37,16 +37,17 @@ def test_gadget_params_pbs_bit_exact(orc, params):
     assert np.array_equal(got, exp)
 
 
-def test_gadget_params_unsupported_n256_fails_loudly():
+def test_gadget_params_unsupported_shape_fails_loudly():
     from tfhe_mi355 import Engine
     from tfhe_mi355._lib import EngineError
     from tfhe_mi355.parameters import GADGET_SHA3_PARAMETERS_40
 
     with pytest.raises(EngineError, match="no kernel"):
-        Engine(GADGET_SHA3_PARAMETERS_40, 0)
+        Engine(GADGET_SHA3_PARAMETERS_40.with_(polynomial_size=128), 0)
 
 
-@pytest.mark.parametrize("name", ["GADGET_ASCON_PARAMETERS_40", "GADGET_ZAMA_TRIVIUM_PARAMETERS"])
+@pytest.mark.parametrize("name", ["GADGET_ASCON_PARAMETERS_40", "GADGET_ZAMA_TRIVIUM_PARAMETERS",
+                                  "GADGET_SHA3_PARAMETERS_40"])
 def test_gadget_apply_lut_both_orders(name):
     """Big-key set (KS -> PBS) and Small-key set (PBS -> KS) end to end, GPU vs oracle engine."""
     from tfhe_mi355 import gadget
@@ -62,4 +63,9 @@ def test_gadget_apply_lut_both_orders(name):
     a = gpu.apply_lut_batch(cts, enc, f)
     b = cpu.apply_lut_batch(cts, enc, f)
     assert all(np.array_equal(x.ct, y.ct) for x, y in zip(a, b))
+    if name == "GADGET_SHA3_PARAMETERS_40":
+        # sigma_lwe = 2^-10 with a 4 x 3 keyswitch leaves keyswitch noise of std ~0.28 of the
+        # torus: the set cannot decrypt anything (the reference defines it at
+        # gadget/parameters/mod.rs:148 and never uses it) -- bit parity with the oracle only
+        return
     assert ck.decrypt_many(a) == [f(x % 3) for x in range(12)]

@@ -582,6 +582,118 @@ struct WaveFft<256> {
     }
 };
 
+// ---------------------------------------------------------------------------------------
+// M = 128 (N = 256, GADGET_SHA3_PARAMETERS_40): radices [16, 8]; 64 lanes x 2 values.
+//   natural layout = fourier layout : lane a, slot b  <->  position a + 64 b
+// Stage 1 (8 butterflies of 16 points, z[a' + 8 b]) is spread over the four 16-lane rows as in
+// WaveFft<256>, on the lanes with (lane & 15) < 8 (the other half computes a duplicate and does
+// not store); stage 2 (16 blocks of 8 points, no twiddles) runs one block per lane on lanes
+// 0-15.  Both stages exchange through the wave's LDS buffer.  N = 256 is a small niche shape:
+// this favours reusing the verified radix-16/8 kernels over lane efficiency.
+// ---------------------------------------------------------------------------------------
+struct LdsTwiddles128 {  // stage-1 twiddles W_128[a' C] (a' < 8, C = 1..15): table [C-1][a']
+    const double2 *t1, *t2;
+    __device__ __forceinline__ cx s1(int c, int a) const {
+        double2 t = t1[(c - 1) * 8 + a];
+        return {t.x, t.y};
+    }
+    static constexpr int s1_len = 15 * 8;
+    static constexpr int s2_len = 0;
+    template <int M>
+    __device__ static void fill(double2 *t1, double2 *, const double2 *__restrict__ W, int tid, int nthreads) {
+        for (int e = tid; e < s1_len; e += nthreads) t1[e] = W[(e & 7) * ((e >> 3) + 1)];
+    }
+};
+
+template <>
+struct WaveFft<128> {
+    static constexpr int M = 128;
+    static constexpr int V = 2;
+    static constexpr int XL = xbuf_len(128);
+    using Lds = LdsTwiddles128;
+
+    template <class TW, class Sync>
+    __device__ __forceinline__ static void forward(cx *v, cx *xb, const TW &tw, int lane, Sync sync) {
+        const int ap = lane & 7, row = (lane >> 4) & 3;
+        const bool st1 = (lane & 15) < 8;
+        sync();
+        lds_st(xb, lane, v[0]);
+        lds_st(xb, lane + 64, v[1]);
+        sync();
+        // stage 1: L = 128, R = 16, m = 8; column A = row holds z[a' + 8 (A + 4 j)]
+        cx u[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) u[j] = lds_ld(xb, ap + 8 * (row + 4 * j));
+        dft16_fwd_rows(u, row);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int C = row + 4 * q;
+            if (C) {
+                cx w = tw.s1(C, ap);
+                u[q] = cmulw(u[q], w.re, w.im);
+            }
+        }
+        sync();
+        if (st1) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) lds_st(xb, ap + 8 * (row + 4 * q), u[q]);
+        }
+        sync();
+        // stage 2: blocks of 8 (lane = block), R = 8, m = 1
+        if (lane < 16) {
+            cx b[8];
+#pragma unroll
+            for (int t = 0; t < 8; t++) b[t] = lds_ld(xb, 8 * lane + t);
+            dft8_fwd(b);
+#pragma unroll
+            for (int t = 0; t < 8; t++) lds_st(xb, 8 * lane + t, b[t]);
+        }
+        sync();
+        v[0] = lds_ld(xb, lane);
+        v[1] = lds_ld(xb, lane + 64);
+    }
+
+    template <class TW, class Sync>
+    __device__ __forceinline__ static void inverse(cx *v, cx *xb, const TW &tw, int lane, Sync sync) {
+        const int ap = lane & 7, row = (lane >> 4) & 3;
+        const bool st1 = (lane & 15) < 8;
+        sync();
+        lds_st(xb, lane, v[0]);
+        lds_st(xb, lane + 64, v[1]);
+        sync();
+        if (lane < 16) {
+            cx b[8];
+#pragma unroll
+            for (int t = 0; t < 8; t++) b[t] = lds_ld(xb, 8 * lane + t);
+            dft8_inv(b);
+#pragma unroll
+            for (int t = 0; t < 8; t++) lds_st(xb, 8 * lane + t, b[t]);
+        }
+        sync();
+        // stage 1: z[a' + 8C] * conj(W[a' C]), C = row + 4 q; out row A slot j -> z[a' + 8 (A + 4 j)]
+        cx u[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int C = row + 4 * q;
+            cx y = lds_ld(xb, ap + 8 * C);
+            if (C) {
+                cx w = tw.s1(C, ap);
+                y = cmulw(y, w.re, -w.im);
+            }
+            u[q] = y;
+        }
+        dft16_inv_rows(u, row);
+        sync();
+        if (st1) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) lds_st(xb, ap + 8 * (row + 4 * j), u[j]);
+        }
+        sync();
+        v[0] = lds_ld(xb, lane);
+        v[1] = lds_ld(xb, lane + 64);
+    }
+};
+
 // exact u64 (mod 2^64) of an integral double |v| <= 2^63: v = hi * 2^32 + lo with hi, lo
 // exact in f64; same value as the reference's f64 -> i64 bit twiddle (x86.rs:28-81).
 __device__ __forceinline__ uint64_t f64_int_to_u64(double v) {

@@ -339,7 +339,7 @@ static hipError_t launch_pbs_t(const ClassicPbsLaunch &a, hipStream_t s) {
 }
 
 // Instantiated shapes: the shortint sets (k = 1, N = 2048 / 1024) and the fork's gadget sets
-// (gadget/parameters/mod.rs:84-235: k = 2, 3 at N = 512 / 1024, levels 1-4).
+// (gadget/parameters/mod.rs:84-235: k = 2, 3 at N = 512 / 1024, levels 1-4; SHA3_40: k = 5, N = 256).
 #define PBS_CLASSIC_SHAPES(X) \
     X(2048, 1, 1) X(2048, 1, 2) \
     X(1024, 1, 1) X(1024, 1, 2) X(1024, 1, 3) X(1024, 1, 4) \
@@ -347,7 +347,8 @@ static hipError_t launch_pbs_t(const ClassicPbsLaunch &a, hipStream_t s) {
     X(1024, 3, 1) X(1024, 3, 2) X(1024, 3, 3) \
     X(512, 1, 1) X(512, 1, 2) X(512, 1, 3) X(512, 1, 4) \
     X(512, 2, 1) X(512, 2, 2) X(512, 2, 3) X(512, 2, 4) \
-    X(512, 3, 1) X(512, 3, 2) X(512, 3, 3) X(512, 3, 4)
+    X(512, 3, 1) X(512, 3, 2) X(512, 3, 3) X(512, 3, 4) \
+    X(256, 5, 1)
 
 bool classic_pbs_supported(int N, int k, int L) {
 #define PBS_SUPPORTED(n_, k_, l_) if (N == n_ && k == k_ && L == l_) return true;
@@ -408,6 +409,9 @@ hipError_t launch_bsk_to_fourier(int N, const uint64_t *std_polys, double2 *four
     } else if (N == 512) {
         hipLaunchKernelGGL(bsk_to_fourier_kernel<512>, dim3(npoly), dim3(64),
                            sizeof(cx) * WaveFft<256>::XL, s, std_polys, fourier, npoly, t.W, t.twist);
+    } else if (N == 256) {
+        hipLaunchKernelGGL(bsk_to_fourier_kernel<256>, dim3(npoly), dim3(64),
+                           sizeof(cx) * WaveFft<128>::XL, s, std_polys, fourier, npoly, t.W, t.twist);
     } else {
         return hipErrorInvalidValue;
     }
