@@ -42,7 +42,7 @@ PARAMS = {  # --params choice -> (parameter set name, workload text, kernel name
             "pbs_multibit_kernel<2048,1,1,3>"),
     "4_4": ("PARAM_MESSAGE_4_CARRY_4_KS_PBS",
             "BASELINE config 3: shortint apply_lookup_table (keyswitch -> PBS) at N=32768 per GPU batch",
-            "large_fwd_kernel<1,2> + large_inv_kernel<1,2> (+ keyswitch_kernel)"),
+            "large_top_fwd_kernel<1,2> + large_sub_kernel<1,2> + large_top_inv_kernel<1> (+ ks_mfma_kernel)"),
     "mul32": ("PARAM_MESSAGE_2_CARRY_2_KS_PBS",
               "BASELINE config 4: FheUint32 multiply (16-block radix DAG, radix_parallel/mul.rs), "
               "K independent pairs per GPU, every DAG layer one batched KS+PBS launch",

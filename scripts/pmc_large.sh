@@ -1,17 +1,11 @@
 #!/bin/bash
-# PMC passes of the N=32768 bench (large_fwd / large_inv kernels).
+# Kernel-trace + PMC passes of the N=32768 bench (large_top_fwd / large_sub / large_top_inv),
+# one chunk of 128; summarise with scripts/pmc_kernels.py.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out; export TMPDIR=/tmp
-i=0
-while read -r grp; do
-  [ -z "$grp" ] && continue
-  i=$((i+1))
-  timeout -k 10 400 rocprofv3 --pmc $grp -d gpurun_out/pmc_large/g$i -o run --output-format csv -- python3 bench.py --params 4_4 --batch 256 --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/pmc_large_g$i.log 2>&1
-  rc=$?; echo "group $i ($grp) rc=$rc"
-  if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc_large_g$i.log; exit $rc; fi
-done <<GROUPS
-SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_BUSY_CYCLES
-SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR SQ_WAVES
-FETCH_SIZE
-WRITE_SIZE
-GROUPS
+B="python3 bench.py --params 4_4 --batch ${BATCH:-128} --steps 1 --warmup 0 --no-cpu-baseline"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/pl_trace -o run --output-format csv -- $B > gpurun_out/pl_trace.log 2>&1 || exit $?
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pl_fetch -o run --output-format csv -- $B > gpurun_out/pl_fetch.log 2>&1 || exit $?
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pl_write -o run --output-format csv -- $B > gpurun_out/pl_write.log 2>&1 || exit $?
+timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_WAVES -d gpurun_out/pl_sq -o run --output-format csv -- $B > gpurun_out/pl_sq.log 2>&1 || exit $?
+echo done

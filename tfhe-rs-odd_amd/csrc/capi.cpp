@@ -141,6 +141,17 @@ void build_tables(TfheMi355Context *c) {
     check(hipMemcpy(c->tables.W, W.data(), bytes, hipMemcpyHostToDevice), "upload W");
     check(hipMemcpy(c->tables.twist, tw.data(), bytes, hipMemcpyHostToDevice), "upload twist");
     check(hipMemcpy(c->tables.twist_inv, twi.data(), bytes, hipMemcpyHostToDevice), "upload twist_inv");
+    if (M >= 16 * 1024) {
+        // the large-N top radix-16 stage reads W[a c] for a < M/16: laid out [c-1][a] so that a
+        // wave's 64 consecutive butterflies read 1 KiB contiguously instead of 64 scattered lines
+        const int A = M / 16;
+        std::vector<double2> top((size_t)15 * A);
+        for (int c = 1; c < 16; c++)
+            for (int a = 0; a < A; a++) top[(size_t)(c - 1) * A + a] = W[(size_t)a * c];
+        const size_t tb = sizeof(double2) * top.size();
+        check(hipMalloc(&c->tables.wtop, tb), "hipMalloc(wtop)");
+        check(hipMemcpy(c->tables.wtop, top.data(), tb, hipMemcpyHostToDevice), "upload wtop");
+    }
     c->tables.N = N;
 }
 
@@ -183,7 +194,7 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
     if (large_pbs_supported((int)c->N(), (int)c->k(), (int)c->p.pbs_level)) {
         if (glwe_out) fail("blind rotation without sample extraction is not available at N = %zu", c->N());
         // ciphertexts per pass: the chunk's accumulators + spectra (1.5 MiB per ciphertext at 4_4)
-        // should stay resident in the 256 MiB Infinity Cache across the two launches of a CMUX
+        // should stay resident in the 256 MiB Infinity Cache across the three launches of a CMUX
         static const size_t kChunk = [] {
             const char *e = std::getenv("TFHE_MI355_LARGE_CHUNK");
             const long v = e ? std::atol(e) : 0;
@@ -199,6 +210,7 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
         a.fbsk = reinterpret_cast<const double2 *>(c->fbsk.ptr);
         a.W = c->tables.W;
         a.twist = c->tables.twist;
+        a.wtop = c->tables.wtop;
         a.n = (int)c->n();
         a.base_log = (int)c->p.pbs_base_log;
         a.count = (int)count;
@@ -387,6 +399,7 @@ int tfhe_mi355_context_destroy(TfheMi355Context *ctx) {
         if (ctx->tables.W) (void)hipFree(ctx->tables.W);
         if (ctx->tables.twist) (void)hipFree(ctx->tables.twist);
         if (ctx->tables.twist_inv) (void)hipFree(ctx->tables.twist_inv);
+        if (ctx->tables.wtop) (void)hipFree(ctx->tables.wtop);
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
         delete ctx;
     });

@@ -11,6 +11,7 @@ struct FftTables {
     double2 *W = nullptr;          // exp(-2 pi i t / M)
     double2 *twist = nullptr;      // exp(i pi j / N)            (fft/mod.rs:58-69)
     double2 *twist_inv = nullptr;  // twist / M (backward, x86.rs:823-874)
+    double2 *wtop = nullptr;       // N = 32768: top-stage twiddles wtop[c-1][a] = W[a c] (a < M/16, c < 16)
     int N = 0;
 };
 
@@ -46,7 +47,7 @@ struct MultiBitPbsLaunch {
 bool multibit_pbs_supported(int N, int k, int L, int g);
 hipError_t launch_multibit_pbs(int N, int k, int L, int g, const MultiBitPbsLaunch &a, hipStream_t s);
 
-// N = 32768 classic PBS: accumulator and spectra in device scratch, two launches per CMUX
+// N = 32768 classic PBS: accumulator and spectra in device scratch, three launches per CMUX
 struct LargePbsLaunch {
     const uint64_t *lwe_in;      // [count][n+1]
     uint64_t *lwe_out;           // [count][k*N+1]
@@ -54,6 +55,7 @@ struct LargePbsLaunch {
     const uint32_t *lut_indexes; // [count] or null
     const double2 *fbsk;         // engine Fourier layout
     const double2 *W, *twist;
+    const double2 *wtop;         // FftTables::wtop
     int n;
     int base_log;
     int count;
@@ -61,6 +63,8 @@ struct LargePbsLaunch {
     size_t scratch_bytes;
     uint64_t *acc;               // set by the launcher
     double2 *spectra;            // set by the launcher
+    int levels;                  // set by the launcher (= pbs_level)
+    int chunk_count;             // set by the launcher: ciphertexts in the current chunk
 };
 bool large_pbs_supported(int N, int k, int L);
 size_t large_pbs_scratch_per_ct(int N, int k, int L);

@@ -7,16 +7,12 @@
 //
 // Why a different structure (DESIGN.md "Kernels"): at N = 32768 one ciphertext's accumulator is
 // (k+1) N u64 = 512 KiB and one spectrum M = 16384 c64 = 256 KiB -- neither fits a CU (160 KiB
-// LDS), so the accumulator lives in HBM scratch and each CMUX is two batch-wide launches:
-//   large_fwd  : one workgroup per (ciphertext, row r): ct1 = X^{a~} acc_r - acc_r, decompose,
-//                then per level: twist, FFT -> spectrum F[ct][lvl][r]   (global)
-//   large_inv  : one workgroup per (ciphertext, column c): sum_{lvl,r} F * GGSW[lvl][r][c],
-//                inverse FFT, acc_c += rounded result                  (global)
-// The M = 16384 FFT is the oracle's [16, 16, 16, 4] DAG: the top radix-16 stage runs across the
-// workgroup (512 threads x 2 butterflies, exchange through LDS in a real and an imaginary pass of
-// 128 KiB each), then each wave runs the 1024-point WaveFft on its two contiguous sub-blocks.
-// Twiddles: top stage W_M[a c] from the global table; sub-blocks W_M[16 x] through the LDS s1
-// table (the oracle's tstride-16 reads of the same table, so bit-identical).
+// LDS), so the accumulator lives in HBM scratch.  The M = 16384 FFT is the oracle's
+// [16, 16, 16, 4] DAG; after its top radix-16 stage the 16 sub-blocks of 1024 positions are
+// independent, and so are the MAC and the inverse up to its own top stage.  A CMUX is three
+// batch-wide launches (below), each streaming at full occupancy.  Twiddles: top stage W_M[a c]
+// from a [c-1][a] copy of the table (coalesced); sub-blocks W_M[16 x] through an LDS table (the
+// oracle's tstride-16 reads of the same table, so bit-identical).
 #include "engine.h"
 #include "pbs_common.h"
 
@@ -38,10 +34,11 @@ struct LargeCtx {
     cx *wxb;            // this wave's 1024-entry buffer inside it
     SubFft::Lds tw;     // sub-block twiddles (LDS)
     const double2 *W;   // W_M, global
+    const double2 *wtop;  // top-stage twiddles [c-1][a] = W[a c], global
     int t, lane, wave;
 };
 
-__device__ __forceinline__ LargeCtx large_setup(const double2 *W) {
+__device__ __forceinline__ LargeCtx large_setup(const double2 *W, const double2 *wtop) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double2 *lds = reinterpret_cast<double2 *>(smem);
     LargeCtx c;
@@ -55,6 +52,7 @@ __device__ __forceinline__ LargeCtx large_setup(const double2 *W) {
     for (int e = threadIdx.x; e < SubFft::Lds::s1_len; e += LT) s1[e] = W[16 * (e & 63) * ((e >> 6) + 1)];
     c.tw = SubFft::Lds{s1, s1};
     c.W = W;
+    c.wtop = wtop;
     __syncthreads();
     return c;
 }
@@ -81,27 +79,6 @@ __device__ __forceinline__ void large_exchange_to_blocks(const LargeCtx &c, cx (
     }
     __syncthreads();  // the region now serves as the per-wave buffers
 }
-__device__ __forceinline__ void large_exchange_to_top(const LargeCtx &c, cx (&u)[2][16]) {
-#pragma unroll
-    for (int part = 0; part < 2; part++) {
-        __syncthreads();
-#pragma unroll
-        for (int h = 0; h < 2; h++)
-#pragma unroll
-            for (int b = 0; b < 16; b++)
-                c.xch[1024 * (2 * c.wave + h) + c.lane + 64 * b] = part ? u[h][b].im : u[h][b].re;
-        __syncthreads();
-#pragma unroll
-        for (int h = 0; h < 2; h++)
-#pragma unroll
-            for (int q = 0; q < 16; q++) {
-                const double x = c.xch[c.t + 512 * h + 1024 * q];
-                if (part) u[h][q].im = x;
-                else u[h][q].re = x;
-            }
-    }
-}
-
 // forward: u[h][b] = twisted input at position (t + 512 h) + 1024 b; on exit u[h] holds
 // sub-block 2 wave + h in the WaveFft<1024> Fourier layout.
 __device__ __forceinline__ void large_forward(const LargeCtx &c, cx (&u)[2][16]) {
@@ -112,7 +89,7 @@ __device__ __forceinline__ void large_forward(const LargeCtx &c, cx (&u)[2][16])
 #pragma unroll
         for (int q = 1; q < 16; q++) {
             if (q % 4 == 1) __builtin_amdgcn_sched_barrier(0);  // bound twiddle loads in flight
-            const cx w = gld(c.W + a * q);
+            const cx w = gld(c.wtop + (q - 1) * 1024 + a);  // = W[a q]
             u[h][q] = cmulw(u[h][q], w.re, w.im);
         }
     }
@@ -120,24 +97,6 @@ __device__ __forceinline__ void large_forward(const LargeCtx &c, cx (&u)[2][16])
     WaveLocalSync wsync;
 #pragma unroll
     for (int h = 0; h < 2; h++) SubFft::forward(u[h], c.wxb, c.tw, c.lane, wsync);
-}
-
-// inverse of the above: on exit u[h][b] = position (t + 512 h) + 1024 b (unnormalised).
-__device__ __forceinline__ void large_inverse(const LargeCtx &c, cx (&u)[2][16]) {
-    WaveLocalSync wsync;
-#pragma unroll
-    for (int h = 0; h < 2; h++) SubFft::inverse(u[h], c.wxb, c.tw, c.lane, wsync);
-    large_exchange_to_top(c, u);
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-        const int a = c.t + 512 * h;
-#pragma unroll
-        for (int q = 1; q < 16; q++) {
-            const cx w = gld(c.W + a * q);
-            u[h][q] = cmulw(u[h][q], w.re, -w.im);
-        }
-        dft16_inv(u[h]);
-    }
 }
 
 // spectrum element (h, slot s) of thread (wave, lane) <-> offset in a poly's engine layout
@@ -167,17 +126,42 @@ __global__ void __launch_bounds__(256) large_init_kernel(LargePbsLaunch a, int c
     a.acc[e] = (wrap != (bool)(full & 1)) ? 0 - v : v;
 }
 
-// One workgroup per (ciphertext, row r): the rotation and the decomposition are done once for all
-// levels; level L's digits go straight into the FFT input, level L-1's (L = 2) are parked as int16
-// pairs in the not-yet-written level-(L-1) spectrum buffer (64 KiB of its 256 KiB; L2-resident)
-// and transformed second.  Halves the accumulator reads and the decomposition work of a
-// per-(row, level) split, and the workgroup count.
+// ---------------------------------------------------------------------------------------
+// CMUX: the M = 16384 FFT is [16 | 16, 16, 4], and after its top radix-16 stage
+// the 16 sub-blocks of 1024 positions are independent -- so are the MAC (per frequency) and the
+// inverse up to its own top stage.  Three launches per CMUX, each streaming at full occupancy
+// (one 512-thread workgroup per CU alternating memory and FFT phases was 16% slower):
+//   large_top_fwd : per (ct, row, butterfly a): rotate, decompose, twist, top DIF radix-16
+//                   -> T[ct][lvl][row][a + 1024 c]                        (no LDS)
+//   large_sub     : per (ct, sub-block q): (k+1) L waves run the 1024-point WaveFft of their
+//                   poly's sub-block q, publish to LDS; wave c: MAC with GGSW sub-block q of
+//                   column c, inverse sub-FFT -> T[ct][0][c][q-block]     (79 KiB LDS)
+//   large_top_inv : per (ct, column, butterfly a): top DIT radix-16, backward conversion,
+//                   acc += increments                                     (no LDS)
+// Same DAG as the oracle (dif_rec/dit_rec stage 0 = top, stages 1-3 = WaveFft<1024> with
+// tstride 16), so the outputs stay bit-exact.  Scratch per ciphertext: acc + T (1.5 MiB at 4_4).
+// ---------------------------------------------------------------------------------------
+#ifndef LARGE_TOPT
+#define LARGE_TOPT 256
+#endif
+#ifndef LARGE_MAC_SB
+#define LARGE_MAC_SB 4  // MAC slots per scheduling region of large_sub (GGSW loads in flight)
+#endif
+constexpr int TOPT = LARGE_TOPT;  // threads per top-stage workgroup
+
 template <int K, int L>
-__global__ void __launch_bounds__(LT) large_fwd_kernel(LargePbsLaunch a, int ct0, int i) {
+__global__ void __launch_bounds__(TOPT, 4) large_top_fwd_kernel(LargePbsLaunch a, int ct0, int i) {
     static_assert(L == 1 || L == 2, "levels L and L-1 only");
-    const LargeCtx c = large_setup(a.W);
-    const int r = blockIdx.x % (K + 1);
-    const int cl = blockIdx.x / (K + 1);
+    constexpr int BPP = 1024 / TOPT;  // workgroups per polynomial
+    // XCD-aware: workgroup w runs on XCD w % 8; all (K+1) BPP workgroups of a ciphertext share
+    // one XCD, so the rotated gather re-reads the accumulator rows from that XCD's L2
+    const int x = blockIdx.x & 7, m = blockIdx.x >> 3;
+    const int sub = m % ((K + 1) * BPP);
+    const int cl = x + 8 * (m / ((K + 1) * BPP));
+    if (cl >= a.chunk_count) return;  // whole workgroup
+    const int ab = sub % BPP;
+    const int r = sub / BPP;
+    const int t = ab * TOPT + threadIdx.x;  // butterfly a
     const uint64_t *in = a.lwe_in + (size_t)(ct0 + cl) * (a.n + 1);
     const uint32_t at = pbs_modulus_switch<15>(in[i]);
     const bool full_odd = (at / LN) & 1;
@@ -185,86 +169,106 @@ __global__ void __launch_bounds__(LT) large_fwd_kernel(LargePbsLaunch a, int ct0
     const uint64_t *acc = a.acc + ((size_t)cl * (K + 1) + r) * LN;
     const int beta = a.base_log;
     const uint32_t dmask = (1u << beta) - 1;
-    auto spectrum = [&](int lvl) { return a.spectra + (((size_t)cl * L + (lvl - 1)) * (K + 1) + r) * LM; };
-    uint32_t *stash = reinterpret_cast<uint32_t *>(spectrum(L - 1 > 0 ? L - 1 : 1));
-
-    cx u[2][16];
+    cx u[16];
+    uint32_t pk[L == 2 ? 16 : 1];
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
+    for (int b = 0; b < 16; b++) {
+        const int j = t + 1024 * b;
+        int32_t dg[2], dl[2];
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+            // ct1 = X^{a~} acc - acc  (polynomial_wrapping_monic_monomial_mul_and_subtract)
+            const int jj = j + half * LM - rem;
+            const bool neg = (jj < 0) != full_odd;
+            const uint64_t x = acc[(unsigned)jj & (unsigned)(LN - 1)];
+            const uint64_t d = (neg ? 0 - x : x) - acc[j + half * LM];
+            uint32_t st = decomp_state32_hi<L>((uint32_t)(d >> 32), beta);
+            dg[half] = decomp_digit32(st, beta, dmask);               // level L
+            dl[half] = L == 2 ? decomp_digit32(st, beta, dmask) : 0;  // level L-1
+        }
+        if constexpr (L == 2) pk[b] = ((uint32_t)dl[0] & 0xffffu) | ((uint32_t)dl[1] << 16);
+        const cx tw = gld(a.twist + j);
+        u[b] = cmulw(cx{(double)dg[0], (double)dg[1]}, tw.re, tw.im);
+    }
+    auto top_and_store = [&](int lvl) {
+        dft16_fwd(u);
+        double2 *T = a.spectra + (((size_t)cl * L + (lvl - 1)) * (K + 1) + r) * LM + t;
+        T[0] = make_double2(u[0].re, u[0].im);
+#pragma unroll
+        for (int c = 1; c < 16; c++) {
+            const cx w = gld(a.wtop + (c - 1) * 1024 + t);  // = W[t c]
+            const cx y = cmulw(u[c], w.re, w.im);
+            T[1024 * c] = make_double2(y.re, y.im);
+        }
+    };
+    top_and_store(L);
+    if constexpr (L == 2) {
 #pragma unroll
         for (int b = 0; b < 16; b++) {
-            const int j = c.t + 512 * h + 1024 * b;
-            int32_t dg[2], dl[2];
-#pragma unroll
-            for (int half = 0; half < 2; half++) {
-                // ct1 = X^{a~} acc - acc  (polynomial_wrapping_monic_monomial_mul_and_subtract)
-                const int jj = j + half * LM - rem;
-                const bool neg = (jj < 0) != full_odd;
-                const uint64_t x = acc[(unsigned)jj & (unsigned)(LN - 1)];
-                const uint64_t d = (neg ? 0 - x : x) - acc[j + half * LM];
-                uint32_t st = decomp_state32_hi<L>((uint32_t)(d >> 32), beta);
-                dg[half] = decomp_digit32(st, beta, dmask);                  // level L
-                dl[half] = L == 2 ? decomp_digit32(st, beta, dmask) : 0;     // level L-1
-            }
-            if constexpr (L == 2)
-                stash[(h * 16 + b) * LT + c.t] = ((uint32_t)dl[0] & 0xffffu) | ((uint32_t)dl[1] << 16);
-            const cx tw = gld(a.twist + j);
-            u[h][b] = cmulw(cx{(double)dg[0], (double)dg[1]}, tw.re, tw.im);
+            const int32_t d0 = (int32_t)(int16_t)(pk[b] & 0xffffu), d1 = (int32_t)pk[b] >> 16;
+            const cx tw = gld(a.twist + t + 1024 * b);
+            u[b] = cmulw(cx{(double)d0, (double)d1}, tw.re, tw.im);
         }
-    }
-    auto store = [&](int lvl) {
-        double2 *F = spectrum(lvl);
-#pragma unroll
-        for (int h = 0; h < 2; h++)
-#pragma unroll
-            for (int s = 0; s < 16; s++)
-                F[spec_off(c.wave, h, s, c.lane)] = make_double2(u[h][s].re, u[h][s].im);
-    };
-    large_forward(c, u);
-    store(L);
-    if constexpr (L == 2) {
-        __builtin_amdgcn_sched_barrier(0);
-        // own stash entries only (written by this thread); the spectrum writes below come after
-        // the FFT's first workgroup barrier, so every thread has read its entries by then
-#pragma unroll
-        for (int h = 0; h < 2; h++)
-#pragma unroll
-            for (int b = 0; b < 16; b++) {
-                int t = c.t;
-                asm volatile("" : "+v"(t));  // per-use address: no block of hoisted addresses
-                const int j = t + 512 * h + 1024 * b;
-                const uint32_t pk = stash[(h * 16 + b) * LT + t];
-                const int32_t d0 = (int32_t)(int16_t)(pk & 0xffffu), d1 = (int32_t)pk >> 16;
-                const cx tw = gld(a.twist + j);
-                u[h][b] = cmulw(cx{(double)d0, (double)d1}, tw.re, tw.im);
-            }
-        large_forward(c, u);
-        store(L - 1);
+        top_and_store(L - 1);
     }
 }
 
+// (k+1) L waves; LDS: sub-block twiddle table + one 1024-entry buffer per wave
 template <int K, int L>
-__global__ void __launch_bounds__(LT) large_inv_kernel(LargePbsLaunch a, int ct0, int i) {
-    const LargeCtx c = large_setup(a.W);
-    const int col = blockIdx.x % (K + 1);
-    const int cl = blockIdx.x / (K + 1);
-    const double2 *F = a.spectra + (size_t)cl * L * (K + 1) * LM;
-    const double2 *G = a.fbsk + (size_t)i * L * (K + 1) * (K + 1) * LM + (size_t)col * LM;
+struct LargeSubCfg {
+    static constexpr int WAVES = (K + 1) * L;
+    static constexpr int THREADS = 64 * WAVES;
+    static constexpr int S1 = WAVES * SubFft::XL;  // table offset (double2 units)
+    static constexpr size_t LDS = sizeof(double2) * (S1 + SubFft::Lds::s1_len);
+};
 
-    cx u[2][16];
+template <int K, int L>
+__global__ void __launch_bounds__((LargeSubCfg<K, L>::THREADS), 2) large_sub_kernel(LargePbsLaunch a, int ct0, int i) {
+    using Cfg = LargeSubCfg<K, L>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double2 *lds = reinterpret_cast<double2 *>(smem);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // XCD-aware: consecutive workgroups land on consecutive XCDs (8), so XCD x only ever sees
+    // sub-blocks q = x and x + 8 -- their GGSW slices (2 x 128 KiB at 4_4) stay in its L2
+    const int x = blockIdx.x & 7, y = blockIdx.x >> 3;
+    const int q = x + 8 * (y & 1);
+    const int cl = y >> 1;
+    double2 *s1 = lds + Cfg::S1;
+    // sub-block stage twiddles W_1024[lane c] = W_M[16 lane c]  (oracle dif_rec tstride 16)
+    for (int e = threadIdx.x; e < SubFft::Lds::s1_len; e += Cfg::THREADS) s1[e] = a.W[16 * (e & 63) * ((e >> 6) + 1)];
+    const SubFft::Lds tw{s1, s1};
+    cx *xb = reinterpret_cast<cx *>(lds) + wave * SubFft::XL;
+    WaveLocalSync wsync;
+    // this wave's poly (lvl - 1) (K+1) + r, sub-block q, natural layout
+    double2 *T = a.spectra + (size_t)cl * L * (K + 1) * LM;
+    cx v[16];
+    {
+        const double2 *src = T + (size_t)wave * LM + 1024 * q + lane;
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
+        for (int b = 0; b < 16; b++) v[b] = gld(src + 64 * b);
+    }
+    __syncthreads();  // twiddle table
+    SubFft::forward(v, xb, tw, lane, wsync);
+    wsync();
+#pragma unroll
+    for (int s = 0; s < 16; s++) reinterpret_cast<double2 *>(xb)[s * 64 + lane] = make_double2(v[s].re, v[s].im);
+    __syncthreads();
+    const bool mac = wave <= K;  // wave c computes output column c
+    if (mac) {
+        // column c: sum over levels L..1 and rows 0..k (ggsw.rs:524-567), oracle order
+        const double2 *G = a.fbsk + (size_t)i * L * (K + 1) * (K + 1) * LM + (size_t)wave * LM + 1024 * q + lane;
 #pragma unroll
         for (int s = 0; s < 16; s++) {
-            const size_t off = spec_off(c.wave, h, s, c.lane);
+            if (s % LARGE_MAC_SB == 0) __builtin_amdgcn_sched_barrier(0);  // bound loads in flight
             cx o{0.0, 0.0};
-            // column col: sum over levels L..1 and rows 0..k (ggsw.rs:524-567), oracle order
 #pragma unroll
             for (int lvl = L; lvl >= 1; lvl--) {
 #pragma unroll
                 for (int r = 0; r <= K; r++) {
-                    const double2 gg = G[((size_t)(lvl - 1) * (K + 1) + r) * (K + 1) * LM + off];
-                    const double2 ff = F[((size_t)(lvl - 1) * (K + 1) + r) * LM + off];
+                    const int p = (lvl - 1) * (K + 1) + r;
+                    const double2 gg = G[(size_t)p * (K + 1) * LM + s * 64];
+                    const double2 ff = reinterpret_cast<const double2 *>(lds)[p * SubFft::XL + s * 64 + lane];
                     if (lvl == L && r == 0) {
                         o.re = fma(gg.x, ff.x, -(gg.y * ff.y));
                         o.im = fma(gg.x, ff.y, gg.y * ff.x);
@@ -274,23 +278,44 @@ __global__ void __launch_bounds__(LT) large_inv_kernel(LargePbsLaunch a, int ct0
                     }
                 }
             }
-            u[h][s] = o;
+            v[s] = o;
         }
     }
-    large_inverse(c, u);
+    __syncthreads();  // every column's MAC has read the published spectra
+    if (!mac) return;
+    SubFft::inverse(v, xb, tw, lane, wsync);
+    double2 *dst = T + (size_t)wave * LM + 1024 * q + lane;  // (lvl 1, row c) slot: read by this WG only
+#pragma unroll
+    for (int b = 0; b < 16; b++) dst[64 * b] = make_double2(v[b].re, v[b].im);
+}
+
+template <int K>
+__global__ void __launch_bounds__(TOPT) large_top_inv_kernel(LargePbsLaunch a, int ct0, int i) {
+    constexpr int BPP = 1024 / TOPT;
+    const int ab = blockIdx.x % BPP;
+    const int col = (blockIdx.x / BPP) % (K + 1);
+    const int cl = blockIdx.x / (BPP * (K + 1));
+    const int t = ab * TOPT + threadIdx.x;
+    const double2 *U = a.spectra + ((size_t)cl * a.levels * (K + 1) + col) * LM + t;
+    cx u[16];
+    u[0] = gld(U);
+#pragma unroll
+    for (int c = 1; c < 16; c++) {
+        const cx w = gld(a.wtop + (c - 1) * 1024 + t);  // = W[t c]
+        u[c] = cmulw(gld(U + 1024 * c), w.re, -w.im);
+    }
+    dft16_inv(u);
     uint64_t *acc = a.acc + ((size_t)cl * (K + 1) + col) * LN;
     const double norm = 1.0 / (double)LM;
 #pragma unroll
-    for (int h = 0; h < 2; h++)
-#pragma unroll
-        for (int b = 0; b < 16; b++) {
-            const int j = c.t + 512 * h + 1024 * b;
-            const cx w = gld(a.twist + j);
-            uint64_t lo = acc[j], hi = acc[j + LM];
-            backward_add(u[h][b], cx{norm * w.re, norm * w.im}, lo, hi);
-            acc[j] = lo;
-            acc[j + LM] = hi;
-        }
+    for (int b = 0; b < 16; b++) {
+        const int j = t + 1024 * b;
+        const cx w = gld(a.twist + j);
+        uint64_t lo = acc[j], hi = acc[j + LM];
+        backward_add(u[b], cx{norm * w.re, norm * w.im}, lo, hi);
+        acc[j] = lo;
+        acc[j + LM] = hi;
+    }
 }
 
 // sample extract at degree 0 (glwe_sample_extraction.rs:91-147)
@@ -316,8 +341,9 @@ __global__ void __launch_bounds__(256) large_extract_kernel(LargePbsLaunch a, in
 __global__ void __launch_bounds__(LT) large_bsk_to_fourier_kernel(const uint64_t *__restrict__ polys,
                                                                   double2 *__restrict__ out,
                                                                   const double2 *__restrict__ W,
+                                                                  const double2 *__restrict__ wtop,
                                                                   const double2 *__restrict__ twist) {
-    const LargeCtx c = large_setup(W);
+    const LargeCtx c = large_setup(W, wtop);
     const uint64_t *x = polys + (size_t)blockIdx.x * LN;
     cx u[2][16];
 #pragma unroll
@@ -352,17 +378,24 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
     const int chunk = (int)std::min<size_t>((size_t)a0.count, a0.scratch_bytes / per_ct);
     if (chunk <= 0) return hipErrorInvalidValue;
     LargePbsLaunch a = a0;
+    a.levels = L;
     a.acc = reinterpret_cast<uint64_t *>(a0.scratch);
     a.spectra = reinterpret_cast<double2 *>(reinterpret_cast<char *>(a0.scratch) +
                                             (size_t)chunk * (K + 1) * LN * sizeof(uint64_t));
     for (int ct0 = 0; ct0 < a.count; ct0 += chunk) {
         const int cnt = std::min(chunk, a.count - ct0);
+        a.chunk_count = cnt;
         const size_t init_elems = (size_t)cnt * (K + 1) * LN;
         hipLaunchKernelGGL(large_init_kernel<K>, dim3((unsigned)((init_elems + 255) / 256)), dim3(256), 0, s, a,
                            ct0, cnt);
         for (int i = 0; i < a.n; i++) {
-            hipLaunchKernelGGL((large_fwd_kernel<K, L>), dim3(cnt * (K + 1)), dim3(LT), LARGE_LDS, s, a, ct0, i);
-            hipLaunchKernelGGL((large_inv_kernel<K, L>), dim3(cnt * (K + 1)), dim3(LT), LARGE_LDS, s, a, ct0, i);
+            using Sub = LargeSubCfg<K, L>;
+            const unsigned top_blocks = (unsigned)cnt * (K + 1) * (1024 / TOPT);
+            const unsigned fwd_blocks = (unsigned)((cnt + 7) / 8) * 8 * (K + 1) * (1024 / TOPT);
+            hipLaunchKernelGGL((large_top_fwd_kernel<K, L>), dim3(fwd_blocks), dim3(TOPT), 0, s, a, ct0, i);
+            hipLaunchKernelGGL((large_sub_kernel<K, L>), dim3((unsigned)cnt * 16), dim3(Sub::THREADS), Sub::LDS, s, a,
+                               ct0, i);
+            hipLaunchKernelGGL((large_top_inv_kernel<K>), dim3(top_blocks), dim3(TOPT), 0, s, a, ct0, i);
         }
         const size_t out_elems = (size_t)cnt * (K * LN + 1);
         hipLaunchKernelGGL(large_extract_kernel<K>, dim3((unsigned)((out_elems + 255) / 256)), dim3(256), 0, s, a,
@@ -381,7 +414,7 @@ hipError_t launch_large_bsk_to_fourier(const uint64_t *std_polys, double2 *fouri
                                        const FftTables &t, hipStream_t s) {
     if (npoly == 0) return hipSuccess;
     hipLaunchKernelGGL(large_bsk_to_fourier_kernel, dim3((unsigned)npoly), dim3(LT), LARGE_LDS, s, std_polys,
-                       fourier, t.W, t.twist);
+                       fourier, t.W, t.wtop, t.twist);
     return hipGetLastError();
 }
 
