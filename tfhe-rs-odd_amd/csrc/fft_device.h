@@ -694,50 +694,68 @@ struct WaveFft<128> {
     }
 };
 
-// exact u64 (mod 2^64) of an integral double |v| <= 2^63: v = hi * 2^32 + lo with hi, lo
-// exact in f64; same value as the reference's f64 -> i64 bit twiddle (x86.rs:28-81).
-__device__ __forceinline__ uint64_t f64_int_to_u64(double v) {
-    double hi = floor(v * 0x1p-32);
-    double lo = fma(hi, -0x1p32, v);
-    double hu = hi < 0.0 ? hi + 0x1p32 : hi;
-    return ((uint64_t)(uint32_t)hu << 32) | (uint64_t)(uint32_t)lo;
+// Torus increment of a fractional part (x86.rs:823-874 + 961-1044): X = rint(fr * 2^64) mod 2^64
+// for fr in [-1/2, 1/2], with four f64 ops, one integer add and no f64->int conversion.
+// For an even integer C in [2^52 + 2^31, 2^53 - 2^31], fma(t, 1, C) with |t| <= 2^31 is
+// C + rint_half_even(t) (ulp 1 there; C even keeps the tie parity) and its bit pattern is
+// bits(C) + rint(t) as a 64-bit integer.  With MB = 1.5 * 2^52 (bits 0x4338000000000000) and
+// MA = MB - 0x43380000:
+//   a = fma(fr, 2^32, MA):  h = a - MA = rint(fr 2^32) exactly, lo32(a) = h - 0x43380000
+//   f = fma(fr, 2^32, -h) = fr 2^32 - h in [-1/2, 1/2] (exact)
+//   b = fma(f, 2^32, MB):   bits(b) = 0x4338000000000000 + l, l = rint(f 2^32) in [-2^31, 2^31]
+// fr 2^64 = h 2^32 + f 2^32 with h 2^32 even, so rint(fr 2^64) = h 2^32 + l (ties included)
+// = bits(b) + (lo32(a) << 32) mod 2^64.  fr = +-1/2 gives h = +-2^31 -> X = 2^63, as the
+// reference's wrapping conversion.  Checked against a long-double rint on 2e8 inputs + edges.
+// X is never built as an integer: X = bits(b) + (lo32(a) << 32) mod 2^64.  The f64 part is one
+// asm block: 2^32 lives in a VGPR and the magics in SGPRs (one constant-bus operand per VOP3 on
+// gfx9; as plain fma() the compiler picks v_fmac with the magic copied into the destination
+// first), and the hazard recognizer, which pads every inline-asm block with an s_nop, sees one
+// block per coefficient.  (v_lshl_add_u64 shifts by at most 4: the high-word add is separate.)
+constexpr double TORUS_MB = 0x1.8p52;
+constexpr double TORUS_MA = 0x1.8p52 - 1127743488.0;  // MB - 0x43380000
+// 2^32 in a VGPR, hoisted by the caller out of its loops
+__device__ __forceinline__ double torus_k32() {
+    double k = 0x1p32;
+    asm volatile("" : "+v"(k));
+    return k;
 }
-
-// c += v (mod 2^64) for an integral double |v| <= 2^63, without building the u64:
-// hi = floor(v / 2^32) in [-2^31, 2^31] and lo = v - hi 2^32 in [0, 2^32) are exact; the
-// v_cvt_i32_f64 of hi is exact except hi = 2^31 (v = 2^63), where it clamps to 2^31 - 1 and is
-// corrected by +1 (2^31 mod 2^32 = 0x80000000).
-__device__ __forceinline__ void torus_add(uint64_t &c, double v) {
-    const double hi = floor(v * 0x1p-32);
-    const double lo = fma(hi, -0x1p32, v);
-    int32_t hi_i;
-    asm("v_cvt_i32_f64 %0, %1" : "=v"(hi_i) : "v"(hi));
-    const uint32_t hi_u = (uint32_t)hi_i + (hi >= 0x1p31 ? 1u : 0u);
-    const uint32_t lo_u = (uint32_t)lo;
-    unsigned int cy;
-    const uint32_t nlo = __builtin_addc((uint32_t)c, lo_u, 0u, &cy);
-    const uint32_t nhi = (uint32_t)(c >> 32) + hi_u + cy;
-    c = ((uint64_t)nhi << 32) | (uint64_t)nlo;
+__device__ __forceinline__ void frac_to_torus(double fr, double k32, double &a, double &b) {
+    asm("v_fma_f64 %[a], %[fr], %[k], %[ma]\n\t"
+        "v_add_f64 %[t], %[a], -%[ma]\n\t"
+        "v_fma_f64 %[t], %[fr], %[k], -%[t]\n\t"
+        "v_fma_f64 %[t], %[t], %[k], %[mb]"
+        : [a] "=&v"(a), [t] "=&v"(b)
+        : [fr] "v"(fr), [k] "v"(k32), [ma] "s"(TORUS_MA), [mb] "s"(TORUS_MB));
+}
+// c += X (mod 2^64)
+__device__ __forceinline__ void torus_add_frac(uint64_t &c, double fr, double k32) {
+    double a, b;
+    frac_to_torus(fr, k32, a, b);
+    const uint32_t hi = (uint32_t)(c >> 32) + (uint32_t)__double2loint(a);
+    c = (((uint64_t)hi << 32) | (uint32_t)c) + (uint64_t)__double_as_longlong(b);
+}
+// c = X
+__device__ __forceinline__ uint64_t torus_from_frac(double fr, double k32) {
+    double a, b;
+    frac_to_torus(fr, k32, a, b);
+    const uint32_t hi = (uint32_t)__double2hiint(b) + (uint32_t)__double2loint(a);
+    return ((uint64_t)hi << 32) | (uint32_t)__double2loint(b);
 }
 
 // backward conversion (x86.rs:823-874 + 961-1044): with ws = twist / M,
 // torus increments for coefficient j (re) and j + M (im).
-__device__ __forceinline__ void backward_convert(cx z, cx ws, uint64_t &dre, uint64_t &dim) {
+__device__ __forceinline__ void backward_convert(cx z, cx ws, uint64_t &dre, uint64_t &dim, double k32) {
     double mr = fma(z.re, ws.re, z.im * ws.im);
     double mi = fma(-z.re, ws.im, z.im * ws.re);
-    double fr = mr - rint(mr);
-    double fi = mi - rint(mi);
-    dre = f64_int_to_u64(rint(fr * 0x1p64));
-    dim = f64_int_to_u64(rint(fi * 0x1p64));
+    dre = torus_from_frac(mr - rint(mr), k32);
+    dim = torus_from_frac(mi - rint(mi), k32);
 }
 // same, added in place: c_re += increment(j), c_im += increment(j + M)
-__device__ __forceinline__ void backward_add(cx z, cx ws, uint64_t &c_re, uint64_t &c_im) {
+__device__ __forceinline__ void backward_add(cx z, cx ws, uint64_t &c_re, uint64_t &c_im, double k32) {
     double mr = fma(z.re, ws.re, z.im * ws.im);
     double mi = fma(-z.re, ws.im, z.im * ws.re);
-    double fr = mr - rint(mr);
-    double fi = mi - rint(mi);
-    torus_add(c_re, rint(fr * 0x1p64));
-    torus_add(c_im, rint(fi * 0x1p64));
+    torus_add_frac(c_re, mr - rint(mr), k32);
+    torus_add_frac(c_im, mi - rint(mi), k32);
 }
 
 }  // namespace tfhe_mi355

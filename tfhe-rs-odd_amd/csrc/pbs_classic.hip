@@ -184,6 +184,7 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
         __builtin_amdgcn_sched_barrier(0);
     }
 
+    const double k32 = torus_k32();
     for (int i = 0; i < n; i++) {
         // Every LDS/GGSW address below is a function of the lane only (loop invariant); hoisted
         // out of the CMUX loop they pin ~100 VGPRs and spill.  An opaque per-iteration copy of the
@@ -290,9 +291,10 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
                 Fft::inverse(v, xb, tw, lane, wsync);
 #pragma unroll
                 for (int b = 0; b < V; b++) {
+                    if (b % PBS_BWD_SB == 0) __builtin_amdgcn_sched_barrier(0);
                     const double2 w = Cfg::TWINV ? s_twinv[lane + 64 * b] : s_twist[lane + 64 * b];
                     const cx ws = Cfg::TWINV ? cx{w.x, w.y} : cx{norm * w.x, norm * w.y};
-                    backward_add(v[b], ws, c0[b], c0[V + b]);
+                    backward_add(v[b], ws, c0[b], c0[V + b], k32);
                 }
             }
         }
@@ -302,7 +304,7 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
             for (int b = 0; b < V; b++) {
                 const double2 w = Cfg::TWINV ? s_twinv[lane + 64 * b] : s_twist[lane + 64 * b];
                 const cx ws = Cfg::TWINV ? cx{w.x, w.y} : cx{norm * w.x, norm * w.y};
-                backward_add(acc[b], ws, c0[b], c0[V + b]);
+                backward_add(acc[b], ws, c0[b], c0[V + b], k32);
             }
         }
     }

@@ -11,6 +11,9 @@
 #ifndef PBS_MB_TWIST_INV_LDS
 #define PBS_MB_TWIST_INV_LDS 0  // multi-bit: the extra 16 KiB of LDS costs more than it saves (7% slower at g3)
 #endif
+#ifndef PBS_BWD_SB
+#define PBS_BWD_SB 2  // backward-conversion slots per scheduling region (bounds live f64 temporaries)
+#endif
 #ifndef PBS_MAC_SB
 #define PBS_MAC_SB 4  // MAC slots per scheduling region
 #endif

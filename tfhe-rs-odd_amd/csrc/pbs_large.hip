@@ -307,12 +307,13 @@ __global__ void __launch_bounds__(TOPT) large_top_inv_kernel(LargePbsLaunch a, i
     dft16_inv(u);
     uint64_t *acc = a.acc + ((size_t)cl * (K + 1) + col) * LN;
     const double norm = 1.0 / (double)LM;
+    const double k32 = torus_k32();
 #pragma unroll
     for (int b = 0; b < 16; b++) {
         const int j = t + 1024 * b;
         const cx w = gld(a.twist + j);
         uint64_t lo = acc[j], hi = acc[j + LM];
-        backward_add(u[b], cx{norm * w.re, norm * w.im}, lo, hi);
+        backward_add(u[b], cx{norm * w.re, norm * w.im}, lo, hi, k32);
         acc[j] = lo;
         acc[j + LM] = hi;
     }

@@ -109,6 +109,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
     const double2 *gcol = a.fbsk + (size_t)wave * M + lane;  // column c = wave, this lane
     const int groups = n / G;
 
+    const double k32 = torus_k32();
     for (int j = 0; j < groups; j++) {
         int lane = lane0;
         asm volatile("" : "+v"(lane));
@@ -230,7 +231,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
                 for (int b = 0; b < V; b++) {
                     const double2 w = PBS_MB_TWIST_INV_LDS ? s_twinv[lane + 64 * b] : s_twist[lane + 64 * b];
                     const cx ws = PBS_MB_TWIST_INV_LDS ? cx{w.x, w.y} : cx{norm * w.x, norm * w.y};
-                    backward_convert(v[b], ws, c0[b], c0[V + b]);
+                    backward_convert(v[b], ws, c0[b], c0[V + b], k32);
                 }
             }
         }
@@ -240,7 +241,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
             for (int b = 0; b < V; b++) {
                 const double2 w = PBS_MB_TWIST_INV_LDS ? s_twinv[lane + 64 * b] : s_twist[lane + 64 * b];
                 const cx ws = PBS_MB_TWIST_INV_LDS ? cx{w.x, w.y} : cx{norm * w.x, norm * w.y};
-                backward_convert(acc[b], ws, c0[b], c0[V + b]);
+                backward_convert(acc[b], ws, c0[b], c0[V + b], k32);
             }
         }
     }
