@@ -122,25 +122,21 @@ double (*volatile host_sin)(double) = static_cast<double (*)(double)>(std::sin);
 void build_tables(TfheMi355Context *c) {
     const int N = c->p.polynomial_size, M = N / 2;
     // W[t] = exp(-2 pi i t / M); twist w_j = exp(i pi j / N) as fft/mod.rs:58-69
-    std::vector<double2> W(M), tw(M), twi(M);
+    std::vector<double2> W(M), tw(M);
     for (int t = 0; t < M; t++) {
         double ang = 2.0 * M_PI * (double)t / (double)M;
         W[t] = make_double2(host_cos(ang), -host_sin(ang));
     }
     double unit = M_PI / (2.0 * (double)M);
-    double norm = 1.0 / (double)M;
     for (int j = 0; j < M; j++) {
         double a = (double)j * unit;
         tw[j] = make_double2(host_cos(a), host_sin(a));
-        twi[j] = make_double2(norm * tw[j].x, norm * tw[j].y);
     }
     size_t bytes = sizeof(double2) * M;
     check(hipMalloc(&c->tables.W, bytes), "hipMalloc(W)");
     check(hipMalloc(&c->tables.twist, bytes), "hipMalloc(twist)");
-    check(hipMalloc(&c->tables.twist_inv, bytes), "hipMalloc(twist_inv)");
     check(hipMemcpy(c->tables.W, W.data(), bytes, hipMemcpyHostToDevice), "upload W");
     check(hipMemcpy(c->tables.twist, tw.data(), bytes, hipMemcpyHostToDevice), "upload twist");
-    check(hipMemcpy(c->tables.twist_inv, twi.data(), bytes, hipMemcpyHostToDevice), "upload twist_inv");
     if (M >= 16 * 1024) {
         // the large-N top radix-16 stage reads W[a c] for a < M/16: laid out [c-1][a] so that a
         // wave's 64 consecutive butterflies read 1 KiB contiguously instead of 64 scattered lines
@@ -182,7 +178,6 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
         a.fbsk = reinterpret_cast<const double2 *>(c->fbsk.ptr);
         a.W = c->tables.W;
         a.twist = c->tables.twist;
-        a.twist_inv = c->tables.twist_inv;
         a.n = (int)c->n();
         a.base_log = (int)c->p.pbs_base_log;
         a.count = (int)count;
@@ -227,7 +222,6 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
     a.fbsk = reinterpret_cast<const double2 *>(c->fbsk.ptr);
     a.W = c->tables.W;
     a.twist = c->tables.twist;
-    a.twist_inv = c->tables.twist_inv;
     a.n = (int)c->n();
     a.base_log = (int)c->p.pbs_base_log;
     a.count = (int)count;
@@ -398,7 +392,6 @@ int tfhe_mi355_context_destroy(TfheMi355Context *ctx) {
             b->release();
         if (ctx->tables.W) (void)hipFree(ctx->tables.W);
         if (ctx->tables.twist) (void)hipFree(ctx->tables.twist);
-        if (ctx->tables.twist_inv) (void)hipFree(ctx->tables.twist_inv);
         if (ctx->tables.wtop) (void)hipFree(ctx->tables.wtop);
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
         delete ctx;

@@ -10,7 +10,6 @@ struct FftTables {
     // device tables, M entries each (M = N/2)
     double2 *W = nullptr;          // exp(-2 pi i t / M)
     double2 *twist = nullptr;      // exp(i pi j / N)            (fft/mod.rs:58-69)
-    double2 *twist_inv = nullptr;  // twist / M (backward, x86.rs:823-874)
     double2 *wtop = nullptr;       // N = 32768: top-stage twiddles wtop[c-1][a] = W[a c] (a < M/16, c < 16)
     int N = 0;
 };
@@ -21,7 +20,7 @@ struct ClassicPbsLaunch {
     const uint64_t *luts;        // [lut_count][(k+1)*N]
     const uint32_t *lut_indexes; // [count] or null
     const double2 *fbsk;         // engine Fourier layout
-    const double2 *W, *twist, *twist_inv;
+    const double2 *W, *twist;
     int n;
     int base_log;
     int count;
@@ -38,7 +37,7 @@ struct MultiBitPbsLaunch {
     const uint64_t *luts;        // [lut_count][(k+1)*N]
     const uint32_t *lut_indexes; // [count] or null
     const double2 *fbsk;         // [n/g][2^g][L][k+1][k+1] polys, engine Fourier layout
-    const double2 *W, *twist, *twist_inv;
+    const double2 *W, *twist;
     int n;
     int base_log;
     int count;

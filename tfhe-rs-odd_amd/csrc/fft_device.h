@@ -208,6 +208,29 @@ __device__ __forceinline__ cx lds_ldx(const cx *xb, int p) {
     double2 t = reinterpret_cast<const double2 *>(xb)[xswz(p)];
     return {t.x, t.y};
 }
+// M = 1024 XOR-swizzled exchange on byte addresses: for a buffer at a 1 KiB-aligned LDS address
+// X, 16 xswz(p) + X is
+//   p = lane + 64 c        : ((X + 16 lane) ^ 16 c) + 1024 c   (one v_xor; 1024 c is the ds offset)
+//   p = 64 cc + a1 + 4 b   : (X + 1024 cc + 16 (a1 ^ cc)) ^ 64 b (one v_xor)
+// since X has no bits in 4..9 and (a1 + 4 b) ^ cc = (a1 ^ cc) ^ 4 b (a1 < 4).
+typedef double lds_d2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) lds_d2v lds_d2;
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)p;
+}
+__device__ __forceinline__ void lds_st_at(uint32_t a, cx v) { *(lds_d2 *)(uintptr_t)a = lds_d2v{v.re, v.im}; }
+__device__ __forceinline__ cx lds_ld_at(uint32_t a) {
+    const lds_d2v t = *(const lds_d2 *)(uintptr_t)a;
+    return {t.x, t.y};
+}
+// The resident Fourier BSK is the reference's forward_as_torus transform (fft/mod.rs:197-218)
+// scaled by 1/M: the torus input is read as (i64)x * 2^-64 / M.  A power-of-two scale commutes
+// with every rounding of the FFT, the MAC and the inverse FFT (no value comes near the subnormal
+// or overflow range), so the inverse spectrum arrives already divided by M and the backward
+// conversion (x86.rs:823-874) multiplies by the plain twist, bit-identically to the reference's
+// twist / M -- without a second twist table or a per-element scale in the CMUX loop.
+__host__ __device__ constexpr double fourier_key_scale(int M) { return 0x1p-64 / (double)M; }
+
 __device__ __forceinline__ cx gld(const double2 *__restrict__ p) {
     double2 t = *p;
     return {t.x, t.y};
@@ -317,13 +340,23 @@ struct WaveFft<1024> {
             v[c] = cmulw(v[c], w.re, w.im);
         }
         sync();  // previous readers of xb done
-#pragma unroll
-        for (int c = 0; c < 16; c++) lds_stx(xb, lane + 64 * c, v[c]);
-        sync();
-        // stage 2: blocks of 64 (cc), R=16, m=4 (a1 = row)
         const int cc = lane & 15, a1 = lane >> 4;
+        if constexpr (TM_XCHG_XOR) {
+            const uint32_t xa = lds_addr(xb), la = xa + 16u * lane;
 #pragma unroll
-        for (int b = 0; b < 16; b++) v[b] = lds_ldx(xb, 64 * cc + a1 + 4 * b);
+            for (int c = 0; c < 16; c++) lds_st_at((la ^ (16u * c)) + 1024u * c, v[c]);
+            sync();
+            // stage 2: blocks of 64 (cc), R=16, m=4 (a1 = row)
+            const uint32_t qa = xa + 1024u * cc + 16u * (a1 ^ cc);
+#pragma unroll
+            for (int b = 0; b < 16; b++) v[b] = lds_ld_at(qa ^ (64u * b));
+        } else {
+#pragma unroll
+            for (int c = 0; c < 16; c++) lds_stx(xb, lane + 64 * c, v[c]);
+            sync();
+#pragma unroll
+            for (int b = 0; b < 16; b++) v[b] = lds_ldx(xb, 64 * cc + a1 + 4 * b);
+        }
         dft16_fwd(v);
 #pragma unroll
         for (int c2 = 1; c2 < 16; c2++) {
@@ -370,15 +403,31 @@ struct WaveFft<1024> {
         }
         dft16_inv(v);
         sync();  // previous readers of xb done
+        if constexpr (TM_XCHG_XOR) {
+            const uint32_t xa = lds_addr(xb);
+            const uint32_t qa = xa + 1024u * cc + 16u * (a1 ^ cc);
 #pragma unroll
-        for (int b = 0; b < 16; b++) lds_stx(xb, 64 * cc + a1 + 4 * b, v[b]);
-        sync();
-        v[0] = lds_ldx(xb, lane);
+            for (int b = 0; b < 16; b++) lds_st_at(qa ^ (64u * b), v[b]);
+            sync();
+            const uint32_t la = xa + 16u * lane;
+            v[0] = lds_ld_at(la);
 #pragma unroll
-        for (int c = 1; c < 16; c++) {
-            cx y = lds_ldx(xb, lane + 64 * c);
-            cx w = tw.s1(c, lane);
-            v[c] = cmulw(y, w.re, -w.im);
+            for (int c = 1; c < 16; c++) {
+                cx y = lds_ld_at((la ^ (16u * c)) + 1024u * c);
+                cx w = tw.s1(c, lane);
+                v[c] = cmulw(y, w.re, -w.im);
+            }
+        } else {
+#pragma unroll
+            for (int b = 0; b < 16; b++) lds_stx(xb, 64 * cc + a1 + 4 * b, v[b]);
+            sync();
+            v[0] = lds_ldx(xb, lane);
+#pragma unroll
+            for (int c = 1; c < 16; c++) {
+                cx y = lds_ldx(xb, lane + 64 * c);
+                cx w = tw.s1(c, lane);
+                v[c] = cmulw(y, w.re, -w.im);
+            }
         }
         dft16_inv(v);
     }

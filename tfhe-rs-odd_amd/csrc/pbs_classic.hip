@@ -45,15 +45,14 @@ struct PbsConfig {
     // VGPRs, no spills) and the twist/M table is dropped, so 31 KiB of tables + 8 x 16 KiB
     // exchange buffers fill the CU's LDS (159 KiB): 8 waves per CU instead of 4, 77.5k -> 96.9k PBS/s.
     static constexpr bool PACK4 = N == 2048 && K == 1 && L == 1;
-    static constexpr bool TWINV = PACK4 ? false : (bool)PBS_TWIST_INV_LDS;
     static constexpr bool MAC_LDS = PACK4 ? true : (bool)PBS_MAC_FROM_LDS;
     // GGSW_i staged in LDS by async global->LDS loads and shared by the workgroup's ciphertexts;
     // fits next to the tables and 2 x (k+1) exchange buffers when it is <= 64 KiB
     // (only without the twist/M table: both do not fit next to four exchange buffers)
-    static constexpr bool STAGE = PBS_GGSW_LDS && !TWINV && !PACK4 && GGSW_ELEMS * 16 <= 65536;
+    static constexpr bool STAGE = PBS_GGSW_LDS && !PACK4 && GGSW_ELEMS * 16 <= 65536;
     static constexpr int CPW = PBS_CPW > 0 ? PBS_CPW : STAGE ? 2 : PACK4 ? 4 : 1;
     static constexpr size_t lds_bytes() {
-        return PbsLds<M, TWINV>::bytes((K + 1) * CPW) + (STAGE ? GGSW_ELEMS * 16 : 0);
+        return PbsLds<M>::bytes((K + 1) * CPW) + (STAGE ? GGSW_ELEMS * 16 : 0);
     }
     static_assert(lds_bytes() <= 160 * 1024, "LDS per workgroup exceeds a CU");
     // register budget per wave: 2 waves/SIMD for the packed 2_2 shape and N = 1024 (<= 256),
@@ -72,7 +71,7 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
     constexpr int CPW = Cfg::CPW;
     constexpr bool STAGE = Cfg::STAGE;
     using Fft = WaveFft<M>;
-    using Lay = PbsLds<M, Cfg::TWINV>;
+    using Lay = PbsLds<M>;
     constexpr int XL = Lay::XL;
     static_assert(sizeof(cx) * XL >= sizeof(uint64_t) * N, "exchange buffer holds one polynomial");
 
@@ -95,7 +94,6 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
     const int dk1 = 31 - beta;                        // L = 1 digit constants (digit_l1)
     const uint32_t dc1 = dmask;
     const int32_t dh1 = (int32_t)(1u << (beta - 1)) - 1;
-    const double norm = 1.0 / (double)M;
     BlockSync sync;       // cross-wave: spectrum exchange
 #if PBS_WAVE_LOCAL
     WaveLocalSync wsync;  // wave-private buffer reuse
@@ -104,11 +102,7 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
 #endif
 
     // twiddles and twist -> LDS (once per workgroup)
-    for (int e = threadIdx.x; e < M; e += blockDim.x) {
-        lds[Lay::twist_off + e] = a.twist[e];
-        if (Cfg::TWINV) lds[Lay::twinv_off + e] = a.twist_inv[e];
-    }
-    const double2 *s_twinv = lds + Lay::twinv_off;
+    for (int e = threadIdx.x; e < M; e += blockDim.x) lds[Lay::twist_off + e] = a.twist[e];
     Fft::Lds::template fill<M>(lds + Lay::s1_off, lds + Lay::s2_off, a.W, threadIdx.x, blockDim.x);
     const typename Fft::Lds tw{lds + Lay::s1_off, lds + Lay::s2_off};
     sync();  // tables visible to every wave (the CMUX loop itself only syncs wave-locally)
@@ -292,9 +286,8 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
 #pragma unroll
                 for (int b = 0; b < V; b++) {
                     if (b % PBS_BWD_SB == 0) __builtin_amdgcn_sched_barrier(0);
-                    const double2 w = Cfg::TWINV ? s_twinv[lane + 64 * b] : s_twist[lane + 64 * b];
-                    const cx ws = Cfg::TWINV ? cx{w.x, w.y} : cx{norm * w.x, norm * w.y};
-                    backward_add(v[b], ws, c0[b], c0[V + b], k32);
+                    const double2 w = s_twist[lane + 64 * b];  // the resident key carries the 1/M
+                    backward_add(v[b], cx{w.x, w.y}, c0[b], c0[V + b], k32);
                 }
             }
         }
@@ -302,9 +295,8 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
             Fft::inverse(acc, xb, tw, lane, wsync);
 #pragma unroll
             for (int b = 0; b < V; b++) {
-                const double2 w = Cfg::TWINV ? s_twinv[lane + 64 * b] : s_twist[lane + 64 * b];
-                const cx ws = Cfg::TWINV ? cx{w.x, w.y} : cx{norm * w.x, norm * w.y};
-                backward_add(acc[b], ws, c0[b], c0[V + b], k32);
+                const double2 w = s_twist[lane + 64 * b];
+                backward_add(acc[b], cx{w.x, w.y}, c0[b], c0[V + b], k32);
             }
         }
     }
@@ -387,8 +379,8 @@ __global__ void __launch_bounds__(64) bsk_to_fourier_kernel(const uint64_t *__re
 #pragma unroll
     for (int b = 0; b < V; b++) {
         const int j = lane + 64 * b;
-        double xr = (double)(int64_t)x[j] * 0x1p-64;
-        double xi = (double)(int64_t)x[j + M] * 0x1p-64;
+        double xr = (double)(int64_t)x[j] * fourier_key_scale(M);
+        double xi = (double)(int64_t)x[j + M] * fourier_key_scale(M);
         cx w = gld(twist + j);
         v[b].re = xr * w.re - xi * w.im;
         v[b].im = xr * w.im + xi * w.re;

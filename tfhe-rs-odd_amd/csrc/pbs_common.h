@@ -5,12 +5,6 @@
 #ifndef PBS_WAVE_LOCAL
 #define PBS_WAVE_LOCAL 1
 #endif
-#ifndef PBS_TWIST_INV_LDS
-#define PBS_TWIST_INV_LDS 1  // LDS table of twist/M for the backward conversion (saves 2 mul/element)
-#endif
-#ifndef PBS_MB_TWIST_INV_LDS
-#define PBS_MB_TWIST_INV_LDS 0  // multi-bit: the extra 16 KiB of LDS costs more than it saves (7% slower at g3)
-#endif
 #ifndef PBS_BWD_SB
 #define PBS_BWD_SB 2  // backward-conversion slots per scheduling region (bounds live f64 temporaries)
 #endif
@@ -84,7 +78,7 @@ __device__ __forceinline__ int32_t decomp_digit32(uint32_t &state, int beta, uin
     return (int32_t)(res - (carry << beta));
 }
 
-template <int M, bool TWINV = PBS_TWIST_INV_LDS>
+template <int M>
 struct PbsLds {
     using Fft = WaveFft<M>;
     using Tw = typename Fft::Lds;
@@ -93,8 +87,9 @@ struct PbsLds {
     static constexpr int twist_off = 0;
     static constexpr int s1_off = M;
     static constexpr int s2_off = s1_off + Tw::s1_len;
-    static constexpr int twinv_off = s2_off + Tw::s2_len;  // twist / M (backward), when TWINV
-    static constexpr int xbuf_off = ((twinv_off + (TWINV ? M : 0) + 3) / 4) * 4;
+    // M = 1024 exchange buffers start on 1 KiB boundaries (WaveFft<1024> XORs into the address)
+    static constexpr int XALIGN = M == 1024 ? 64 : 4;
+    static constexpr int xbuf_off = ((s2_off + Tw::s2_len + XALIGN - 1) / XALIGN) * XALIGN;
     static constexpr size_t bytes(int waves) { return sizeof(double2) * (size_t)(xbuf_off + waves * XL); }
 };
 

@@ -306,14 +306,13 @@ __global__ void __launch_bounds__(TOPT) large_top_inv_kernel(LargePbsLaunch a, i
     }
     dft16_inv(u);
     uint64_t *acc = a.acc + ((size_t)cl * (K + 1) + col) * LN;
-    const double norm = 1.0 / (double)LM;
     const double k32 = torus_k32();
 #pragma unroll
     for (int b = 0; b < 16; b++) {
         const int j = t + 1024 * b;
         const cx w = gld(a.twist + j);
         uint64_t lo = acc[j], hi = acc[j + LM];
-        backward_add(u[b], cx{norm * w.re, norm * w.im}, lo, hi, k32);
+        backward_add(u[b], w, lo, hi, k32);  // the resident key carries the 1/M
         acc[j] = lo;
         acc[j + LM] = hi;
     }
@@ -352,8 +351,8 @@ __global__ void __launch_bounds__(LT) large_bsk_to_fourier_kernel(const uint64_t
 #pragma unroll
         for (int b = 0; b < 16; b++) {
             const int j = c.t + 512 * h + 1024 * b;
-            const double xr = (double)(int64_t)x[j] * 0x1p-64;
-            const double xi = (double)(int64_t)x[j + LM] * 0x1p-64;
+            const double xr = (double)(int64_t)x[j] * fourier_key_scale(LM);
+            const double xi = (double)(int64_t)x[j + LM] * fourier_key_scale(LM);
             const cx w = gld(twist + j);
             u[h][b].re = xr * w.re - xi * w.im;
             u[h][b].im = xr * w.im + xi * w.re;

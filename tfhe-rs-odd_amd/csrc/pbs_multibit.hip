@@ -48,7 +48,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
     constexpr int LOG2M = LOG2N - 1;
     constexpr int NSEL = 1 << G;
     using Fft = WaveFft<M>;
-    using Lay = PbsLds<M, PBS_MB_TWIST_INV_LDS>;
+    using Lay = PbsLds<M>;
     constexpr int XL = Lay::XL;
     static_assert(sizeof(cx) * XL >= sizeof(uint64_t) * N, "exchange buffer holds one polynomial");
 
@@ -70,15 +70,10 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
     const int dk1 = 31 - beta;
     const uint32_t dc1 = dmask;
     const int32_t dh1 = (int32_t)(1u << (beta - 1)) - 1;
-    const double norm = 1.0 / (double)M;
     BlockSync sync;
     WaveLocalSync wsync;
 
-    for (int e = threadIdx.x; e < M; e += blockDim.x) {
-        lds[Lay::twist_off + e] = a.twist[e];
-        if (PBS_MB_TWIST_INV_LDS) lds[Lay::twinv_off + e] = a.twist_inv[e];
-    }
-    const double2 *s_twinv = lds + Lay::twinv_off;
+    for (int e = threadIdx.x; e < M; e += blockDim.x) lds[Lay::twist_off + e] = a.twist[e];
     Fft::Lds::template fill<M>(lds + Lay::s1_off, lds + Lay::s2_off, a.W, threadIdx.x, blockDim.x);
     const typename Fft::Lds tw{lds + Lay::s1_off, lds + Lay::s2_off};
     sync();
@@ -229,9 +224,8 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
                 Fft::inverse(v, xb, tw, lane, wsync);
 #pragma unroll
                 for (int b = 0; b < V; b++) {
-                    const double2 w = PBS_MB_TWIST_INV_LDS ? s_twinv[lane + 64 * b] : s_twist[lane + 64 * b];
-                    const cx ws = PBS_MB_TWIST_INV_LDS ? cx{w.x, w.y} : cx{norm * w.x, norm * w.y};
-                    backward_convert(v[b], ws, c0[b], c0[V + b], k32);
+                    const double2 w = s_twist[lane + 64 * b];  // the resident key carries the 1/M
+                    backward_convert(v[b], cx{w.x, w.y}, c0[b], c0[V + b], k32);
                 }
             }
         }
@@ -239,9 +233,8 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
             Fft::inverse(acc, xb, tw, lane, wsync);
 #pragma unroll
             for (int b = 0; b < V; b++) {
-                const double2 w = PBS_MB_TWIST_INV_LDS ? s_twinv[lane + 64 * b] : s_twist[lane + 64 * b];
-                const cx ws = PBS_MB_TWIST_INV_LDS ? cx{w.x, w.y} : cx{norm * w.x, norm * w.y};
-                backward_convert(acc[b], ws, c0[b], c0[V + b], k32);
+                const double2 w = s_twist[lane + 64 * b];
+                backward_convert(acc[b], cx{w.x, w.y}, c0[b], c0[V + b], k32);
             }
         }
     }
@@ -270,7 +263,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
 template <int N, int K, int L, int G>
 static hipError_t launch_mb_t(const MultiBitPbsLaunch &a, hipStream_t s) {
     constexpr int M = N / 2;
-    constexpr size_t lds = PbsLds<M, PBS_MB_TWIST_INV_LDS>::bytes((K + 1) * PBS_MB_CPW);
+    constexpr size_t lds = PbsLds<M>::bytes((K + 1) * PBS_MB_CPW);
     static_assert(lds <= 160 * 1024, "LDS per workgroup exceeds a CU");
     if (a.count == 0) return hipSuccess;
     if (a.n % G) return hipErrorInvalidValue;
