@@ -51,9 +51,9 @@ struct PbsConfig {
     // (only without the twist/M table: both do not fit next to four exchange buffers)
     static constexpr bool STAGE = PBS_GGSW_LDS && !PACK4 && GGSW_ELEMS * 16 <= 65536;
     static constexpr int CPW = PBS_CPW > 0 ? PBS_CPW : STAGE ? 2 : PACK4 ? 4 : 1;
-    static constexpr size_t lds_bytes() {
-        return PbsLds<M>::bytes((K + 1) * CPW) + (STAGE ? GGSW_ELEMS * 16 : 0);
-    }
+    static constexpr bool GSYNC = PBS_GROUP_SYNC && !STAGE;  // the staged GGSW is shared by the workgroup
+    static constexpr size_t flags_off() { return PbsLds<M>::bytes((K + 1) * CPW) + (STAGE ? GGSW_ELEMS * 16 : 0); }
+    static constexpr size_t lds_bytes() { return flags_off() + (GSYNC ? 4 * (K + 1) * CPW : 0); }
     static_assert(lds_bytes() <= 160 * 1024, "LDS per workgroup exceeds a CU");
     // register budget per wave: 2 waves/SIMD for the packed 2_2 shape and N = 1024 (<= 256),
     // 3 at N = 512 (<= 168), 1 for the other N = 2048 shapes (~430 VGPR+AGPR at L = 2)
@@ -103,11 +103,17 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
 
     // twiddles and twist -> LDS (once per workgroup)
     for (int e = threadIdx.x; e < M; e += blockDim.x) lds[Lay::twist_off + e] = a.twist[e];
+    uint32_t *gflags = reinterpret_cast<uint32_t *>(smem + Cfg::flags_off());
+    if (Cfg::GSYNC && threadIdx.x < (K + 1) * CPW) gflags[threadIdx.x] = 0;
     Fft::Lds::template fill<M>(lds + Lay::s1_off, lds + Lay::s2_off, a.W, threadIdx.x, blockDim.x);
     const typename Fft::Lds tw{lds + Lay::s1_off, lds + Lay::s2_off};
     sync();  // tables visible to every wave (the CMUX loop itself only syncs wave-locally)
 
     cx *xct = reinterpret_cast<cx *>(lds + Lay::xbuf_off) + (size_t)slot * (K + 1) * XL;  // this ct's buffers
+    // spectrum exchange among this ciphertext's waves
+    std::conditional_t<Cfg::GSYNC, GroupSync<K + 1>, BlockSync> xsync;
+    if constexpr (Cfg::GSYNC)
+        xsync = {lds_addr(gflags + slot * (K + 1)), lds_addr(gflags + wid)};
     cx *xb = xct + wave * XL;
     uint64_t *xb64 = reinterpret_cast<uint64_t *>(xb);
     const uint64_t *in = a.lwe_in + (size_t)ct * (n + 1);
@@ -241,7 +247,7 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
             for (int s = 0; s < V; s++)
                 reinterpret_cast<double2 *>(xb)[s * 64 + lane] = make_double2(v[s].re, v[s].im);
             if constexpr (STAGE) stage_ggsw_wait();  // this wave's part of GGSW_i has landed
-            sync();
+            xsync();
             // output column c = wave: sum_r F_r * G[lvl][r][c]   (ggsw.rs:524-567, update_with_fmadd)
             const double2 *lm = ggsw + (size_t)(lvl - 1) * (K + 1) * (K + 1) * M;
 #pragma unroll
@@ -270,7 +276,7 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
                 if constexpr (L > 1) acc[s] = o;
                 else v[s] = o;
             }
-            sync();  // every wave is done reading the published spectra (and the staged GGSW)
+            xsync();  // every wave is done reading the published spectra (and the staged GGSW)
             if constexpr (PREF) {
                 __builtin_amdgcn_sched_barrier(0);
                 if (i + 1 < n) prefetch(i + 1);

@@ -21,6 +21,10 @@
 #define PBS_WAVES_PER_EU 0  // 0: per-shape default (PbsConfig::WPE); the multi-bit kernel uses 1
 #endif
 
+#ifndef PBS_GROUP_SYNC
+#define PBS_GROUP_SYNC 1  // CMUX-loop syncs between the (k+1) waves of ONE ciphertext (LDS flags), not s_barrier
+#endif
+
 namespace tfhe_mi355 {
 
 template <int LOG2N>
@@ -44,6 +48,44 @@ struct WaveLocalSync {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+};
+
+// Sync among the (k+1) waves of one ciphertext through LDS flags instead of s_barrier, so the
+// ciphertexts sharing a workgroup (and a CU) are not forced into lockstep: their LDS bursts and
+// VALU phases drift apart and overlap.  Each wave publishes a per-wave counter after its LDS
+// writes (a wave's LDS operations execute in issue order, so a partner that reads the new
+// count also sees the data) and polls its partners' counters.  Every wave of a group executes
+// the same number of syncs, so every wait ends.
+// The store and the poll are asm blocks (memory clobbers keep the compiler from moving LDS
+// accesses across them); as C++ atomics in a loop the CMUX loop's register allocation spilled.
+template <int W>  // waves in the group
+struct GroupSync {
+    uint32_t base;      // LDS byte address of the group's first flag word
+    uint32_t mine;      // LDS byte address of this wave's flag word
+    uint32_t seq = 0;
+    __device__ __forceinline__ void operator()() {
+        seq++;
+        asm volatile("ds_write_b32 %0, %1" ::"v"(mine), "v"(seq) : "memory");
+#pragma unroll
+        for (int r = 0; r < W; r++) {  // polling its own (already published) flag passes at once
+            const uint32_t addr = base + 4u * r;
+            uint32_t tmp, stmp;
+            asm volatile(
+                "1:\n\t"
+                "ds_read_b32 %[v], %[a]\n\t"
+                "s_waitcnt lgkmcnt(0)\n\t"
+                "v_readfirstlane_b32 %[s], %[v]\n\t"
+                "s_nop 1\n\t"
+                "s_cmp_lt_u32 %[s], %[q]\n\t"
+                "s_cbranch_scc0 2f\n\t"
+                "s_sleep 1\n\t"
+                "s_branch 1b\n\t"
+                "2:"
+                : [v] "=&v"(tmp), [s] "=&s"(stmp)
+                : [a] "v"(addr), [q] "s"(seq)
+                : "scc", "memory");
+        }
     }
 };
 
