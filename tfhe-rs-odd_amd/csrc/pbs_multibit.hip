@@ -74,6 +74,11 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
     WaveLocalSync wsync;
 
     for (int e = threadIdx.x; e < M; e += blockDim.x) lds[Lay::twist_off + e] = a.twist[e];
+    // spectrum exchange among this ciphertext's waves (GroupSync, pbs_common.h): flags after the buffers
+    uint32_t *gflags = reinterpret_cast<uint32_t *>(smem + Lay::bytes((K + 1) * CPW));
+    if (PBS_GROUP_SYNC && threadIdx.x < (K + 1) * CPW) gflags[threadIdx.x] = 0;
+    std::conditional_t<(bool)PBS_GROUP_SYNC, GroupSync<K + 1>, BlockSync> xsync;
+    if constexpr ((bool)PBS_GROUP_SYNC) xsync = {lds_addr(gflags + slot * (K + 1)), lds_addr(gflags + wid)};
     Fft::Lds::template fill<M>(lds + Lay::s1_off, lds + Lay::s2_off, a.W, threadIdx.x, blockDim.x);
     const typename Fft::Lds tw{lds + Lay::s1_off, lds + Lay::s2_off};
     sync();
@@ -162,7 +167,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
 #pragma unroll
             for (int s = 0; s < V; s++)
                 reinterpret_cast<double2 *>(xb)[s * 64 + lane] = make_double2(v[s].re, v[s].im);
-            sync();
+            xsync();
             const double2 *lm = grp + (size_t)(lvl - 1) * lvl_len;
 #pragma unroll
             for (int s = 0; s < V; s++) {
@@ -219,7 +224,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
                 if constexpr (L > 1) acc[s] = o;
                 else v[s] = o;
             }
-            sync();  // every wave is done reading the published spectra before xb is reused
+            xsync();  // every wave is done reading the published spectra before xb is reused
             if constexpr (L == 1) {
                 Fft::inverse(v, xb, tw, lane, wsync);
 #pragma unroll
@@ -263,7 +268,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
 template <int N, int K, int L, int G>
 static hipError_t launch_mb_t(const MultiBitPbsLaunch &a, hipStream_t s) {
     constexpr int M = N / 2;
-    constexpr size_t lds = PbsLds<M>::bytes((K + 1) * PBS_MB_CPW);
+    constexpr size_t lds = PbsLds<M>::bytes((K + 1) * PBS_MB_CPW) + (PBS_GROUP_SYNC ? 4 * (K + 1) * PBS_MB_CPW : 0);
     static_assert(lds <= 160 * 1024, "LDS per workgroup exceeds a CU");
     if (a.count == 0) return hipSuccess;
     if (a.n % G) return hipErrorInvalidValue;
