@@ -202,6 +202,12 @@ int tfhe_mi355_trivial_pbs_async(TfheMi355Context *ctx, uint64_t *d_body, size_t
 int tfhe_mi355_fill_accumulator(const TfheMi355Parameters *params, const uint64_t *f_values,
                                 uint64_t *accumulator);
 
+/* Diagnostic (test hook, host buffers, synchronous): the PBS kernels' backward torus conversion
+ * (x86.rs:823-874 + 961-1044 after the fract) applied to n given fractions fr in [-1/2, 1/2]:
+ * acc_inout[i] += X_i and set_out[i] = X_i, X_i = rint_half_even(fr[i] * 2^64) mod 2^64. */
+int tfhe_mi355_debug_torus_from_fraction(int device, const double *fr, uint64_t *acc_inout, uint64_t *set_out,
+                                         size_t n);
+
 /* ---- client-side helpers (not on the PBS path; seeded, deterministic per (seed, index)) ----
  * Binary secret keys, Gaussian noise (commons/math/random/gaussian.rs:15-52), GGSW/BSK
  * (ggsw_encryption.rs:116-150,300-331), KSK (lwe_keyswitch_key_generation.rs:60-135),

@@ -894,6 +894,32 @@ int tfhe_mi355_trivial_pbs_async(TfheMi355Context *ctx, uint64_t *d_body, size_t
     });
 }
 
+int tfhe_mi355_debug_torus_from_fraction(int device, const double *fr, uint64_t *acc_inout, uint64_t *set_out,
+                                         size_t n) {
+    return guarded([&] {
+        if ((!fr || !acc_inout || !set_out) && n) fail("null argument");
+        if (n == 0) return;
+        check(hipSetDevice(device), "hipSetDevice");
+        DeviceBuffer d_fr, d_acc, d_set;
+        struct Release {
+            DeviceBuffer *b[3];
+            ~Release() {
+                for (DeviceBuffer *x : b) x->release();
+            }
+        } release{{&d_fr, &d_acc, &d_set}};
+        d_fr.reserve(n * sizeof(double));
+        d_acc.reserve(n * sizeof(uint64_t));
+        d_set.reserve(n * sizeof(uint64_t));
+        check(hipMemcpy(d_fr.ptr, fr, n * sizeof(double), hipMemcpyHostToDevice), "H2D fr");
+        check(hipMemcpy(d_acc.ptr, acc_inout, n * sizeof(uint64_t), hipMemcpyHostToDevice), "H2D acc");
+        check(launch_torus_from_fraction((const double *)d_fr.ptr, (uint64_t *)d_acc.ptr, (uint64_t *)d_set.ptr, n,
+                                         nullptr),
+              "torus conversion");
+        check(hipMemcpy(acc_inout, d_acc.ptr, n * sizeof(uint64_t), hipMemcpyDeviceToHost), "D2H acc");
+        check(hipMemcpy(set_out, d_set.ptr, n * sizeof(uint64_t), hipMemcpyDeviceToHost), "D2H set");
+    });
+}
+
 int tfhe_mi355_fill_accumulator(const TfheMi355Parameters *params, const uint64_t *f_values, uint64_t *acc) {
     return guarded([&] {
         if (!params || !f_values || !acc) fail("null argument");

@@ -96,6 +96,7 @@ hipError_t launch_ksk_repack(const uint64_t *ksk, int8_t *kt, int in_dim, int le
 hipError_t launch_keyswitch_mfma(const KeyswitchLaunch &a, const int8_t *kt, void *scratch, hipStream_t s);
 
 // batched LWE linear algebra / trivial PBS (lwe_ops.hip)
+hipError_t launch_torus_from_fraction(const double *fr, uint64_t *acc, uint64_t *set, size_t n, hipStream_t s);
 hipError_t launch_lwe_scalar_mul_add(uint64_t *y, const uint64_t *x, uint64_t scalar, size_t rows, size_t words,
                                      size_t y_stride, size_t x_stride, hipStream_t s);
 hipError_t launch_trivial_pbs(uint64_t *body, size_t rows, size_t stride, const uint64_t *lut_body, uint64_t delta,

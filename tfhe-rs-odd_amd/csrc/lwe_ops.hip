@@ -9,6 +9,7 @@
 //   trivial_pbs_assign     (shortint/server_key/mod.rs:763-781)
 // All arithmetic is wrapping mod 2^64, as the reference's.
 #include "engine.h"
+#include "fft_device.h"
 
 namespace tfhe_mi355 {
 
@@ -34,6 +35,26 @@ __global__ void __launch_bounds__(256) trivial_pbs_kernel(uint64_t *__restrict__
     const uint64_t value = body[r * stride] / delta;
     const uint64_t entry = lut_body[(value % modulus_sup) * box];
     body[r * stride] = value >= modulus_sup ? 0 - entry : entry;
+}
+
+// Diagnostic: the PBS kernels' backward torus conversion (fft_device.h frac_to_torus) applied to
+// given fractions: acc[i] += X(fr[i]) and set[i] = X(fr[i]), X = rint(fr * 2^64) mod 2^64.
+__global__ void __launch_bounds__(256) torus_from_fraction_kernel(const double *__restrict__ fr,
+                                                                  uint64_t *__restrict__ acc,
+                                                                  uint64_t *__restrict__ set, size_t n) {
+    const size_t e = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const double k32 = torus_k32();
+    if (e >= n) return;
+    uint64_t c = acc[e];
+    torus_add_frac(c, fr[e], k32);
+    acc[e] = c;
+    set[e] = torus_from_frac(fr[e], k32);
+}
+
+hipError_t launch_torus_from_fraction(const double *fr, uint64_t *acc, uint64_t *set, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(torus_from_fraction_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, fr, acc, set, n);
+    return hipGetLastError();
 }
 
 hipError_t launch_lwe_scalar_mul_add(uint64_t *y, const uint64_t *x, uint64_t scalar, size_t rows, size_t words,

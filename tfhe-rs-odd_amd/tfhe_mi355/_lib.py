@@ -85,6 +85,8 @@ SIGNATURES = [
     ("tfhe_mi355_bootstrap_key_upload_seeded", ctypes.c_int, [vp, u64p, sz, ctypes.c_uint64, ctypes.c_uint64]),
     ("tfhe_mi355_keyswitch_key_upload_seeded", ctypes.c_int, [vp, u64p, sz, ctypes.c_uint64, ctypes.c_uint64]),
     ("tfhe_mi355_csprng_mask_words", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64, u64p, sz]),
+    ("tfhe_mi355_debug_torus_from_fraction", ctypes.c_int,
+     [ctypes.c_int, ctypes.POINTER(ctypes.c_double), u64p, u64p, sz]),
     ("tfhe_mi355_client_gen_seeded_bootstrap_key", ctypes.c_int,
      [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u64p, ctypes.c_uint32, u64p, ctypes.c_uint32,
       ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double, u64p, ctypes.c_uint32]),
