@@ -21,6 +21,12 @@
 #define PBS_WAVES_PER_EU 0  // 0: per-shape default (PbsConfig::WPE); the multi-bit kernel uses 1
 #endif
 
+#ifndef PBS_SYNC_SLEEP
+#define PBS_SYNC_SLEEP 1  // s_sleep argument between polls of a partner's flag (64 clocks per unit)
+#endif
+#define PBS_STR2(x) #x
+#define PBS_STR(x) PBS_STR2(x)
+#define PBS_SYNC_SLEEP_STR PBS_STR(PBS_SYNC_SLEEP)
 #ifndef PBS_GROUP_SYNC
 #define PBS_GROUP_SYNC 1  // CMUX-loop syncs between the (k+1) waves of ONE ciphertext (LDS flags), not s_barrier
 #endif
@@ -79,7 +85,7 @@ struct GroupSync {
                 "s_nop 1\n\t"
                 "s_cmp_lt_u32 %[s], %[q]\n\t"
                 "s_cbranch_scc0 2f\n\t"
-                "s_sleep 1\n\t"
+                "s_sleep " PBS_SYNC_SLEEP_STR "\n\t"
                 "s_branch 1b\n\t"
                 "2:"
                 : [v] "=&v"(tmp), [s] "=&s"(stmp)
