@@ -74,8 +74,10 @@ struct GroupSync {
         seq++;
         asm volatile("ds_write_b32 %0, %1" ::"v"(mine), "v"(seq) : "memory");
 #pragma unroll
-        for (int r = 0; r < W; r++) {  // polling its own (already published) flag passes at once
-            const uint32_t addr = base + 4u * r;
+        for (int r = 0; r < (W == 2 ? 1 : W); r++) {
+            // W = 2: only the partner's word (the group's two words are 8-byte aligned, so it is
+            // this wave's address ^ 4); otherwise every word, its own (already published) included
+            const uint32_t addr = W == 2 ? (mine ^ 4u) : base + 4u * r;
             uint32_t tmp, stmp;
             asm volatile(
                 "1:\n\t"
