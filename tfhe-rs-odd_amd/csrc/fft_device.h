@@ -231,6 +231,11 @@ __device__ __forceinline__ cx lds_ld_at(uint32_t a) {
 // twist / M -- without a second twist table or a per-element scale in the CMUX loop.
 __host__ __device__ constexpr double fourier_key_scale(int M) { return 0x1p-64 / (double)M; }
 
+__device__ __forceinline__ double lds_ld_f64(uint32_t a) { return *(const __attribute__((address_space(3))) double *)(uintptr_t)a; }
+// -x when bit 31 of m is set, else x (one XOR into the high word)
+__device__ __forceinline__ double flip_sign(double x, uint32_t m) {
+    return __hiloint2double(__double2hiint(x) ^ (int)(m & 0x80000000u), __double2loint(x));
+}
 __device__ __forceinline__ cx gld(const double2 *__restrict__ p) {
     double2 t = *p;
     return {t.x, t.y};

@@ -130,11 +130,14 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
         }
         // per-lane part of t = d (1 - 4 f) mod 2N with f = freq_lane + freq_slot
         const uint32_t fl = Fft::freq_lane(lane);
+        const uint32_t tw_base = lds_addr(s_twist);
         uint32_t tb[NSEL];
 #pragma unroll
         for (int sel = 1; sel < NSEL; sel++) {
-            tb[sel] = d4[sel] - 4u * d4[sel] * fl;
-            d4[sel] *= 4u;
+            // kept as 16 t (mod 2^32): masked to 16 bits it is the byte offset of table entry t
+            // mod M in its low bits and the quadrant q in bits 14-15 (t < 2N = 4M)
+            tb[sel] = 16u * (d4[sel] - 4u * d4[sel] * fl);
+            d4[sel] *= 64u;
         }
         const double2 *grp = gcol + (size_t)j * NSEL * ggsw_len;
 
@@ -184,14 +187,16 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
                 cx mono[NSEL];
 #pragma unroll
                 for (int sel = 1; sel < NSEL; sel++) {
-                    const uint32_t t = (tb[sel] - d4[sel] * Fft::freq_slot(s)) & (uint32_t)(2 * N - 1);
-                    const uint32_t q = t >> LOG2M;
-                    const double2 w = s_twist[t & (uint32_t)(M - 1)];
-                    const bool sw = q & 1;
-                    double re = sw ? w.y : w.x;
-                    double im = sw ? w.x : w.y;
-                    mono[sel].re = (q == 1 || q == 2) ? -re : re;
-                    mono[sel].im = (q & 2) ? -im : im;
+                    // i^q twist[r]: the swap for odd q is done by the two 8-byte reads' addresses,
+                    // the signs (re: q0 ^ q1, im: q1) by XOR into the high words -- no selects
+                    static_assert(16 * 2 * N == 65536 || LOG2M != 10, "16 t fits 16 bits at N = 2048");
+                    const uint32_t t16 = (tb[sel] - d4[sel] * Fft::freq_slot(s)) & (uint32_t)(16 * 2 * N - 1);
+                    const uint32_t are = tw_base + ((t16 & (uint32_t)(16 * M - 16)) | ((t16 >> (LOG2M + 1)) & 8u));
+                    const double re = lds_ld_f64(are), im = lds_ld_f64(are ^ 8u);
+                    const uint32_t sre = (t16 ^ (t16 >> 1)) << (31 - (LOG2M + 4));  // bit 31 = q0 ^ q1
+                    const uint32_t sim = t16 << (31 - (LOG2M + 5));                // bit 31 = q1
+                    mono[sel].re = flip_sign(re, sre);
+                    mono[sel].im = flip_sign(im, sim);
                 }
                 cx o = (L > 1 && lvl != L) ? acc[L > 1 ? s : 0] : cx{0.0, 0.0};
 #pragma unroll
