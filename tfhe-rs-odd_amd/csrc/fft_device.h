@@ -236,6 +236,17 @@ __device__ __forceinline__ double lds_ld_f64(uint32_t a) { return *(const __attr
 __device__ __forceinline__ double flip_sign(double x, uint32_t m) {
     return __hiloint2double(__double2hiint(x) ^ (int)(m & 0x80000000u), __double2loint(x));
 }
+// Buffer-resource loads: SGPR base (the V#) + a per-lane VGPR byte offset + an SGPR byte offset +
+// an immediate, so a wave-uniform stream costs no VALU address arithmetic.  dword3 0x00020000:
+// raw dwords on gfx9 (CDNA); num_records = 2^31 - 1 bytes.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ double2 buffer_ld_d2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    const v4u t = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+    return make_double2(__hiloint2double((int)t.y, (int)t.x), __hiloint2double((int)t.w, (int)t.z));
+}
 __device__ __forceinline__ cx gld(const double2 *__restrict__ p) {
     double2 t = *p;
     return {t.x, t.y};

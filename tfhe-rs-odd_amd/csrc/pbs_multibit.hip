@@ -36,6 +36,9 @@ namespace tfhe_mi355 {
 #ifndef PBS_MB_MAC_LDS
 #define PBS_MB_MAC_LDS 1
 #endif
+#ifndef PBS_MB_BUFLD
+#define PBS_MB_BUFLD 1  // GGSW loads through a buffer resource: scalar offsets, no 64-bit VALU address adds
+#endif
 constexpr int mb_wpe() { return PBS_WAVES_PER_EU > 0 ? PBS_WAVES_PER_EU : (PBS_MB_CPW >= 4 ? 2 : 1); }
 
 template <int N, int K, int L, int G>
@@ -107,6 +110,9 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
     constexpr size_t ggsw_len = (size_t)L * (K + 1) * (K + 1) * M;
     constexpr size_t lvl_len = (size_t)(K + 1) * (K + 1) * M;
     const double2 *gcol = a.fbsk + (size_t)wave * M + lane;  // column c = wave, this lane
+    // the same column as a buffer resource: per-lane byte offset (VGPR, loop invariant; laundered
+    // through the issue window) + scalar offsets for group / selector / level / row / slot
+    const __amdgpu_buffer_rsrc_t gres = make_rsrc(a.fbsk + (size_t)wave * M);
     const int groups = n / G;
 
     const double k32 = torus_k32();
@@ -140,6 +146,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
             d4[sel] *= 64u;
         }
         const double2 *grp = gcol + (size_t)j * NSEL * ggsw_len;
+        const uint32_t gsoff = (uint32_t)((size_t)j * NSEL * ggsw_len * 16);  // < 2^31 (MB-BSK bytes)
 
         uint32_t st[L > 1 ? 2 * V : 1];
         if constexpr (L > 1) {
@@ -172,6 +179,8 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
                 reinterpret_cast<double2 *>(xb)[s * 64 + lane] = make_double2(v[s].re, v[s].im);
             xsync();
             const double2 *lm = grp + (size_t)(lvl - 1) * lvl_len;
+            const uint32_t lsoff = gsoff + (uint32_t)((lvl - 1) * lvl_len * 16);
+            uint32_t loff = 16u * (uint32_t)lane;
 #pragma unroll
             for (int s = 0; s < V; s++) {
                 // Issue window: slot s's GGSW loads and monomial reads take their addresses from
@@ -179,7 +188,8 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
                 // operands are in flight (hoisted all at once they need ~1 KiB/lane and spill).
                 if (s >= PBS_MB_WINDOW) {
                     const double dep = (L > 1) ? acc[L > 1 ? s - PBS_MB_WINDOW : 0].re : v[s - PBS_MB_WINDOW].re;
-                    asm volatile("" : "+v"(lm) : "v"(dep));
+                    if (PBS_MB_BUFLD) asm volatile("" : "+v"(loff) : "v"(dep));
+                    else asm volatile("" : "+v"(lm) : "v"(dep));
 #pragma unroll
                     for (int sel = 1; sel < NSEL; sel++) asm volatile("" : "+v"(tb[sel]) : "v"(dep));
                 }
@@ -203,10 +213,12 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
                 for (int r = 0; r <= K; r++) {
                     // KB[lvl][r][c] at this frequency (keybundle, oracle mb_keybundle order)
                     const double2 *gp = lm + (size_t)r * (K + 1) * M + s * 64;
-                    double2 kb = gp[0];
+                    const uint32_t rsoff = lsoff + (uint32_t)((r * (K + 1) * M + s * 64) * 16);
+                    double2 kb = PBS_MB_BUFLD ? buffer_ld_d2(gres, loff, rsoff) : gp[0];
 #pragma unroll
                     for (int sel = 1; sel < NSEL; sel++) {
-                        const double2 gg = gp[(size_t)sel * ggsw_len];
+                        const double2 gg = PBS_MB_BUFLD ? buffer_ld_d2(gres, loff, rsoff + (uint32_t)(sel * ggsw_len * 16))
+                                                        : gp[(size_t)sel * ggsw_len];
                         kb.x = fma(gg.x, mono[sel].re, fma(-gg.y, mono[sel].im, kb.x));
                         kb.y = fma(gg.x, mono[sel].im, fma(gg.y, mono[sel].re, kb.y));
                     }
