@@ -136,7 +136,9 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
         }
         // per-lane part of t = d (1 - 4 f) mod 2N with f = freq_lane + freq_slot
         const uint32_t fl = Fft::freq_lane(lane);
-        const uint32_t tw_base = lds_addr(s_twist);
+        // the twist table is the first LDS object and the kernel has no static LDS, so its byte
+        // address is 0 and the monomial read addresses need no base
+        static_assert(Lay::twist_off == 0, "twist table at LDS offset 0");
         uint32_t tb[NSEL];
 #pragma unroll
         for (int sel = 1; sel < NSEL; sel++) {
@@ -199,12 +201,13 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
                 for (int sel = 1; sel < NSEL; sel++) {
                     // i^q twist[r]: the swap for odd q is done by the two 8-byte reads' addresses,
                     // the signs (re: q0 ^ q1, im: q1) by XOR into the high words -- no selects
-                    static_assert(16 * 2 * N == 65536 || LOG2M != 10, "16 t fits 16 bits at N = 2048");
-                    const uint32_t t16 = (tb[sel] - d4[sel] * Fft::freq_slot(s)) & (uint32_t)(16 * 2 * N - 1);
-                    const uint32_t are = tw_base + ((t16 & (uint32_t)(16 * M - 16)) | ((t16 >> (LOG2M + 1)) & 8u));
+                    // 16 t mod 2^32; only bits 4 .. LOG2M + 5 (r, q0, q1) are used below
+                    const uint32_t t16 = tb[sel] - d4[sel] * Fft::freq_slot(s);
+                    const uint32_t are = (t16 & (uint32_t)(16 * M - 16)) | ((t16 >> (LOG2M + 1)) & 8u);
                     const double re = lds_ld_f64(are), im = lds_ld_f64(are ^ 8u);
-                    const uint32_t sre = (t16 ^ (t16 >> 1)) << (31 - (LOG2M + 4));  // bit 31 = q0 ^ q1
-                    const uint32_t sim = t16 << (31 - (LOG2M + 5));                // bit 31 = q1
+                    // q1 at bit 31; adding 2^30 there carries q0 into it: bit 31 = q0 ^ q1
+                    const uint32_t sim = t16 << (31 - (LOG2M + 5));
+                    const uint32_t sre = sim + 0x40000000u;
                     mono[sel].re = flip_sign(re, sre);
                     mono[sel].im = flip_sign(im, sim);
                 }
