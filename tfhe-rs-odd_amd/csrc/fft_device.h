@@ -796,8 +796,13 @@ __device__ __forceinline__ void frac_to_torus(double fr, double k32, double &a, 
 __device__ __forceinline__ void torus_add_frac(uint64_t &c, double fr, double k32) {
     double a, b;
     frac_to_torus(fr, k32, a, b);
-    const uint32_t hi = (uint32_t)(c >> 32) + (uint32_t)__double2loint(a);
-    c = (((uint64_t)hi << 32) | (uint32_t)c) + (uint64_t)__double_as_longlong(b);
+    // one 64-bit add of bits(b), then a 32-bit add into the high word; the opaque copy keeps the
+    // compiler from re-associating the latter into a 64-bit add of the pair (0, lo32(a)), which
+    // costs a v_mov per coefficient to build
+    c += (uint64_t)__double_as_longlong(b);
+    uint32_t hi = (uint32_t)(c >> 32) + (uint32_t)__double2loint(a);
+    asm("" : "+v"(hi));
+    c = ((uint64_t)hi << 32) | (uint32_t)c;
 }
 // c = X
 __device__ __forceinline__ uint64_t torus_from_frac(double fr, double k32) {
