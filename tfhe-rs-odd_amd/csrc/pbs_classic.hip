@@ -45,7 +45,11 @@ struct PbsConfig {
     // VGPRs, no spills) and the twist/M table is dropped, so 31 KiB of tables + 8 x 16 KiB
     // exchange buffers fill the CU's LDS (159 KiB): 8 waves per CU instead of 4, 77.5k -> 96.9k PBS/s.
     static constexpr bool PACK4 = N == 2048 && K == 1 && L == 1;
-    static constexpr bool MAC_LDS = PACK4 ? true : (bool)PBS_MAC_FROM_LDS;
+    // MAC operands (every row spectrum, the wave's own included) read back from LDS instead of
+    // kept in registers: frees the own row's VGPRs.  Per shape (measured, gadget sets): on at
+    // N = 2048 (PACK4) and N = 1024 (TFHE_LIB 93.7k -> 109.3k, ASCON_40 34.3k -> 37.4k,
+    // MANTICORE +2%), off at N = 512 (SIMON_40 -3%, AES_40 -5%: no spills to remove there)
+    static constexpr bool MAC_LDS = PBS_MAC_FROM_LDS >= 0 ? (bool)PBS_MAC_FROM_LDS : (PACK4 || N == 1024);
     // GGSW_i staged in LDS by async global->LDS loads and shared by the workgroup's ciphertexts;
     // fits next to the tables and 2 x (k+1) exchange buffers when it is <= 64 KiB
     // (only without the twist/M table: both do not fit next to four exchange buffers)

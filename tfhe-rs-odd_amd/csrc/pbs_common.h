@@ -15,7 +15,7 @@
 #define PBS_GGSW_PREFETCH 0  // L = 1: GGSW_{i+1} column into registers during CMUX i's inverse FFT (measured 8% slower: AGPR shuffles)
 #endif
 #ifndef PBS_MAC_FROM_LDS
-#define PBS_MAC_FROM_LDS 0
+#define PBS_MAC_FROM_LDS -1  // classic kernel: -1 per-shape default (PbsConfig::MAC_LDS), 0/1 force
 #endif
 #ifndef PBS_WAVES_PER_EU
 #define PBS_WAVES_PER_EU 0  // 0: per-shape default (PbsConfig::WPE); the multi-bit kernel uses 1
