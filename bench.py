@@ -183,10 +183,17 @@ def main():
     P = ALL[pname]
 
     rank, world, local = env_rank_world()
+    # one process per GPU; on a box with fewer GPUs than ranks (a rehearsal of the multi-rank
+    # path, BENCH_DIST_BACKEND=gloo) ranks share devices round-robin
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     def barrier():
         if world > 1:
