@@ -5,15 +5,25 @@ BASELINE.json metric "programmable bootstraps/sec (PARAM_MESSAGE_2_CARRY_2) at 1
 workload = BASELINE config 2: a batch of 4096 independent classic PBS per GPU, identity LUT
 (PARAM_MESSAGE_2_CARRY_2_KS_PBS: n=742, k=1, N=2048, L=1, base 2^23).  One step = one PBS
 launch over the GPU's batch (blind rotation + sample extraction), inputs resident in HBM.
+Model: the reference's throughput bench, tfhe/benches/core_crypto/pbs_bench.rs:430-549.
 
-Multi-GPU (weak scaling): one process per GPU launched by torch.distributed.run; the standard
-BSK is generated once on rank 0 and broadcast ONCE over RCCL (xGMI), each rank converts it to
-the Fourier domain on its own GPU, then each rank bootstraps its own batch -- no collective in
-the timed loop except the bracketing barriers.  value = sum of PBS over ranks / max wall time.
+Multi-GPU (weak scaling): one process per GPU.  `python bench.py --gpus N` with no
+WORLD_SIZE in the environment starts `python -m torch.distributed.run --nproc-per-node N bench.py
+...` as a child process (before anything touches the GPU) and exits with its return code; the
+driver may also launch the ranks itself.  The global batch (N x the per-GPU batch) is split into
+contiguous shards (`shard_range`); the standard BSK is generated once on rank 0 and broadcast
+ONCE over RCCL (xGMI); each rank converts it to the Fourier domain on its own GPU and bootstraps
+its shard -- no collective in the timed loop except the bracketing barriers.  value = sum of PBS
+over ranks / max wall time over ranks.
 
-Also printed: roofline of the dominant kernel (pbs_classic_kernel) -- BSK-streaming HBM model
- with the FP64 fraction beside it -- and the CPU baseline (oracle C restatement,
-1 PBS per thread, rank 0, N=1 only).
+The JSON line also carries the roofline of the dominant kernel (FP64-VALU bound for the
+N <= 2048 kernels; BSK-streaming HBM model at N = 32768 -- DESIGN.md 6), the measured HBM traffic
+from the committed rocprofv3 PMC summaries (profiles/r02_pmc_*.json), the rate of the
+host-pointer C ABI (PCIe-inclusive; never `value`) and the CPU baseline (oracle C restatement,
+1 PBS per thread on the host's CPU share, rank 0, N = 1 only).
+
+`--launch-selftest` runs the rank/shard/aggregation code with a stub step on the CPU (gloo), so
+that the multi-rank path is testable without a GPU (tests/test_bench_launch.py).
 """
 from __future__ import annotations
 
@@ -21,6 +31,8 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -37,6 +49,11 @@ PARAMS = {  # --params choice -> (parameter set name, workload text, kernel name
     "2_2": ("PARAM_MESSAGE_2_CARRY_2_KS_PBS",
             "BASELINE config 2: batch of 4096 independent classic PBS per GPU, identity LUT",
             "pbs_classic_kernel<2048,1,1>"),
+    "2_2ks": ("PARAM_MESSAGE_2_CARRY_2_KS_PBS",
+              "shortint keyswitch -> PBS (apply_lookup_table, shortint/server_key/mod.rs:783-857) over a batch "
+              "of 4096 big-key ciphertexts per GPU, identity LUT; the reference publishes 16.6 ms per KS+PBS "
+              "(benchmarks.md:42)",
+              "pbs_classic_kernel<2048,1,1> (+ ks_digits_kernel + ks_mfma_kernel)"),
     "mb3": ("PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS",
             "BASELINE config 5: batch of 4096 independent multi-bit (grouping 3) PBS per GPU, identity LUT",
             "pbs_multibit_kernel<2048,1,1,3>"),
@@ -45,8 +62,9 @@ PARAMS = {  # --params choice -> (parameter set name, workload text, kernel name
             "large_top_fwd_kernel<1,2> + large_sub_kernel<1,2> + large_top_inv_kernel<1> (+ ks_mfma_kernel)"),
     "mul32": ("PARAM_MESSAGE_2_CARRY_2_KS_PBS",
               "BASELINE config 4: FheUint32 multiply (16-block radix DAG, radix_parallel/mul.rs), "
-              "K independent pairs per GPU, every DAG layer one batched KS+PBS launch",
-              "pbs_classic_kernel<2048,1,1> + keyswitch_kernel"),
+              "K independent pairs per GPU, every DAG layer one batched KS+PBS launch, the whole DAG "
+              "replayed as one hipGraph",
+              "pbs_classic_kernel<2048,1,1> + ks_mfma_kernel"),
     "mb2": ("PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS",
             "batch of 4096 independent multi-bit (grouping 2) PBS per GPU, identity LUT",
             "pbs_multibit_kernel<2048,1,1,2>"),
@@ -72,24 +90,44 @@ PARAMS = {  # --params choice -> (parameter set name, workload text, kernel name
 }
 
 
+# ---------------------------------------------------------------------------------------------
+# models
+
 def ggsw_count(p) -> int:
     g = p.grouping_factor
     return (p.lwe_dimension // g) << g if g else p.lwe_dimension
 
 
-def pbs_algorithmic_bytes(p) -> int:
-    """SURVEY.md 8d BSK-streaming model: |BSK_fourier| + 8(n+1) + 8(kN+1) + 8(k+1)N
-    (multi-bit: (n/g) 2^g GGSWs in the BSK)."""
+def fourier_bsk_bytes(p) -> int:
     M = p.polynomial_size // 2
     k1 = p.glwe_dimension + 1
-    fbsk = ggsw_count(p) * p.pbs_level * k1 * k1 * M * 16
-    return fbsk + 8 * (p.lwe_dimension + 1) + 8 * (p.glwe_dimension * p.polynomial_size + 1) + 8 * k1 * p.polynomial_size
+    return ggsw_count(p) * p.pbs_level * k1 * k1 * M * 16
+
+
+def io_bytes(p, with_ks: bool) -> int:
+    """Per ciphertext: LWE in (big key when keyswitched first) + LWE out."""
+    big = p.glwe_dimension * p.polynomial_size + 1
+    return 8 * ((big if with_ks else p.lwe_dimension + 1) + big)
+
+
+def pbs_streaming_bytes(p) -> int:
+    """BSK-streaming model: |BSK_fourier| + 8(n+1) + 8(kN+1) + 8(k+1)N (every PBS reads the whole
+    key once; multi-bit: (n/g) 2^g GGSWs)."""
+    return fourier_bsk_bytes(p) + io_bytes(p, False) + 8 * (p.glwe_dimension + 1) * p.polynomial_size
+
+
+def pbs_min_unique_bytes(p, batch: int, with_ks: bool) -> float:
+    """Minimal unique bytes per PBS at batch B: |BSK|/B (+ |KSK|/B) + in + out + LUT/B."""
+    b = fourier_bsk_bytes(p) + 8 * (p.glwe_dimension + 1) * p.polynomial_size
+    if with_ks:
+        b += 8 * p.glwe_dimension * p.polynomial_size * p.ks_level * (p.lwe_dimension + 1)
+    return b / batch + io_bytes(p, with_ks)
 
 
 def pbs_flops(p) -> float:
-    """per CMUX ((k+1)L + (k+1)) (5 M log2 M + 6 M) + (k+1)^2 L M 8, times n.
-    Multi-bit: the same external product per group of g, plus the keybundle's (2^g - 1)
-    complex FMAs (8 flop) per GGSW element, times n/g."""
+    """Per CMUX ((k+1)L + (k+1)) (5 M log2 M + 6 M) + (k+1)^2 L M 8, times n.  Multi-bit: the same
+    external product per group of g, plus the keybundle's (2^g - 1) complex FMAs (8 flop) per
+    GGSW element, times n/g."""
     M = p.polynomial_size // 2
     k1 = p.glwe_dimension + 1
     per = (k1 * p.pbs_level + k1) * (5 * M * math.log2(M) + 6 * M) + k1 * k1 * p.pbs_level * M * 8
@@ -100,21 +138,101 @@ def pbs_flops(p) -> float:
     return per * p.lwe_dimension
 
 
-def load_pmc_traffic(batch: int, tag: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json,
-    FETCH_SIZE doubled per MI355X_MICROARCH.md 'HBM' + WRITE_SIZE), scaled to this batch."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json" if tag == "2_2" else f"pmc_traffic_{tag}.json")
+def load_pmc(tag: str):
+    """Committed rocprofv3 PMC summary of this workload (scripts/pmc_workload.sh ->
+    profiles/r02_pmc_<tag>.json): HBM bytes per unit (2*FETCH_SIZE + WRITE_SIZE, gfx950
+    correction of MI355X_MICROARCH.md 'HBM') and the SQ VALU-busy fraction."""
+    for name in (f"r02_pmc_{tag}.json",):
+        path = os.path.join(ROOT, "profiles", name)
+        if os.path.exists(path):
+            d = json.load(open(path))
+            d["_file"] = f"profiles/{name}"
+            return d
+    return None
+
+
+def roofline(tag, p, units_per_launch: int, kernel_ms: float, kname: str, with_ks: bool):
+    """Roofline object of the dominant kernel.  N <= 2048: bound by FP64 VALU issue (DESIGN.md 5.1
+    -- the Fourier BSK is L2/MALL-resident, measured HBM traffic is ~1% of peak); N = 32768: the
+    BSK (2.09 GB) and the spectra stream through HBM/MALL, so the HBM model bounds it."""
+    secs = kernel_ms * 1e-3
+    flop = pbs_flops(p) * units_per_launch
+    fp64 = flop / secs / 1e12
+    pmc = load_pmc(tag)
+    traffic = None
+    if pmc and "hbm_bytes_per_unit" in pmc:
+        traffic = pmc["hbm_bytes_per_unit"] * units_per_launch
+    stream_b = pbs_streaming_bytes(p) + (io_bytes(p, True) - io_bytes(p, False) if with_ks else 0)
+    hbm = {
+        "streaming_model_bytes_per_pbs": stream_b,
+        "streaming_model_GBps": stream_b * units_per_launch / secs / 1e9,
+        "min_unique_bytes_per_pbs": pbs_min_unique_bytes(p, units_per_launch, with_ks),
+        "measured_traffic_GBps": traffic / secs / 1e9 if traffic else None,
+        "measured_frac_of_peak": traffic / secs / 1e9 / HBM_PEAK_GBS if traffic else None,
+        "measured_bytes_per_pbs": traffic / units_per_launch if traffic else None,
+        "traffic_source": pmc["_file"] if pmc else None,
+    }
+    if p.polynomial_size > 2048:
+        achieved = stream_b * units_per_launch / secs / 1e9
+        r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+             "model": (f"BSK-streaming bytes (SURVEY.md 8d): {stream_b:,} B per PBS (incl. the keyswitch's "
+                       "KSK and big-LWE input when keyswitched) x PBS per launch / kernel time"),
+             "fp64": {"achieved": fp64, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                      "frac": fp64 / FP64_PEAK_TFLOPS, "flop_per_pbs": pbs_flops(p)}}
+    else:
+        r = {"bound": "fp64-valu", "achieved": fp64, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+             "frac": fp64 / FP64_PEAK_TFLOPS, "traffic": traffic,
+             "model": (f"FP64 flop model (SURVEY.md 8d): {pbs_flops(p):,.0f} flop per PBS x PBS per launch / "
+                       "kernel time (HIP events on the launch stream"
+                       + (", keyswitch included in the time, its int8 MFMA work not counted)" if with_ks else ")")),
+             "flop_per_pbs": pbs_flops(p),
+             "valu_busy": pmc.get("valu_busy") if pmc else None,
+             "valu_busy_note": ("SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES x waves per SIMD (fraction of each SIMD's "
+                                "issue cycles with a VALU instruction), from the PMC file" if pmc else None)}
+    r["kernel"] = kname
+    r["kernel_ms"] = kernel_ms
+    r["units_per_launch"] = units_per_launch
+    r["hbm"] = hbm
+    return r
+
+
+# ---------------------------------------------------------------------------------------------
+# host / CPU baseline
+
+def cpu_share() -> int:
+    """Threads the CPU baseline may use: the process's affinity set, capped by OMP_NUM_THREADS
+    (the GPU box exports its per-GPU CPU share there: 16)."""
     try:
-        d = json.load(open(path))
-        return float(d["hbm_bytes_per_pbs"]) * batch
+        aff = len(os.sched_getaffinity(0))
     except Exception:
-        return None
+        aff = os.cpu_count() or 1
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(aff, cap) if cap > 0 else aff)
+
+
+def host_info() -> dict:
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 def cpu_baseline(params, bsk, cts, acc, threads: int, ksk=None):
-    """Oracle (C restatement of the reference fft64 PBS) on the host cores, one PBS per thread,
-    as the reference's pbs_throughput bench (benches/core_crypto/pbs_bench.rs:430-549).
-    With `ksk` (config 3) each ciphertext is keyswitched first (threads split the batch)."""
+    """Oracle (C restatement of the reference fft64 PBS, built -O3 -march=x86-64-v3, bit-identical to
+    the -O2 build) on the host cores, one PBS per thread, as the reference's pbs_throughput bench
+    (benches/core_crypto/pbs_bench.rs:430-549).  With `ksk` each ciphertext is keyswitched first
+    (threads split the batch)."""
     sys.path.insert(0, ROOT)
     from concurrent.futures import ThreadPoolExecutor
 
@@ -138,26 +256,176 @@ def cpu_baseline(params, bsk, cts, acc, threads: int, ksk=None):
     else:
         fb = O.FourierBsk(bsk, params.lwe_dimension, params.glwe_dimension, params.polynomial_size,
                           params.pbs_base_log, params.pbs_level)
+    fb.pbs(ks(cts[:1]), acc, threads=1)  # warm (page-in, FFT plan)
     t = time.perf_counter()
     fb.pbs(ks(cts[:1]), acc, threads=1)
     t1 = time.perf_counter() - t
+    # about 15 s of CPU work in total, rounded to whole rounds of `threads`
     count = max(threads, int(round(15.0 / max(t1, 1e-3))))
     count = min(((count + threads - 1) // threads) * threads, cts.shape[0])
     t = time.perf_counter()
     fb.pbs(ks(cts[:count]), acc, threads=threads)
     wall = time.perf_counter() - t
+    ref = "811 ms" if p.polynomial_size == 32768 else "16.6 ms"
+    label = "4_4" if p.polynomial_size == 32768 else "2_2"
+    h = host_info()
     return {
         "value": count / wall,
-        "unit": "PBS/s",
+        "unit": "KS+PBS/s" if ksk is not None else "PBS/s",
         "cores": threads,
         "kind": "port",
+        "host": h,
+        "single_thread_ms": t1 * 1e3,
         "sample": (f"{count} {'KS+' if ksk is not None else ''}PBS of the same {params.name} batch, oracle C "
-                   f"restatement of the reference fft64 PBS, 1 PBS per thread on {threads} threads ({wall:.1f} s wall); "
-                   f"single-thread latency {t1 * 1e3:.1f} ms/PBS (reference published "
-                   f"{'811 ms' if p.polynomial_size == 32768 else '16.6 ms'} KS+PBS at "
-                   f"{'4_4' if p.polynomial_size == 32768 else '2_2'} on Xeon 8375C AVX-512, benchmarks.md:42)"),
+                   f"restatement of the reference fft64 PBS (scalar FFT, -O3 -march=x86-64-v3), 1 PBS per thread "
+                   f"on {threads} threads = this process's CPU share ({wall:.1f} s wall) on {h['cpu_model']} "
+                   f"(nproc {h['nproc']}); single-thread {t1 * 1e3:.1f} ms/{'KS+' if ksk is not None else ''}PBS "
+                   f"against the reference's published {ref} KS+PBS at {label} (Xeon 8375C, concrete-fft AVX-512, "
+                   f"benchmarks.md:42) -- the gap is the restatement's scalar FFT vs concrete-fft's SIMD kernels "
+                   f"and the host CPU, not the algorithm"),
     }
 
+
+# ---------------------------------------------------------------------------------------------
+# ranks
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args) -> int:
+    """--gpus N without a launcher: start N ranks with torch.distributed.run as a child process
+    (nothing in this process has touched the GPU) and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def env_world():
+    return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
+
+
+class Ranks:
+    """Process-group plumbing shared by the GPU workloads and the CPU self-test."""
+
+    def __init__(self, device, backend: str | None):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist = torch, dist
+        self.rank, self.world, self.local = env_world()
+        self.device = device
+        self.backend = None
+        if self.world > 1:
+            self.backend = backend
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=device)
+            else:
+                dist.init_process_group(backend)
+            assert dist.get_world_size() == self.world
+
+    @property
+    def coll_device(self):
+        # gloo reduces host tensors; nccl (RCCL) device tensors
+        return self.device if self.backend == "nccl" else self.torch.device("cpu")
+
+    def barrier(self):
+        if self.world > 1:
+            t = self.torch.ones(1, device=self.coll_device)
+            self.dist.all_reduce(t)
+        if self.device.type == "cuda":
+            self.torch.cuda.synchronize(self.device)
+
+    def max(self, x: float) -> float:
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.coll_device)
+        if self.world > 1:
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, xs) -> list:
+        t = self.torch.tensor(list(xs), dtype=self.torch.int64, device=self.coll_device)
+        if self.world > 1:
+            self.dist.all_reduce(t)
+        return [int(v) for v in t.tolist()]
+
+    def gather(self, xs) -> list:
+        t = self.torch.tensor(list(xs), dtype=self.torch.int64, device=self.coll_device)
+        if self.world == 1:
+            return [list(xs)]
+        outs = [self.torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(outs, t)
+        return [o.tolist() for o in outs]
+
+    def finish(self):
+        if self.world > 1:
+            self.dist.barrier()
+            self.dist.destroy_process_group()
+
+    def info(self) -> dict:
+        ws = self.dist.get_world_size() if self.world > 1 else 1
+        return {"backend": self.backend or "none (single process)", "world_size": ws}
+
+
+def aggregate(R: Ranks, units: int, wall: float, ok: int, of: int, lo: int, hi: int) -> dict:
+    """Sum of units over ranks / max wall over ranks; all-reduced decrypt check; shard table."""
+    wall_max = R.max(wall)
+    total, ok_all, of_all = R.sum([units, ok, of])
+    shards = R.gather([lo, hi])
+    return {"units": total, "wall_max": wall_max, "ok": ok_all, "of": of_all, "shards": shards,
+            "value": total / wall_max}
+
+
+# ---------------------------------------------------------------------------------------------
+# the CPU self-test of the multi-rank path
+
+def run_selftest(args) -> int:
+    import torch
+
+    from tfhe_mi355.distributed import shard_range
+
+    R = Ranks(torch.device("cpu"), os.environ.get("BENCH_DIST_BACKEND", "gloo"))
+    B = args.batch or 64
+    G = R.world * B
+    lo, hi = shard_range(G, R.rank, R.world)
+    msgs = np.random.default_rng(args.seed).integers(0, 16, G).astype(np.uint64)[lo:hi]
+    per_step = 0.02 * (R.rank + 1)   # ranks run at different speeds: the max must win
+
+    def step():
+        time.sleep(per_step)
+        return msgs.copy()            # stub "PBS" with the identity LUT
+
+    for _ in range(args.warmup):
+        step()
+    R.barrier()
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(args.steps):
+        out = step()
+    R.barrier()
+    wall = time.perf_counter() - t0
+    ok = int(np.count_nonzero(out == msgs))
+    agg = aggregate(R, (hi - lo) * args.steps, wall, ok, hi - lo, lo, hi)
+    if R.rank == 0:
+        line = {"metric": "launch self-test (stub step, no GPU)", "selftest": True,
+                "value": agg["value"], "unit": "stub units/s", "n_gpus": R.world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": agg["wall_max"] / args.steps * 1e3,
+                "check": {"decrypted_ok": agg["ok"], "of": agg["of"]},
+                "config": {"global_batch": G, "batch_per_rank": B, "shards": agg["shards"],
+                           "stub_seconds_per_step": [0.02 * (r + 1) for r in range(R.world)]},
+                "units_total": agg["units"], "wall_max_s": agg["wall_max"], **R.info()}
+        print(json.dumps(line), flush=True)
+    R.finish()
+    return 0
+
+
+# ---------------------------------------------------------------------------------------------
+# GPU workloads
 
 def main():
     ap = argparse.ArgumentParser()
@@ -166,54 +434,56 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=0, help="ciphertexts per GPU per step (default 4096; 1024 at 4_4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-abi", action="store_true", help="skip the host-pointer ABI rate")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--params", choices=sorted(PARAMS), default="2_2",
-                    help="2_2 = the BASELINE metric; mb3/mb2 = multi-bit PBS (config 5)")
+                    help="2_2 = the BASELINE metric; 2_2ks = KS+PBS; mb3/mb2 = multi-bit PBS (config 5)")
+    ap.add_argument("--launch-selftest", action="store_true",
+                    help="exercise the rank launch / shard / aggregation path on the CPU (gloo, stub step)")
     args = ap.parse_args()
 
-    import torch
-    import torch.distributed as dist
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}; n_gpus is taken from the world that runs")
+    if args.launch_selftest:
+        sys.exit(run_selftest(args))
 
-    from tfhe_mi355 import Engine, client, fill_accumulator
-    from tfhe_mi355.distributed import broadcast_u64, env_rank_world
+    import torch
+
     from tfhe_mi355.parameters import ALL
 
     pname, workload, kname = PARAMS[args.params]
     P = ALL[pname]
-
-    rank, world, local = env_rank_world()
+    _, world, local = env_world()
     # one process per GPU; on a box with fewer GPUs than ranks (a rehearsal of the multi-rank
     # path, BENCH_DIST_BACKEND=gloo) ranks share devices round-robin
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    if world > 1:
-        backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
-        else:
-            dist.init_process_group(backend)
-
-    def barrier():
-        if world > 1:
-            t = torch.ones(1, device=device)
-            dist.all_reduce(t)
-        torch.cuda.synchronize()
-
+    R = Ranks(device, os.environ.get("BENCH_DIST_BACKEND", "nccl"))  # nccl = RCCL over xGMI
     if args.params == "mul32":
-        return run_mul32(args, P, workload, kname, rank, world, local, device, barrier)
-    B = args.batch or (1024 if args.params == "4_4" else 4096)
-    with_ks = args.params == "4_4"   # config 3 is the shortint KS -> PBS
-    msg_space = P.message_modulus * P.carry_modulus
-    eng = Engine(P, local)
-    # secret keys: derived from the seed on every rank (cheap); the BSK once on rank 0
+        return run_mul32(args, P, workload, kname, R)
+    return run_pbs(args, P, pname, workload, kname, R)
+
+
+def make_keys(args, P, R, with_ks):
+    """Secret keys from the seed on every rank (cheap); BSK (and KSK) generated once on rank 0 and
+    broadcast over RCCL; each rank converts its copy to the Fourier domain."""
+    import torch
+
+    from tfhe_mi355 import Engine, client
+    from tfhe_mi355.distributed import broadcast_u64
+
+    eng = Engine(P, R.device.index)
     lwe_sk = client.gen_binary_key(args.seed, 1, P.lwe_dimension)
     glwe_sk = client.gen_binary_key(args.seed, 2, P.big_lwe_dimension)
     bsk_len = ggsw_count(P) * P.pbs_level * (P.glwe_dimension + 1) ** 2 * P.polynomial_size
-    bsk = None
-    t_key = time.perf_counter()
-    if rank == 0:
+    bsk = ksk = None
+    t = time.perf_counter()
+    if R.rank == 0:
         if P.grouping_factor:
             bsk = client.gen_multi_bit_bootstrap_key(args.seed + 100, lwe_sk, glwe_sk, P.glwe_dimension,
                                                      P.polynomial_size, P.pbs_base_log, P.pbs_level,
@@ -222,218 +492,237 @@ def main():
             bsk = client.gen_bootstrap_key(args.seed + 100, lwe_sk, glwe_sk, P.glwe_dimension,
                                            P.polynomial_size, P.pbs_base_log, P.pbs_level,
                                            P.glwe_modular_std_dev)
-    t_gen = time.perf_counter() - t_key
-    t_bc = time.perf_counter()
-    d_bsk = broadcast_u64(bsk, bsk_len, 0, device)  # one RCCL broadcast (48.6 MB at 2_2)
+    t_gen = time.perf_counter() - t
+    t = time.perf_counter()
+    d_bsk = broadcast_u64(bsk, bsk_len, 0, R.device if R.backend != "gloo" else torch.device("cpu"))
     torch.cuda.synchronize()
-    t_bc = time.perf_counter() - t_bc
-    eng.convert_bootstrap_key_device(d_bsk, bsk_len)
-    torch.cuda.synchronize()
+    t_bc = time.perf_counter() - t
+    eng.convert_bootstrap_key_device(d_bsk.to(R.device), bsk_len)
     del d_bsk
     if with_ks:
         ksk_len = P.big_lwe_dimension * P.ks_level * (P.lwe_dimension + 1)
-        ksk = None
-        if rank == 0:
+        if R.rank == 0:
             ksk = client.gen_keyswitch_key(args.seed + 200, glwe_sk, lwe_sk, P.ks_base_log, P.ks_level,
                                            P.lwe_modular_std_dev)
-        d_ksk = broadcast_u64(ksk, ksk_len, 0, device)
-        eng.upload_keyswitch_key_device(d_ksk, ksk_len)
-        torch.cuda.synchronize()
+        d_ksk = broadcast_u64(ksk, ksk_len, 0, R.device if R.backend != "gloo" else torch.device("cpu"))
+        eng.upload_keyswitch_key_device(d_ksk.to(R.device), ksk_len)
         del d_ksk
-    else:
-        ksk = None
+    torch.cuda.synchronize()
+    return eng, lwe_sk, glwe_sk, bsk, ksk, {"bsk_keygen_s": t_gen, "bsk_broadcast_s": t_bc}
 
-    rng = np.random.default_rng(args.seed * 1000 + rank)
-    msgs = rng.integers(0, msg_space, B).astype(np.uint64)
-    if with_ks:
-        cts = client.lwe_encrypt(args.seed * 1000 + rank, glwe_sk, msgs * np.uint64(P.delta),
-                                 P.glwe_modular_std_dev)
-    else:
-        cts = client.lwe_encrypt(args.seed * 1000 + rank, lwe_sk, msgs * np.uint64(P.delta),
-                                 P.lwe_modular_std_dev)
+
+def host_abi_rate(eng, P, cts, acc, with_ks: bool, reps: int = 3) -> dict:
+    """Rate of the synchronous host-pointer entry point (numpy in, numpy out: the form the Rust
+    binding of INTEGRATION.md calls), chunk-pipelined through pinned staging; PCIe-inclusive."""
+    f = eng.keyswitch_programmable_bootstrap if with_ks else eng.programmable_bootstrap
+    f(cts, acc)
+    t = time.perf_counter()
+    for _ in range(reps):
+        out = f(cts, acc)
+    wall = time.perf_counter() - t
+    B = cts.shape[0]
+    mb_in, mb_out = cts.nbytes / 1e6, out.nbytes / 1e6
+    return {"value": B * reps / wall, "unit": "KS+PBS/s" if with_ks else "PBS/s", "batch": B,
+            "entry_point": ("tfhe_mi355_keyswitch_programmable_bootstrap" if with_ks
+                            else "tfhe_mi355_programmable_bootstrap"),
+            "note": (f"host numpy buffers in and out ({mb_in:.1f} MB in, {mb_out:.1f} MB out per call), "
+                     "two-lane chunked H2D/kernel/D2H pipeline through pinned staging; PCIe-inclusive, "
+                     "rank 0's GPU, not the headline value")}
+
+
+def run_pbs(args, P, pname, workload, kname, R):
+    import torch
+
+    from tfhe_mi355 import client, fill_accumulator
+    from tfhe_mi355.distributed import shard_range
+
+    with_ks = args.params in ("4_4", "2_2ks")   # config 3 and the 2_2 KS+PBS line
+    B = args.batch or (1024 if args.params == "4_4" else 4096)
+    msg_space = P.message_modulus * P.carry_modulus
+    eng, lwe_sk, glwe_sk, bsk, ksk, setup = make_keys(args, P, R, with_ks)
+
+    G = R.world * B
+    lo, hi = shard_range(G, R.rank, R.world)
+    msgs = np.random.default_rng(args.seed).integers(0, msg_space, G).astype(np.uint64)[lo:hi]
+    key, std = (glwe_sk, P.glwe_modular_std_dev) if with_ks else (lwe_sk, P.lwe_modular_std_dev)
+    cts = client.lwe_encrypt(args.seed * 1000 + R.rank, key, msgs * np.uint64(P.delta), std)
+    nb = hi - lo
     acc = fill_accumulator(P, lambda x: x)
-    d_in = torch.from_numpy(cts.view(np.int64)).to(device)
-    d_out = torch.zeros((B, P.big_lwe_dimension + 1), dtype=torch.int64, device=device)
-    d_lut = torch.from_numpy(acc.view(np.int64)).to(device)
+    d_in = torch.from_numpy(cts.view(np.int64)).to(R.device)
+    d_out = torch.zeros((nb, P.big_lwe_dimension + 1), dtype=torch.int64, device=R.device)
+    d_lut = torch.from_numpy(acc.view(np.int64)).to(R.device)
     stream = torch.cuda.current_stream()
-    if with_ks:
-        d_scratch = torch.empty(eng.ks_pbs_scratch_bytes(B), dtype=torch.uint8, device=device)
+    need = eng.ks_pbs_scratch_bytes(nb) if with_ks else eng.pbs_scratch_bytes(nb)
+    d_scratch = torch.empty(max(need, 1), dtype=torch.uint8, device=R.device)
 
     def step():
         if with_ks:
-            eng.keyswitch_programmable_bootstrap_async(d_in, d_out, d_lut, 1, B, d_scratch, stream=stream)
+            eng.keyswitch_programmable_bootstrap_async(d_in, d_out, d_lut, 1, nb, d_scratch, stream=stream)
         else:
-            eng.programmable_bootstrap_async(d_in, d_out, d_lut, 1, B, stream=stream)
+            eng.programmable_bootstrap_async(d_in, d_out, d_lut, 1, nb, stream=stream, d_scratch=d_scratch)
 
     for _ in range(args.warmup):
         step()
-    barrier()
+    R.barrier()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for s, e in evs:
         s.record(stream)
         step()
         e.record(stream)
-    barrier()
+    R.barrier()
     wall = time.perf_counter() - t0
     kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
-    tt = torch.tensor([wall], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    wall_max = float(tt.item())
 
-    # correctness of this rank's outputs (decrypt with the big key)
     out = d_out.cpu().numpy().view(np.uint64)
     dec = client.decode(client.lwe_decrypt(glwe_sk, out), P.delta) % np.uint64(msg_space)
     ok = int(np.count_nonzero(dec == msgs))
-    okt = torch.tensor([ok, B], dtype=torch.int64, device=device)
-    if world > 1:
-        dist.all_reduce(okt)
+    agg = aggregate(R, nb * args.steps, wall, ok, nb, lo, hi)
 
-    if rank == 0:
-        total = world * B * args.steps
-        value = total / wall_max
-        per_launch_bytes = pbs_algorithmic_bytes(P) * B
-        achieved = per_launch_bytes / (kernel_ms * 1e-3) / 1e9
-        flops = pbs_flops(P) * B / (kernel_ms * 1e-3) / 1e12
+    host_abi = None
+    if not args.no_host_abi and R.rank == 0 and P.polynomial_size <= 2048:
+        host_abi = host_abi_rate(eng, P, cts, acc, with_ks)
+
+    if R.rank == 0:
+        unit = "KS+PBS/s" if with_ks else "PBS/s"
+        if args.params == "2_2":
+            metric = "programmable bootstraps/sec (PARAM_MESSAGE_2_CARRY_2) at 1/2/4/8 MI355X"
+        elif with_ks:
+            metric = f"keyswitch + programmable bootstraps/sec ({pname}) at 1/2/4/8 MI355X"
+        else:
+            metric = f"programmable bootstraps/sec ({pname}) at 1/2/4/8 MI355X"
         line = {
-            "metric": ("programmable bootstraps/sec (PARAM_MESSAGE_2_CARRY_2) at 1/2/4/8 MI355X"
-                       if args.params == "2_2" else f"programmable bootstraps/sec ({pname}) at 1/2/4/8 MI355X"),
-            "value": value,
-            "unit": "PBS/s",
-            "n_gpus": world,
+            "metric": metric,
+            "value": agg["value"],
+            "unit": unit,
+            "n_gpus": R.world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": wall_max / args.steps * 1e3,
+            "ms_per_step": agg["wall_max"] / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (seeded LWE encryptions of uniform 4-bit messages; keys from the engine's client-side keygen)",
+            "data": "synthetic (seeded LWE encryptions of uniform messages; keys from the engine's client-side keygen)",
             "config": {
                 "workload": workload,
                 "parameters": (f"{pname} (n={P.lwe_dimension}, k={P.glwe_dimension}, N={P.polynomial_size}, "
                                f"pbs 2^{P.pbs_base_log} x {P.pbs_level}"
+                               + (f", ks 2^{P.ks_base_log} x {P.ks_level}" if with_ks else "")
                                + (f", grouping {P.grouping_factor})" if P.grouping_factor else ")")),
                 "batch_per_gpu": B,
-                "global_batch": world * B,
-                "parallelism": f"dp{world} (batch shards, BSK replicated by one RCCL broadcast)",
+                "global_batch": G,
+                "shards": agg["shards"],
+                "parallelism": f"dp{R.world} (contiguous batch shards, BSK replicated by one RCCL broadcast)",
             },
-            "roofline": {
-                "bound": "hbm",
-                "model": (f"BSK-streaming (SURVEY.md 8d): {pbs_algorithmic_bytes(P):,} B per PBS; "
-                          "frac > 1 would mean reuse beyond streaming"),
-                "kernel": kname,
-                "kernel_ms": kernel_ms,
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": load_pmc_traffic(B, args.params),
-                "fp64": {"achieved": flops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": flops / FP64_PEAK_TFLOPS,
-                         "flop_per_pbs": pbs_flops(P)},
-            },
-            "check": {"decrypted_ok": int(okt[0].item()), "of": int(okt[1].item())},
-            "setup": {"bsk_keygen_s": t_gen, "bsk_broadcast_s": t_bc},
+            **R.info(),
+            "roofline": roofline(args.params, P, nb, kernel_ms, kname, with_ks),
+            "check": {"decrypted_ok": agg["ok"], "of": agg["of"]},
+            "setup": setup,
         }
-        if world == 1 and not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        if host_abi:
+            line["host_abi"] = host_abi
+        if R.world == 1 and not args.no_cpu_baseline:
+            threads = args.cpu_threads or cpu_share()
             line["cpu_baseline"] = cpu_baseline(P, bsk, cts, acc, threads, ksk)
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    R.finish()
 
 
-def run_mul32(args, P, workload, kname, rank, world, local, device, barrier):
+def run_mul32(args, P, workload, kname, R):
     """Config 4: K FheUint32 multiplies per GPU per step through the batched integer DAG
-    (tfhe_mi355.integer); value = multiplies/s over all ranks."""
+    (tfhe_mi355.integer), the whole DAG captured once into a hipGraph and replayed per step;
+    value = multiplies/s over all ranks."""
     import torch
-    import torch.distributed as dist
 
     from tfhe_mi355 import Engine, client, integer, shortint
-    from tfhe_mi355.distributed import broadcast_u64
+    from tfhe_mi355.distributed import broadcast_u64, shard_range
 
     K = args.batch or 256
     ck = shortint.ClientKey(P, args.seed)
-    eng = Engine(P, local)
+    eng = Engine(P, R.device.index)
     bsk_len = ggsw_count(P) * P.pbs_level * (P.glwe_dimension + 1) ** 2 * P.polynomial_size
     ksk_len = P.big_lwe_dimension * P.ks_level * (P.lwe_dimension + 1)
     bsk = ksk = None
-    if rank == 0:
+    if R.rank == 0:
         bsk = client.gen_bootstrap_key(args.seed + 100, ck.small_lwe_secret_key, ck.glwe_secret_key,
                                        P.glwe_dimension, P.polynomial_size, P.pbs_base_log, P.pbs_level,
                                        P.glwe_modular_std_dev)
         ksk = client.gen_keyswitch_key(args.seed + 200, ck.large_lwe_secret_key, ck.small_lwe_secret_key,
                                        P.ks_base_log, P.ks_level, P.lwe_modular_std_dev)
-    d = broadcast_u64(bsk, bsk_len, 0, device)
-    eng.convert_bootstrap_key_device(d, bsk_len)
-    d = broadcast_u64(ksk, ksk_len, 0, device)
-    eng.upload_keyswitch_key_device(d, ksk_len)
+    bdev = R.device if R.backend != "gloo" else torch.device("cpu")
+    d = broadcast_u64(bsk, bsk_len, 0, bdev)
+    eng.convert_bootstrap_key_device(d.to(R.device), bsk_len)
+    d = broadcast_u64(ksk, ksk_len, 0, bdev)
+    eng.upload_keyswitch_key_device(d.to(R.device), ksk_len)
     torch.cuda.synchronize()
     del d
     sks = integer.ServerKey(shortint.ServerKey(None, engine=eng, parameters=P))
     cks = integer.ClientKey(ck, 16)
-    rng = np.random.default_rng(args.seed * 1000 + rank)
-    a = rng.integers(0, 2 ** 32, K, dtype=np.uint64)
-    b = rng.integers(0, 2 ** 32, K, dtype=np.uint64)
+    G = R.world * K
+    lo, hi = shard_range(G, R.rank, R.world)
+    rng = np.random.default_rng(args.seed)
+    a = rng.integers(0, 2 ** 32, G, dtype=np.uint64)[lo:hi]
+    b = rng.integers(0, 2 ** 32, G, dtype=np.uint64)[lo:hi]
     ca, cb = cks.encrypt(a), cks.encrypt(b)
     ca_d, cb_d = sks.to_device(ca), sks.to_device(cb)   # operands resident in HBM
 
-    out = None
-    for _ in range(args.warmup):
-        out = sks.mul_parallelized(ca_d, cb_d)
-    barrier()
+    # eager warm-up (fills the layer LUT caches), then capture the whole DAG once
+    out = sks.mul_parallelized(ca_d, cb_d)
+    torch.cuda.synchronize()
     pbs0, l0 = sks.pbs_count, sks.launches
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
         out = sks.mul_parallelized(ca_d, cb_d)
-    barrier()
+    pbs_per_mul = (sks.pbs_count - pbs0) / (hi - lo)
+    launches = sks.launches - l0
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        graph.replay()
+    R.barrier()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for s, e in evs:
+        s.record(stream)
+        graph.replay()
+        e.record(stream)
+    R.barrier()
     wall = time.perf_counter() - t0
-    pbs_per_mul = (sks.pbs_count - pbs0) / (args.steps * K)
-    launches = (sks.launches - l0) / args.steps
-    tt = torch.tensor([wall], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    wall_max = float(tt.item())
+    step_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
     ok = int(np.count_nonzero(cks.decrypt(out) == (a * b) % np.uint64(1 << 32)))
-    okt = torch.tensor([ok, K], dtype=torch.int64, device=device)
-    if world > 1:
-        dist.all_reduce(okt)
-    if rank == 0:
-        muls = world * K * args.steps
-        pbs_rate = muls * pbs_per_mul / wall_max
+    agg = aggregate(R, (hi - lo) * args.steps, wall, ok, hi - lo, lo, hi)
+    if R.rank == 0:
+        pbs_rate = agg["value"] * pbs_per_mul
+        units = int(round(pbs_per_mul * (hi - lo)))
+        rl = roofline("mul32", P, units, step_ms, kname, True)
+        rl["model"] += "; the step is the whole multiply DAG (11 KS+PBS layers and the LWE additions)"
         line = {
             "metric": "FheUint32 multiplies/sec (PARAM_MESSAGE_2_CARRY_2 radix, 16 blocks) at 1/2/4/8 MI355X",
-            "value": muls / wall_max,
+            "value": agg["value"],
             "unit": "mul/s",
-            "n_gpus": world,
+            "n_gpus": R.world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": wall_max / args.steps * 1e3,
+            "ms_per_step": agg["wall_max"] / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (uniform u32 operand pairs, seeded encryptions)",
             "config": {"workload": workload, "parameters": P.name, "pairs_per_gpu": K,
-                       "global_pairs": world * K, "pbs_per_multiply": pbs_per_mul,
+                       "global_pairs": G, "shards": agg["shards"], "pbs_per_multiply": pbs_per_mul,
                        "launches_per_multiply_batch": launches,
-                       "parallelism": f"dp{world} (whole multiplies sharded, keys broadcast once)"},
+                       "parallelism": f"dp{R.world} (whole multiplies sharded, keys broadcast once)"},
+            **R.info(),
             "pbs_per_sec": pbs_rate,
-            "roofline": {"bound": "hbm", "kernel": kname,
-                         "achieved": pbs_rate * pbs_algorithmic_bytes(P) / 1e9, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": pbs_rate * pbs_algorithmic_bytes(P) / 1e9 / HBM_PEAK_GBS,
-                         "traffic": None,
-                         "model": "BSK-streaming bytes per PBS x PBS/s of the whole DAG (host orchestration included)"},
-            "check": {"decrypted_ok": int(okt[0].item()), "of": int(okt[1].item())},
+            "roofline": rl,
+            "check": {"decrypted_ok": agg["ok"], "of": agg["of"]},
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if R.world == 1 and not args.no_cpu_baseline:
             sys.path.insert(0, ROOT)
             from oracle.oracle import OracleEngine  # oracle behind the engine API (test infrastructure)
 
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            threads = args.cpu_threads or cpu_share()
             oe = OracleEngine(P, threads=threads)
             oe.upload_bootstrap_key(bsk)
             oe.upload_keyswitch_key(ksk)
@@ -442,15 +731,13 @@ def run_mul32(args, P, workload, kname, rank, world, local, device, barrier):
             csk.mul_parallelized(RadixSlice(ca, 2), RadixSlice(cb, 2))
             cw = time.perf_counter() - t
             line["cpu_baseline"] = {
-                "value": 2 / cw, "unit": "mul/s", "cores": threads, "kind": "port",
+                "value": 2 / cw, "unit": "mul/s", "cores": threads, "kind": "port", "host": host_info(),
                 "sample": (f"2 FheUint32 multiplies through the same DAG with the oracle C restatement behind "
                            f"the engine API, {threads} threads ({cw:.1f} s); reference published 333 ms/mul "
                            f"on a 128-vCPU m6i.metal (benchmarks.md:17)"),
             }
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    R.finish()
 
 
 def RadixSlice(rb, n):

@@ -19,9 +19,20 @@
  *                          (lwe_keyswitch_key.rs:102-108, lwe_keyswitch_key_generation.rs:109);
  *   - "_async" entry points take DEVICE pointers and a hipStream_t (as void*), enqueue the work
  *     and return immediately; the others take HOST pointers and return after the outputs are
- *     written (synchronous);
- *   - a context is bound to one GPU; calls on one context are serialised by an internal mutex,
- *     so rayon-style concurrent callers sharing a key are safe (SURVEY.md 8b "Threading").
+ *     written (synchronous).  The host-pointer forms pipeline the batch in chunks through
+ *     page-locked staging on two streams (copies of one chunk overlap the kernels of the next);
+ *   - a context is bound to one GPU; host-pointer calls on one context are serialised by an
+ *     internal mutex, so rayon-style concurrent callers sharing a key are safe (SURVEY.md 8b
+ *     "Threading").  The _async calls hold no per-context mutable state: every device scratch
+ *     buffer they need comes from the caller (d_scratch, sized by the matching *_scratch query;
+ *     a query returning 0 means d_scratch may be NULL), so concurrent callers on different
+ *     streams only need scratch buffers of their own, and the calls can be captured into a
+ *     hipGraph (no allocation or synchronisation inside);
+ *   - _async lut index arrays are not checked on the host (they live on the device): an entry
+ *     >= lut_count is clamped to lut_count - 1 by the kernels (no out-of-bounds read); the
+ *     host-pointer forms reject such an entry with an error;
+ *   - keys uploaded through the _async/device forms are complete when the upload call returns
+ *     (it waits for its stream), so any later call on any stream sees the whole key.
  */
 #ifndef TFHE_MI355_H
 #define TFHE_MI355_H
@@ -106,7 +117,12 @@ int tfhe_mi355_programmable_bootstrap(TfheMi355Context *ctx, const uint64_t *lwe
 int tfhe_mi355_programmable_bootstrap_async(TfheMi355Context *ctx, const uint64_t *d_lwe_in,
                                             uint64_t *d_lwe_out, const uint64_t *d_luts,
                                             size_t lut_count, const uint32_t *d_lut_indexes,
-                                            size_t count, void *stream);
+                                            size_t count, void *d_scratch, size_t scratch_bytes,
+                                            void *stream);
+/* Device scratch (bytes) of the async PBS for `count` ciphertexts: 0 for N <= 2048 and multi-bit;
+ * at N = 32768 the accumulators + spectra of one pass (1.5 MiB per ciphertext, passes of <= 128;
+ * less scratch = smaller passes, at least one ciphertext's worth). */
+int tfhe_mi355_programmable_bootstrap_scratch(TfheMi355Context *ctx, size_t count, size_t *bytes);
 
 /* Batched blind rotation WITHOUT sample extraction: glwe_out[c] = the rotated accumulator
  * ((k+1)*N words, GLWE layout) of lwe_in[c] with LUT luts[lut_indexes ? lut_indexes[c] : 0].
@@ -144,7 +160,8 @@ int tfhe_mi355_packing_keyswitch_key_upload(TfheMi355Context *ctx, const uint64_
                                             uint32_t base_log, uint32_t level);
 int tfhe_mi355_packing_keyswitch(TfheMi355Context *ctx, const uint64_t *lwe_in, uint64_t *glwe_out, size_t count);
 int tfhe_mi355_packing_keyswitch_async(TfheMi355Context *ctx, const uint64_t *d_lwe_in, uint64_t *d_glwe_out,
-                                       size_t count, void *stream);
+                                       size_t count, void *d_scratch, size_t scratch_bytes, void *stream);
+int tfhe_mi355_packing_keyswitch_scratch(TfheMi355Context *ctx, size_t count, size_t *bytes);
 
 /* GLWE x plaintext-polynomial products over (Z/2^64)[X]/(X^N+1):
  *   out[c][i] = sum_{j < glwe_per_item} glwe_in[c][j] * polys[i][j]   (each GLWE polynomial)
@@ -163,7 +180,9 @@ int tfhe_mi355_glwe_poly_mul_async(TfheMi355Context *ctx, const uint64_t *d_glwe
  * Replaces keyswitch_lwe_ciphertext (lwe_keyswitch.rs:96-170). */
 int tfhe_mi355_keyswitch(TfheMi355Context *ctx, const uint64_t *lwe_in, uint64_t *lwe_out, size_t count);
 int tfhe_mi355_keyswitch_async(TfheMi355Context *ctx, const uint64_t *d_lwe_in, uint64_t *d_lwe_out,
-                               size_t count, void *stream);
+                               size_t count, void *d_scratch, size_t scratch_bytes, void *stream);
+/* Device scratch (bytes) of the async keyswitch: the int8-MFMA path's digit matrix. */
+int tfhe_mi355_keyswitch_scratch(TfheMi355Context *ctx, size_t count, size_t *bytes);
 
 /* shortint KS -> PBS (PBSOrder::KeyswitchBootstrap): lwe_in/out count x (k*N+1).
  * Replaces ServerKey::keyswitch_programmable_bootstrap_assign (shortint/server_key/mod.rs:783-857). */
@@ -173,8 +192,10 @@ int tfhe_mi355_keyswitch_programmable_bootstrap(TfheMi355Context *ctx, const uin
 int tfhe_mi355_keyswitch_programmable_bootstrap_async(TfheMi355Context *ctx, const uint64_t *d_lwe_in,
                                                       uint64_t *d_lwe_out, const uint64_t *d_luts,
                                                       size_t lut_count, const uint32_t *d_lut_indexes,
-                                                      size_t count, void *d_scratch, void *stream);
-/* Device scratch (bytes) needed by the async KS->PBS for `count` ciphertexts. */
+                                                      size_t count, void *d_scratch, size_t scratch_bytes,
+                                                      void *stream);
+/* Device scratch (bytes) needed by the async KS->PBS for `count` ciphertexts: the small-LWE
+ * intermediate plus the larger of the keyswitch and PBS scratch. */
 int tfhe_mi355_keyswitch_programmable_bootstrap_scratch(TfheMi355Context *ctx, size_t count,
                                                         size_t *bytes);
 
@@ -183,6 +204,14 @@ int tfhe_mi355_keyswitch_programmable_bootstrap_scratch(TfheMi355Context *ctx, s
 int tfhe_mi355_programmable_bootstrap_keyswitch(TfheMi355Context *ctx, const uint64_t *lwe_in,
                                                 uint64_t *lwe_out, const uint64_t *luts, size_t lut_count,
                                                 const uint32_t *lut_indexes, size_t count);
+int tfhe_mi355_programmable_bootstrap_keyswitch_async(TfheMi355Context *ctx, const uint64_t *d_lwe_in,
+                                                      uint64_t *d_lwe_out, const uint64_t *d_luts,
+                                                      size_t lut_count, const uint32_t *d_lut_indexes,
+                                                      size_t count, void *d_scratch, size_t scratch_bytes,
+                                                      void *stream);
+/* Device scratch (bytes) of the async PBS->KS: the big-LWE intermediate plus the larger of the
+ * PBS and keyswitch scratch. */
+int tfhe_mi355_programmable_bootstrap_keyswitch_scratch(TfheMi355Context *ctx, size_t count, size_t *bytes);
 
 /* Batched LWE linear algebra on device rows of u64 words (wrapping mod 2^64):
  *   y[r] = y[r] * scalar + (d_x ? x[r] : 0)   for r < rows, `words` words per row,

@@ -1,0 +1,27 @@
+#!/bin/bash
+# rocprofv3 PMC passes (one counter group per run, each under its own time limit) of one bench
+# workload, summarised into profiles/r02_pmc_<tag>.json.   usage: pmc_workload.sh <tag>
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+tag=$1
+mkdir -p gpurun_out/pmc_$tag
+case $tag in
+  2_2)   K='pbs_classic_kernel'; U='pbs_classic_kernel'; UPD=4096; M='pbs_classic_kernel'; ARGS="--params 2_2" ;;
+  2_2ks) K='pbs_classic_kernel|ks_digits|ks_mfma'; U='pbs_classic_kernel'; UPD=4096; M='pbs_classic_kernel'; ARGS="--params 2_2ks" ;;
+  mb3)   K='pbs_multibit_kernel'; U='pbs_multibit_kernel'; UPD=4096; M='pbs_multibit_kernel'; ARGS="--params mb3" ;;
+  mb2)   K='pbs_multibit_kernel'; U='pbs_multibit_kernel'; UPD=4096; M='pbs_multibit_kernel'; ARGS="--params mb2" ;;
+  4_4)   K='large_(init|top|sub|extract)|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=128; M='large_sub_kernel'; ARGS="--params 4_4" ;;
+  *) echo "unknown tag $tag"; exit 2 ;;
+esac
+B="$ARGS --steps 2 --warmup 1 --no-cpu-baseline --no-host-abi"
+run() {  # run NAME COUNTERS...
+  local n=$1; shift
+  timeout -k 10 240 rocprofv3 --pmc "$@" -d gpurun_out/pmc_$tag/$n -o run --output-format csv -- python3 bench.py $B \
+    > gpurun_out/pmc_$tag/$n.log 2>&1
+  local rc=$?; echo "pmc $tag $n rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/pmc_$tag/$n.log; exit $rc; }
+}
+run fetch FETCH_SIZE && run write WRITE_SIZE && \
+run sq SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE && \
+python3 scripts/pmc_workload.py --fetch gpurun_out/pmc_$tag/fetch --write gpurun_out/pmc_$tag/write \
+  --sq gpurun_out/pmc_$tag/sq --tag $tag --kernels "$K" --unit-kernel "$U" --units-per-dispatch $UPD \
+  --main-kernel "$M" --out gpurun_out/r02_pmc_$tag.json

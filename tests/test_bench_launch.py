@@ -1,0 +1,52 @@
+"""bench.py's multi-rank path on the CPU (no GPU): `--gpus 2` without a launcher starts two ranks
+through torch.distributed.run (gloo), the ranks take contiguous shards of the global batch
+(shard_range), and rank 0 reports sum-of-units / max-wall and the all-reduced check count --
+the aggregation the 1/2/4/8-GPU PBS/s line uses (model
+tfhe/benches/core_crypto/pbs_bench.rs:430-549)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, extra_env=None, timeout=150):
+    env = dict(os.environ, BENCH_DIST_BACKEND="gloo", OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    env.pop("LOCAL_RANK", None)
+    if extra_env:
+        env.update(extra_env)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p, lines
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpus_flag_launches_ranks_and_aggregates(world):
+    p, lines = _run(["--gpus", str(world), "--launch-selftest", "--steps", "3", "--warmup", "1", "--batch", "10"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert len(lines) == 1, p.stdout          # only rank 0 prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == world and d["world_size"] == world and d["backend"] == "gloo"
+    G = 10 * world
+    assert d["config"]["global_batch"] == G
+    shards = d["config"]["shards"]
+    assert shards[0][0] == 0 and shards[-1][1] == G
+    assert all(a[1] == b[0] for a, b in zip(shards, shards[1:]))
+    assert d["check"] == {"decrypted_ok": G, "of": G}
+    assert d["units_total"] == G * 3
+    # value = all units / the SLOWEST rank's wall (rank world-1 sleeps 0.02*world s per step)
+    assert d["wall_max_s"] >= 3 * 0.02 * world
+    assert abs(d["value"] - d["units_total"] / d["wall_max_s"]) < 1e-6 * d["value"]
+
+
+def test_gpus_mismatch_with_world_is_an_error():
+    p, _ = _run(["--gpus", "2", "--launch-selftest"], extra_env={"WORLD_SIZE": "1"})
+    assert p.returncode != 0
+    assert "WORLD_SIZE" in (p.stderr + p.stdout)

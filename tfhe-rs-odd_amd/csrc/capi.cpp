@@ -57,6 +57,10 @@ int guarded(F &&f) {
 struct DeviceBuffer {
     void *ptr = nullptr;
     size_t bytes = 0;
+    DeviceBuffer() = default;
+    DeviceBuffer(const DeviceBuffer &) = delete;
+    DeviceBuffer &operator=(const DeviceBuffer &) = delete;
+    ~DeviceBuffer() { release(); }
     void reserve(size_t b) {
         if (b <= bytes) return;
         if (ptr) check(hipFree(ptr), "hipFree");
@@ -72,6 +76,35 @@ struct DeviceBuffer {
     }
 };
 
+// page-locked host staging of the host-pointer entry points (hipHostMalloc), one per pipeline lane
+struct PinnedBuffer {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+    PinnedBuffer() = default;
+    PinnedBuffer(const PinnedBuffer &) = delete;
+    PinnedBuffer &operator=(const PinnedBuffer &) = delete;
+    ~PinnedBuffer() { release(); }
+    void reserve(size_t b) {
+        if (b <= bytes) return;
+        release();
+        check(hipHostMalloc(&ptr, b, hipHostMallocDefault), "hipHostMalloc");
+        bytes = b;
+    }
+    void release() {
+        if (ptr) (void)hipHostFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+};
+
+// an environment switch is on when set to a non-empty value other than "0"
+bool env_flag(const char *name) {
+    const char *e = std::getenv(name);
+    return e && *e && std::strcmp(e, "0") != 0;
+}
+
+size_t align256(size_t b) { return (b + 255) / 256 * 256; }
+
 bool is_pow2(uint32_t x) { return x && !(x & (x - 1)); }
 }  // namespace
 
@@ -82,10 +115,21 @@ struct TfheMi355Context {
     hipStream_t stream = nullptr;
     FftTables tables;
     DeviceBuffer fbsk, ksk, std_staging;
-    DeviceBuffer io_in, io_out, io_luts, io_idx, io_tmp;
-    DeviceBuffer pbs_scratch;  // N = 32768: accumulators + spectra of one chunk of ciphertexts
+    DeviceBuffer io_luts, io_tmp;
     DeviceBuffer ksk_planes;   // int8 byte planes of the KSK for the MFMA keyswitch
-    DeviceBuffer ks_scratch;   // MFMA keyswitch digits
+    // Host-pointer entry points: a two-lane pipeline (stream, pinned staging, device buffers and
+    // scratch per lane) so that chunk i's copies overlap chunk i+-1's kernels.  Only the
+    // synchronous entry points use these, under `mu`; the _async entry points take all their
+    // scratch from the caller (no shared mutable state, capturable into a hipGraph).
+    struct Lane {
+        hipStream_t stream = nullptr;
+        hipEvent_t done = nullptr;
+        PinnedBuffer h_in, h_out, h_idx;
+        DeviceBuffer d_in, d_out, d_idx, scratch;
+        bool pending = false;
+        size_t first = 0, count = 0;
+    } lanes[2];
+    hipEvent_t luts_ready = nullptr;
     bool ksk_planes_ready = false;
     bool fbsk_ready = false, ksk_ready = false;
     // LWE -> GLWE packing keyswitching key of the gadget layer (big LWE key -> GLWE key)
@@ -164,17 +208,77 @@ hipError_t convert_bsk(TfheMi355Context *c, const uint64_t *d_std, size_t npoly,
     return launch_bsk_to_fourier((int)c->N(), d_std, (double2 *)c->fbsk.ptr, npoly, c->tables, s);
 }
 
+// ---- scratch sizes -----------------------------------------------------------------------------
+// Every launcher takes its device scratch explicitly: the _async entry points pass the caller's
+// d_scratch (sized by the *_scratch queries), the host-pointer entry points a lane's own buffer.
+
+bool is_large(const TfheMi355Context *c) {
+    return !c->p.grouping_factor && large_pbs_supported((int)c->N(), (int)c->k(), (int)c->p.pbs_level);
+}
+
+// N = 32768: ciphertexts per pass of the three-launch CMUX.  The chunk's accumulators + spectra
+// (1.5 MiB per ciphertext at 4_4) should stay resident in the 256 MiB Infinity Cache.
+size_t large_chunk() {
+    static const size_t v = [] {
+        const char *e = std::getenv("TFHE_MI355_LARGE_CHUNK");
+        const long x = e ? std::atol(e) : 0;
+        return x > 0 ? (size_t)x : (size_t)128;  // 128: best of 64..1024 at 4_4 (profiles)
+    }();
+    return v;
+}
+
+size_t pbs_scratch_bytes(const TfheMi355Context *c, size_t count) {
+    if (!is_large(c) || count == 0) return 0;
+    const size_t per_ct = large_pbs_scratch_per_ct((int)c->N(), (int)c->k(), (int)c->p.pbs_level);
+    return per_ct * std::min(count, large_chunk());
+}
+
+bool ks_use_mfma(const TfheMi355Context *c) {
+    static const bool disabled = env_flag("TFHE_MI355_KS_NO_MFMA");
+    return !disabled && ks_mfma_supported((int)c->big_dim(), (int)c->p.ks_level, (int)c->p.ks_base_log);
+}
+
+size_t ks_scratch_bytes(const TfheMi355Context *c, size_t count) {
+    if (!c->ksk_planes_ready && !ks_use_mfma(c)) return 0;
+    return count ? ks_mfma_scratch_bytes((int)c->big_dim(), (int)c->p.ks_level, (int)count) : 0;
+}
+
+size_t pks_scratch_bytes(const TfheMi355Context *c, size_t count) {
+    if (!c->pksk_planes_ready || count == 0) return 0;
+    return ks_mfma_scratch_bytes((int)c->big_dim(), (int)c->pks_level, (int)count);
+}
+
+// KS -> PBS: the small-LWE intermediate, then (reused in stream order) the KS digits or the PBS
+// chunk scratch
+size_t ks_pbs_scratch_bytes(const TfheMi355Context *c, size_t count) {
+    return align256(count * (c->n() + 1) * 8) + std::max(ks_scratch_bytes(c, count), pbs_scratch_bytes(c, count));
+}
+// PBS -> KS: the big-LWE intermediate, then the PBS or KS scratch
+size_t pbs_ks_scratch_bytes(const TfheMi355Context *c, size_t count) {
+    return align256(count * (c->big_dim() + 1) * 8) + std::max(ks_scratch_bytes(c, count), pbs_scratch_bytes(c, count));
+}
+
+void require_scratch(size_t have, size_t need) {
+    if (have < need) fail("device scratch too small: %zu bytes given, %zu needed (see the *_scratch queries)", have, need);
+}
+
+// ---- launchers ---------------------------------------------------------------------------------
+
 void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, const uint64_t *d_luts,
-                    size_t lut_count, const uint32_t *d_idx, size_t count, hipStream_t s, bool glwe_out = false) {
+                    size_t lut_count, const uint32_t *d_idx, size_t count, void *scratch, size_t scratch_bytes,
+                    hipStream_t s, bool glwe_out = false) {
     require_fbsk(c);
     if (lut_count == 0) fail("lut_count must be >= 1");
+    if (lut_count > 0xffffffffu) fail("lut_count too large");
     if (count > 0x7fffffff) fail("batch too large");
+    if (count == 0) return;
     if (c->p.grouping_factor) {
         MultiBitPbsLaunch a;
         a.lwe_in = d_in;
         a.lwe_out = d_out;
         a.luts = d_luts;
         a.lut_indexes = d_idx;
+        a.lut_count = (uint32_t)lut_count;
         a.fbsk = reinterpret_cast<const double2 *>(c->fbsk.ptr);
         a.W = c->tables.W;
         a.twist = c->tables.twist;
@@ -186,22 +290,18 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
               "launch multi-bit pbs");
         return;
     }
-    if (large_pbs_supported((int)c->N(), (int)c->k(), (int)c->p.pbs_level)) {
+    if (is_large(c)) {
         if (glwe_out) fail("blind rotation without sample extraction is not available at N = %zu", c->N());
-        // ciphertexts per pass: the chunk's accumulators + spectra (1.5 MiB per ciphertext at 4_4)
-        // should stay resident in the 256 MiB Infinity Cache across the three launches of a CMUX
-        static const size_t kChunk = [] {
-            const char *e = std::getenv("TFHE_MI355_LARGE_CHUNK");
-            const long v = e ? std::atol(e) : 0;
-            return v > 0 ? (size_t)v : (size_t)128;  // 128: best of 64..1024 at 4_4 (profiles)
-        }();
         const size_t per_ct = large_pbs_scratch_per_ct((int)c->N(), (int)c->k(), (int)c->p.pbs_level);
-        c->pbs_scratch.reserve(per_ct * std::max<size_t>(1, std::min(count, kChunk)));
+        if (!scratch || scratch_bytes < per_ct)
+            fail("N = %zu PBS needs >= %zu bytes of device scratch per chunk ciphertext (%zu given)", c->N(), per_ct,
+                 scratch_bytes);
         LargePbsLaunch a{};
         a.lwe_in = d_in;
         a.lwe_out = d_out;
         a.luts = d_luts;
         a.lut_indexes = d_idx;
+        a.lut_count = (uint32_t)lut_count;
         a.fbsk = reinterpret_cast<const double2 *>(c->fbsk.ptr);
         a.W = c->tables.W;
         a.twist = c->tables.twist;
@@ -209,8 +309,8 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
         a.n = (int)c->n();
         a.base_log = (int)c->p.pbs_base_log;
         a.count = (int)count;
-        a.scratch = c->pbs_scratch.ptr;
-        a.scratch_bytes = c->pbs_scratch.bytes;
+        a.scratch = scratch;
+        a.scratch_bytes = std::min(scratch_bytes, per_ct * large_chunk());
         check(launch_large_pbs((int)c->N(), (int)c->k(), (int)c->p.pbs_level, a, s), "launch large pbs");
         return;
     }
@@ -219,6 +319,7 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
     a.lwe_out = d_out;
     a.luts = d_luts;
     a.lut_indexes = d_idx;
+    a.lut_count = (uint32_t)lut_count;
     a.fbsk = reinterpret_cast<const double2 *>(c->fbsk.ptr);
     a.W = c->tables.W;
     a.twist = c->tables.twist;
@@ -227,11 +328,6 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
     a.count = (int)count;
     a.glwe_out = glwe_out;
     check(launch_classic_pbs((int)c->N(), (int)c->k(), (int)c->p.pbs_level, a, s), "launch pbs");
-}
-
-bool ks_use_mfma(TfheMi355Context *c) {
-    static const bool disabled = std::getenv("TFHE_MI355_KS_NO_MFMA") != nullptr;
-    return !disabled && ks_mfma_supported((int)c->big_dim(), (int)c->p.ks_level, (int)c->p.ks_base_log);
 }
 
 // KSK -> int8 byte planes (once per key, after the u64 KSK is on the device)
@@ -246,22 +342,11 @@ void repack_ksk(TfheMi355Context *c, hipStream_t s) {
     c->ksk_planes_ready = true;
 }
 
-void launch_ks_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, size_t count, hipStream_t s) {
+void launch_ks_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, size_t count, void *scratch,
+                   size_t scratch_bytes, hipStream_t s) {
     require_ksk(c);
-    if (c->ksk_planes_ready && count > 0) {
-        KeyswitchLaunch a;
-        a.lwe_in = d_in;
-        a.lwe_out = d_out;
-        a.ksk = reinterpret_cast<const uint64_t *>(c->ksk.ptr);
-        a.in_dim = (int)c->big_dim();
-        a.out_dim = (int)c->n();
-        a.base_log = (int)c->p.ks_base_log;
-        a.level = (int)c->p.ks_level;
-        a.count = (int)count;
-        c->ks_scratch.reserve(ks_mfma_scratch_bytes(a.in_dim, a.level, a.count));
-        check(launch_keyswitch_mfma(a, (const int8_t *)c->ksk_planes.ptr, c->ks_scratch.ptr, s), "launch mfma keyswitch");
-        return;
-    }
+    if (count == 0) return;
+    if (count > 0x7fffffffu) fail("count too large");
     KeyswitchLaunch a;
     a.lwe_in = d_in;
     a.lwe_out = d_out;
@@ -271,6 +356,11 @@ void launch_ks_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, s
     a.base_log = (int)c->p.ks_base_log;
     a.level = (int)c->p.ks_level;
     a.count = (int)count;
+    if (c->ksk_planes_ready) {
+        require_scratch(scratch ? scratch_bytes : 0, ks_scratch_bytes(c, count));
+        check(launch_keyswitch_mfma(a, (const int8_t *)c->ksk_planes.ptr, scratch, s), "launch mfma keyswitch");
+        return;
+    }
     check(launch_keyswitch(a, s), "launch keyswitch");
 }
 
@@ -290,18 +380,49 @@ KeyswitchLaunch packing_ks_args(TfheMi355Context *c, const uint64_t *d_in, uint6
     return a;
 }
 
-void launch_packing_ks_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, size_t count, hipStream_t s) {
+void launch_packing_ks_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, size_t count, void *scratch,
+                           size_t scratch_bytes, hipStream_t s) {
     if (!c->pksk_ready) fail("packing keyswitching key not uploaded");
     if (count == 0) return;
     if (count > 0x7fffffffu) fail("count too large");
     KeyswitchLaunch a = packing_ks_args(c, d_in, d_out, count);
     if (c->pksk_planes_ready) {
-        c->ks_scratch.reserve(ks_mfma_scratch_bytes(a.in_dim, a.level, a.count));
-        check(launch_keyswitch_mfma(a, (const int8_t *)c->pksk_planes.ptr, c->ks_scratch.ptr, s),
+        require_scratch(scratch ? scratch_bytes : 0, pks_scratch_bytes(c, count));
+        check(launch_keyswitch_mfma(a, (const int8_t *)c->pksk_planes.ptr, scratch, s),
               "launch mfma packing keyswitch");
     } else {
         check(launch_keyswitch(a, s), "launch packing keyswitch");
     }
+}
+
+// shortint KS -> PBS on device: scratch = [small LWE intermediate | KS digits or PBS chunk scratch]
+void launch_ks_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, const uint64_t *d_luts,
+                       size_t lut_count, const uint32_t *d_idx, size_t count, void *scratch, size_t scratch_bytes,
+                       hipStream_t s) {
+    require_fbsk(c);
+    require_ksk(c);
+    if (count == 0) return;
+    require_scratch(scratch ? scratch_bytes : 0, ks_pbs_scratch_bytes(c, count));
+    const size_t head = align256(count * (c->n() + 1) * 8);
+    uint64_t *small = reinterpret_cast<uint64_t *>(scratch);
+    void *rest = reinterpret_cast<char *>(scratch) + head;
+    launch_ks_dev(c, d_in, small, count, rest, scratch_bytes - head, s);
+    launch_pbs_dev(c, small, d_out, d_luts, lut_count, d_idx, count, rest, scratch_bytes - head, s);
+}
+
+// shortint PBS -> KS on device: scratch = [big LWE intermediate | PBS or KS scratch]
+void launch_pbs_ks_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, const uint64_t *d_luts,
+                       size_t lut_count, const uint32_t *d_idx, size_t count, void *scratch, size_t scratch_bytes,
+                       hipStream_t s) {
+    require_fbsk(c);
+    require_ksk(c);
+    if (count == 0) return;
+    require_scratch(scratch ? scratch_bytes : 0, pbs_ks_scratch_bytes(c, count));
+    const size_t head = align256(count * (c->big_dim() + 1) * 8);
+    uint64_t *big = reinterpret_cast<uint64_t *>(scratch);
+    void *rest = reinterpret_cast<char *>(scratch) + head;
+    launch_pbs_dev(c, d_in, big, d_luts, lut_count, d_idx, count, rest, scratch_bytes - head, s);
+    launch_ks_dev(c, big, d_out, count, rest, scratch_bytes - head, s);
 }
 
 void launch_glwe_poly_mul_dev(TfheMi355Context *c, const uint64_t *d_glwe, size_t glwe_per_item,
@@ -328,6 +449,119 @@ void validate_lut_indexes(const uint32_t *idx, size_t count, size_t lut_count) {
         if (idx[i] >= lut_count) fail("lut_indexes[%zu] = %u out of range (lut_count %zu)", i, idx[i], lut_count);
 }
 
+// ---- host-pointer pipeline ------------------------------------------------------------------------
+// The synchronous entry points (host buffers in and out, the form the Rust binding calls) run as a
+// two-lane pipeline over chunks of the batch: per chunk, the host input slice is copied into the
+// lane's page-locked buffer, DMA'd to the device, processed and DMA'd back on the lane's stream,
+// and its output is copied to the caller's buffer while the other lane's chunk runs on the GPU.
+// The LUTs go up once per call.  Callers are serialised by ctx->mu.
+
+using ChunkLaunch = void (*)(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, const uint64_t *d_luts,
+                             size_t lut_count, const uint32_t *d_idx, size_t count, void *scratch,
+                             size_t scratch_bytes, hipStream_t s);
+using ScratchSize = size_t (*)(const TfheMi355Context *c, size_t count);
+
+size_t host_chunk(const TfheMi355Context *c, size_t out_words) {
+    static const size_t forced = [] {
+        const char *e = std::getenv("TFHE_MI355_HOST_CHUNK");
+        const long x = e ? std::atol(e) : 0;
+        return x > 0 ? (size_t)x : (size_t)0;
+    }();
+    if (forced) return forced;
+    // >= one full wave of PBS slots (256 CUs x 4 ciphertexts), else ~16 MiB of output per chunk
+    const size_t min_chunk = is_large(c) ? large_chunk() : 1024;
+    return std::max(min_chunk, ((size_t)16 << 20) / (out_words * 8));
+}
+
+void lane_finish(TfheMi355Context::Lane &L, void *out, size_t out_words) {
+    if (!L.pending) return;
+    L.pending = false;
+    check(hipEventSynchronize(L.done), "chunk sync");
+    std::memcpy(static_cast<uint64_t *>(out) + L.first * out_words, L.h_out.ptr, L.count * out_words * 8);
+}
+
+void run_host_pipeline(TfheMi355Context *c, const uint64_t *in, size_t in_words, uint64_t *out, size_t out_words,
+                       const uint64_t *luts, size_t lut_words, size_t lut_count, const uint32_t *idx, size_t count,
+                       ChunkLaunch launch, ScratchSize scratch_size) {
+    if (count == 0) return;
+    const uint64_t *d_luts = nullptr;
+    if (luts) {
+        c->io_luts.reserve(lut_count * lut_words * 8);
+        check(hipMemcpyAsync(c->io_luts.ptr, luts, lut_count * lut_words * 8, hipMemcpyHostToDevice, c->stream),
+              "H2D luts");
+        check(hipEventRecord(c->luts_ready, c->stream), "luts event");
+        d_luts = (const uint64_t *)c->io_luts.ptr;
+    }
+    const size_t chunk = std::min(count, host_chunk(c, out_words));
+    const size_t need_scratch = scratch_size ? scratch_size(c, chunk) : 0;
+    try {
+        size_t next = 0;
+        for (int q = 0; next < count; q ^= 1) {
+            TfheMi355Context::Lane &L = c->lanes[q];
+            lane_finish(L, out, out_words);
+            const size_t cnt = std::min(chunk, count - next);
+            L.h_in.reserve(chunk * in_words * 8);
+            L.h_out.reserve(chunk * out_words * 8);
+            L.d_in.reserve(chunk * in_words * 8);
+            L.d_out.reserve(chunk * out_words * 8);
+            if (need_scratch) L.scratch.reserve(need_scratch);
+            std::memcpy(L.h_in.ptr, in + next * in_words, cnt * in_words * 8);
+            check(hipMemcpyAsync(L.d_in.ptr, L.h_in.ptr, cnt * in_words * 8, hipMemcpyHostToDevice, L.stream),
+                  "H2D in");
+            const uint32_t *d_idx = nullptr;
+            if (idx) {
+                L.h_idx.reserve(chunk * 4);
+                L.d_idx.reserve(chunk * 4);
+                std::memcpy(L.h_idx.ptr, idx + next, cnt * 4);
+                check(hipMemcpyAsync(L.d_idx.ptr, L.h_idx.ptr, cnt * 4, hipMemcpyHostToDevice, L.stream), "H2D idx");
+                d_idx = (const uint32_t *)L.d_idx.ptr;
+            }
+            if (luts) check(hipStreamWaitEvent(L.stream, c->luts_ready, 0), "wait luts");
+            launch(c, (const uint64_t *)L.d_in.ptr, (uint64_t *)L.d_out.ptr, d_luts, lut_count, d_idx, cnt,
+                   L.scratch.ptr, L.scratch.bytes, L.stream);
+            check(hipMemcpyAsync(L.h_out.ptr, L.d_out.ptr, cnt * out_words * 8, hipMemcpyDeviceToHost, L.stream),
+                  "D2H out");
+            check(hipEventRecord(L.done, L.stream), "chunk event");
+            L.pending = true;
+            L.first = next;
+            L.count = cnt;
+            next += cnt;
+        }
+        // retire in chunk order: the lane holding the older chunk first
+        TfheMi355Context::Lane &a = c->lanes[0], &b = c->lanes[1];
+        if (a.pending && b.pending && b.first < a.first) {
+            lane_finish(b, out, out_words);
+            lane_finish(a, out, out_words);
+        } else {
+            lane_finish(a, out, out_words);
+            lane_finish(b, out, out_words);
+        }
+    } catch (...) {
+        for (auto &L : c->lanes) {
+            (void)hipStreamSynchronize(L.stream);
+            L.pending = false;
+        }
+        throw;
+    }
+}
+
+// adapters of the launchers to ChunkLaunch
+void chunk_pbs(TfheMi355Context *c, const uint64_t *i, uint64_t *o, const uint64_t *l, size_t lc, const uint32_t *x,
+               size_t n, void *sc, size_t sb, hipStream_t s) {
+    launch_pbs_dev(c, i, o, l, lc, x, n, sc, sb, s);
+}
+void chunk_blind_rotate(TfheMi355Context *c, const uint64_t *i, uint64_t *o, const uint64_t *l, size_t lc,
+                        const uint32_t *x, size_t n, void *sc, size_t sb, hipStream_t s) {
+    launch_pbs_dev(c, i, o, l, lc, x, n, sc, sb, s, true);
+}
+void chunk_ks(TfheMi355Context *c, const uint64_t *i, uint64_t *o, const uint64_t *, size_t, const uint32_t *,
+              size_t n, void *sc, size_t sb, hipStream_t s) {
+    launch_ks_dev(c, i, o, n, sc, sb, s);
+}
+void chunk_pks(TfheMi355Context *c, const uint64_t *i, uint64_t *o, const uint64_t *, size_t, const uint32_t *,
+               size_t n, void *sc, size_t sb, hipStream_t s) {
+    launch_packing_ks_dev(c, i, o, n, sc, sb, s);
+}
 }  // namespace
 
 extern "C" {
@@ -372,6 +606,11 @@ int tfhe_mi355_context_create(const TfheMi355Parameters *params, int device, Tfh
         c->device = device;
         try {
             check(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+            for (auto &L : c->lanes) {
+                check(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking), "hipStreamCreate(lane)");
+                check(hipEventCreateWithFlags(&L.done, hipEventDisableTiming), "hipEventCreate(lane)");
+            }
+            check(hipEventCreateWithFlags(&c->luts_ready, hipEventDisableTiming), "hipEventCreate(luts)");
             build_tables(c);
         } catch (...) {
             tfhe_mi355_context_destroy(c);
@@ -386,15 +625,18 @@ int tfhe_mi355_context_destroy(TfheMi355Context *ctx) {
         if (!ctx) return;
         (void)hipSetDevice(ctx->device);
         if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-        for (DeviceBuffer *b : {&ctx->fbsk, &ctx->ksk, &ctx->std_staging, &ctx->io_in, &ctx->io_out,
-                                &ctx->io_luts, &ctx->io_idx, &ctx->io_tmp, &ctx->pbs_scratch,
-                                &ctx->ksk_planes, &ctx->ks_scratch, &ctx->pksk, &ctx->pksk_planes})
-            b->release();
+        for (auto &L : ctx->lanes)
+            if (L.stream) (void)hipStreamSynchronize(L.stream);
         if (ctx->tables.W) (void)hipFree(ctx->tables.W);
         if (ctx->tables.twist) (void)hipFree(ctx->tables.twist);
         if (ctx->tables.wtop) (void)hipFree(ctx->tables.wtop);
+        for (auto &L : ctx->lanes) {
+            if (L.done) (void)hipEventDestroy(L.done);
+            if (L.stream) (void)hipStreamDestroy(L.stream);
+        }
+        if (ctx->luts_ready) (void)hipEventDestroy(ctx->luts_ready);
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-        delete ctx;
+        delete ctx;  // device and pinned buffers free themselves
     });
 }
 
@@ -492,10 +734,11 @@ int tfhe_mi355_csprng_mask_words(TfheMi355Context *ctx, uint64_t seed_lo, uint64
         if (words == 0) return;
         DeviceBuffer tab;
         upload_aes_tables(ctx, seed_lo, seed_hi, tab);
-        ctx->io_out.reserve(words * sizeof(uint64_t));
-        check(launch_seeded_decompress(tab.ptr, nullptr, 1, words, 0, (uint64_t *)ctx->io_out.ptr, ctx->stream),
+        DeviceBuffer d_words;
+        d_words.reserve(words * sizeof(uint64_t));
+        check(launch_seeded_decompress(tab.ptr, nullptr, 1, words, 0, (uint64_t *)d_words.ptr, ctx->stream),
               "csprng");
-        check(hipMemcpyAsync(out, ctx->io_out.ptr, words * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream),
+        check(hipMemcpyAsync(out, d_words.ptr, words * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream),
               "D2H words");
         check(hipStreamSynchronize(ctx->stream), "csprng sync");
         tab.release();
@@ -509,8 +752,12 @@ int tfhe_mi355_bootstrap_key_convert_async(TfheMi355Context *ctx, const uint64_t
         std::lock_guard<std::mutex> g(ctx->mu);
         check(hipSetDevice(ctx->device), "hipSetDevice");
         if (len != ctx->std_bsk_len()) fail("bootstrapping key has %zu words, expected %zu", len, ctx->std_bsk_len());
+        ctx->fbsk_ready = false;
         ctx->fbsk.reserve(ctx->fourier_bsk_bytes());
         check(convert_bsk(ctx, d_bsk, len / ctx->N(), (hipStream_t)stream), "bsk conversion");
+        // the key counts as ready only once the conversion has run: every later call (on any
+        // stream, including ctx->stream, which is not ordered after the caller's) sees it whole
+        check(hipStreamSynchronize((hipStream_t)stream), "bsk conversion sync");
         ctx->fbsk_ready = true;
     });
 }
@@ -531,6 +778,7 @@ int tfhe_mi355_bootstrap_key_fourier(TfheMi355Context *ctx, void **d_ptr, size_t
 int tfhe_mi355_bootstrap_key_fourier_set_ready(TfheMi355Context *ctx) {
     return guarded([&] {
         if (!ctx) fail("null ctx");
+        std::lock_guard<std::mutex> g(ctx->mu);
         if (!ctx->fbsk.ptr) fail("no Fourier key buffer");
         ctx->fbsk_ready = true;
     });
@@ -558,9 +806,11 @@ int tfhe_mi355_keyswitch_key_upload_async(TfheMi355Context *ctx, const uint64_t 
         check(hipSetDevice(ctx->device), "hipSetDevice");
         if (len != ctx->ksk_len()) fail("keyswitching key has %zu words, expected %zu", len, ctx->ksk_len());
         ctx->ksk.reserve(len * sizeof(uint64_t));
+        ctx->ksk_ready = false;
         check(hipMemcpyAsync(ctx->ksk.ptr, d_ksk, len * sizeof(uint64_t), hipMemcpyDeviceToDevice,
                              (hipStream_t)stream), "copy ksk");
         repack_ksk(ctx, (hipStream_t)stream);
+        check(hipStreamSynchronize((hipStream_t)stream), "ksk upload sync");  // see bootstrap_key_convert_async
         ctx->ksk_ready = true;
     });
 }
@@ -581,6 +831,7 @@ int tfhe_mi355_keyswitch_key_device(TfheMi355Context *ctx, void **d_ptr, size_t 
 int tfhe_mi355_keyswitch_key_set_ready(TfheMi355Context *ctx) {
     return guarded([&] {
         if (!ctx) fail("null ctx");
+        std::lock_guard<std::mutex> g(ctx->mu);
         if (!ctx->ksk.ptr) fail("no keyswitching key buffer");
         check(hipSetDevice(ctx->device), "hipSetDevice");
         repack_ksk(ctx, ctx->stream);
@@ -597,34 +848,28 @@ int tfhe_mi355_programmable_bootstrap(TfheMi355Context *ctx, const uint64_t *lwe
         std::lock_guard<std::mutex> g(ctx->mu);
         check(hipSetDevice(ctx->device), "hipSetDevice");
         require_fbsk(ctx);
-        if (count == 0) return;
+        if (lut_count == 0) fail("lut_count must be >= 1");
         validate_lut_indexes(lut_indexes, count, lut_count);
-        const size_t in_b = count * (ctx->n() + 1) * 8, out_b = count * (ctx->big_dim() + 1) * 8;
-        const size_t lut_b = lut_count * ctx->glwe_len() * 8;
-        ctx->io_in.reserve(in_b);
-        ctx->io_out.reserve(out_b);
-        ctx->io_luts.reserve(lut_b);
-        if (lut_indexes) ctx->io_idx.reserve(count * 4);
-        hipStream_t s = ctx->stream;
-        check(hipMemcpyAsync(ctx->io_in.ptr, lwe_in, in_b, hipMemcpyHostToDevice, s), "H2D in");
-        check(hipMemcpyAsync(ctx->io_luts.ptr, luts, lut_b, hipMemcpyHostToDevice, s), "H2D luts");
-        if (lut_indexes)
-            check(hipMemcpyAsync(ctx->io_idx.ptr, lut_indexes, count * 4, hipMemcpyHostToDevice, s), "H2D idx");
-        launch_pbs_dev(ctx, (const uint64_t *)ctx->io_in.ptr, (uint64_t *)ctx->io_out.ptr,
-                       (const uint64_t *)ctx->io_luts.ptr, lut_count,
-                       lut_indexes ? (const uint32_t *)ctx->io_idx.ptr : nullptr, count, s);
-        check(hipMemcpyAsync(lwe_out, ctx->io_out.ptr, out_b, hipMemcpyDeviceToHost, s), "D2H out");
-        check(hipStreamSynchronize(s), "pbs sync");
+        run_host_pipeline(ctx, lwe_in, ctx->n() + 1, lwe_out, ctx->big_dim() + 1, luts, ctx->glwe_len(), lut_count,
+                          lut_indexes, count, chunk_pbs, pbs_scratch_bytes);
+    });
+}
+
+int tfhe_mi355_programmable_bootstrap_scratch(TfheMi355Context *ctx, size_t count, size_t *bytes) {
+    return guarded([&] {
+        if (!ctx || !bytes) fail("null argument");
+        *bytes = pbs_scratch_bytes(ctx, count);
     });
 }
 
 int tfhe_mi355_programmable_bootstrap_async(TfheMi355Context *ctx, const uint64_t *d_in, uint64_t *d_out,
-                                            const uint64_t *d_luts, size_t lut_count,
-                                            const uint32_t *d_idx, size_t count, void *stream) {
+                                            const uint64_t *d_luts, size_t lut_count, const uint32_t *d_idx,
+                                            size_t count, void *d_scratch, size_t scratch_bytes, void *stream) {
     return guarded([&] {
         if (!ctx || (!d_in && count) || (!d_out && count) || !d_luts) fail("null argument");
         check(hipSetDevice(ctx->device), "hipSetDevice");
-        launch_pbs_dev(ctx, d_in, d_out, d_luts, lut_count, d_idx, count, (hipStream_t)stream);
+        launch_pbs_dev(ctx, d_in, d_out, d_luts, lut_count, d_idx, count, d_scratch, scratch_bytes,
+                       (hipStream_t)stream);
     });
 }
 
@@ -635,24 +880,11 @@ int tfhe_mi355_blind_rotate(TfheMi355Context *ctx, const uint64_t *lwe_in, uint6
         std::lock_guard<std::mutex> g(ctx->mu);
         check(hipSetDevice(ctx->device), "hipSetDevice");
         require_fbsk(ctx);
-        if (count == 0) return;
+        if (lut_count == 0) fail("lut_count must be >= 1");
+        if (is_large(ctx)) fail("blind rotation without sample extraction is not available at N = %zu", ctx->N());
         validate_lut_indexes(lut_indexes, count, lut_count);
-        const size_t in_b = count * (ctx->n() + 1) * 8, out_b = count * ctx->glwe_len() * 8;
-        const size_t lut_b = lut_count * ctx->glwe_len() * 8;
-        ctx->io_in.reserve(in_b);
-        ctx->io_out.reserve(out_b);
-        ctx->io_luts.reserve(lut_b);
-        if (lut_indexes) ctx->io_idx.reserve(count * 4);
-        hipStream_t s = ctx->stream;
-        check(hipMemcpyAsync(ctx->io_in.ptr, lwe_in, in_b, hipMemcpyHostToDevice, s), "H2D in");
-        check(hipMemcpyAsync(ctx->io_luts.ptr, luts, lut_b, hipMemcpyHostToDevice, s), "H2D luts");
-        if (lut_indexes)
-            check(hipMemcpyAsync(ctx->io_idx.ptr, lut_indexes, count * 4, hipMemcpyHostToDevice, s), "H2D idx");
-        launch_pbs_dev(ctx, (const uint64_t *)ctx->io_in.ptr, (uint64_t *)ctx->io_out.ptr,
-                       (const uint64_t *)ctx->io_luts.ptr, lut_count,
-                       lut_indexes ? (const uint32_t *)ctx->io_idx.ptr : nullptr, count, s, true);
-        check(hipMemcpyAsync(glwe_out, ctx->io_out.ptr, out_b, hipMemcpyDeviceToHost, s), "D2H out");
-        check(hipStreamSynchronize(s), "blind rotate sync");
+        run_host_pipeline(ctx, lwe_in, ctx->n() + 1, glwe_out, ctx->glwe_len(), luts, ctx->glwe_len(), lut_count,
+                          lut_indexes, count, chunk_blind_rotate, pbs_scratch_bytes);
     });
 }
 
@@ -662,7 +894,8 @@ int tfhe_mi355_blind_rotate_async(TfheMi355Context *ctx, const uint64_t *d_in, u
     return guarded([&] {
         if (!ctx || (!d_in && count) || (!d_glwe_out && count) || !d_luts) fail("null argument");
         check(hipSetDevice(ctx->device), "hipSetDevice");
-        launch_pbs_dev(ctx, d_in, d_glwe_out, d_luts, lut_count, d_lut_indexes, count, (hipStream_t)stream, true);
+        launch_pbs_dev(ctx, d_in, d_glwe_out, d_luts, lut_count, d_lut_indexes, count, nullptr, 0,
+                       (hipStream_t)stream, true);
     });
 }
 
@@ -681,8 +914,7 @@ int tfhe_mi355_packing_keyswitch_key_upload(TfheMi355Context *ctx, const uint64_
         ctx->pks_base_log = base_log;
         ctx->pks_level = level;
         const int in_dim = (int)ctx->big_dim(), out_dim = (int)ctx->glwe_len() - 1;
-        const char *no_mfma = std::getenv("TFHE_MI355_KS_NO_MFMA");
-        if (!(no_mfma && *no_mfma && *no_mfma != '0') && ks_mfma_supported(in_dim, (int)level, (int)base_log)) {
+        if (!env_flag("TFHE_MI355_KS_NO_MFMA") && ks_mfma_supported(in_dim, (int)level, (int)base_log)) {
             ctx->pksk_planes.reserve(8 * ks_mfma_rows(in_dim, (int)level) * ks_mfma_cols(out_dim));
             check(launch_ksk_repack((const uint64_t *)ctx->pksk.ptr, (int8_t *)ctx->pksk_planes.ptr, in_dim,
                                     (int)level, out_dim, ctx->stream),
@@ -700,24 +932,25 @@ int tfhe_mi355_packing_keyswitch(TfheMi355Context *ctx, const uint64_t *lwe_in, 
         std::lock_guard<std::mutex> g(ctx->mu);
         check(hipSetDevice(ctx->device), "hipSetDevice");
         if (!ctx->pksk_ready) fail("packing keyswitching key not uploaded");
-        if (count == 0) return;
-        const size_t in_b = count * (ctx->big_dim() + 1) * 8, out_b = count * ctx->glwe_len() * 8;
-        ctx->io_in.reserve(in_b);
-        ctx->io_out.reserve(out_b);
-        hipStream_t s = ctx->stream;
-        check(hipMemcpyAsync(ctx->io_in.ptr, lwe_in, in_b, hipMemcpyHostToDevice, s), "H2D in");
-        launch_packing_ks_dev(ctx, (const uint64_t *)ctx->io_in.ptr, (uint64_t *)ctx->io_out.ptr, count, s);
-        check(hipMemcpyAsync(glwe_out, ctx->io_out.ptr, out_b, hipMemcpyDeviceToHost, s), "D2H out");
-        check(hipStreamSynchronize(s), "packing ks sync");
+        run_host_pipeline(ctx, lwe_in, ctx->big_dim() + 1, glwe_out, ctx->glwe_len(), nullptr, 0, 0, nullptr, count,
+                          chunk_pks, pks_scratch_bytes);
+    });
+}
+
+int tfhe_mi355_packing_keyswitch_scratch(TfheMi355Context *ctx, size_t count, size_t *bytes) {
+    return guarded([&] {
+        if (!ctx || !bytes) fail("null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        *bytes = pks_scratch_bytes(ctx, count);
     });
 }
 
 int tfhe_mi355_packing_keyswitch_async(TfheMi355Context *ctx, const uint64_t *d_lwe_in, uint64_t *d_glwe_out,
-                                       size_t count, void *stream) {
+                                       size_t count, void *d_scratch, size_t scratch_bytes, void *stream) {
     return guarded([&] {
         if (!ctx || (!d_lwe_in && count) || (!d_glwe_out && count)) fail("null argument");
         check(hipSetDevice(ctx->device), "hipSetDevice");
-        launch_packing_ks_dev(ctx, d_lwe_in, d_glwe_out, count, (hipStream_t)stream);
+        launch_packing_ks_dev(ctx, d_lwe_in, d_glwe_out, count, d_scratch, scratch_bytes, (hipStream_t)stream);
     });
 }
 
@@ -731,16 +964,16 @@ int tfhe_mi355_glwe_poly_mul(TfheMi355Context *ctx, const uint64_t *glwe_in, siz
         const size_t out_words = extract ? ctx->big_dim() + 1 : ctx->glwe_len();
         const size_t in_b = count * glwe_per_item * ctx->glwe_len() * 8;
         const size_t poly_b = npoly * glwe_per_item * ctx->N() * 8, out_b = count * npoly * out_words * 8;
-        ctx->io_in.reserve(in_b);
-        ctx->io_luts.reserve(poly_b);
-        ctx->io_out.reserve(out_b);
+        DeviceBuffer d_in, d_polys, d_out;
+        d_in.reserve(in_b);
+        d_polys.reserve(poly_b);
+        d_out.reserve(out_b);
         hipStream_t s = ctx->stream;
-        check(hipMemcpyAsync(ctx->io_in.ptr, glwe_in, in_b, hipMemcpyHostToDevice, s), "H2D glwe");
-        check(hipMemcpyAsync(ctx->io_luts.ptr, polys, poly_b, hipMemcpyHostToDevice, s), "H2D polys");
-        launch_glwe_poly_mul_dev(ctx, (const uint64_t *)ctx->io_in.ptr, glwe_per_item,
-                                 (const uint64_t *)ctx->io_luts.ptr, npoly, count, extract != 0,
-                                 (uint64_t *)ctx->io_out.ptr, s);
-        check(hipMemcpyAsync(out, ctx->io_out.ptr, out_b, hipMemcpyDeviceToHost, s), "D2H out");
+        check(hipMemcpyAsync(d_in.ptr, glwe_in, in_b, hipMemcpyHostToDevice, s), "H2D glwe");
+        check(hipMemcpyAsync(d_polys.ptr, polys, poly_b, hipMemcpyHostToDevice, s), "H2D polys");
+        launch_glwe_poly_mul_dev(ctx, (const uint64_t *)d_in.ptr, glwe_per_item, (const uint64_t *)d_polys.ptr, npoly,
+                                 count, extract != 0, (uint64_t *)d_out.ptr, s);
+        check(hipMemcpyAsync(out, d_out.ptr, out_b, hipMemcpyDeviceToHost, s), "D2H out");
         check(hipStreamSynchronize(s), "glwe poly mul sync");
     });
 }
@@ -764,45 +997,46 @@ int tfhe_mi355_keyswitch(TfheMi355Context *ctx, const uint64_t *lwe_in, uint64_t
         std::lock_guard<std::mutex> g(ctx->mu);
         check(hipSetDevice(ctx->device), "hipSetDevice");
         require_ksk(ctx);
-        if (count == 0) return;
-        const size_t in_b = count * (ctx->big_dim() + 1) * 8, out_b = count * (ctx->n() + 1) * 8;
-        ctx->io_in.reserve(in_b);
-        ctx->io_out.reserve(out_b);
-        hipStream_t s = ctx->stream;
-        check(hipMemcpyAsync(ctx->io_in.ptr, lwe_in, in_b, hipMemcpyHostToDevice, s), "H2D in");
-        launch_ks_dev(ctx, (const uint64_t *)ctx->io_in.ptr, (uint64_t *)ctx->io_out.ptr, count, s);
-        check(hipMemcpyAsync(lwe_out, ctx->io_out.ptr, out_b, hipMemcpyDeviceToHost, s), "D2H out");
-        check(hipStreamSynchronize(s), "ks sync");
+        run_host_pipeline(ctx, lwe_in, ctx->big_dim() + 1, lwe_out, ctx->n() + 1, nullptr, 0, 0, nullptr, count,
+                          chunk_ks, ks_scratch_bytes);
+    });
+}
+
+int tfhe_mi355_keyswitch_scratch(TfheMi355Context *ctx, size_t count, size_t *bytes) {
+    return guarded([&] {
+        if (!ctx || !bytes) fail("null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        *bytes = ks_scratch_bytes(ctx, count);
     });
 }
 
 int tfhe_mi355_keyswitch_async(TfheMi355Context *ctx, const uint64_t *d_in, uint64_t *d_out, size_t count,
-                               void *stream) {
+                               void *d_scratch, size_t scratch_bytes, void *stream) {
     return guarded([&] {
         if (!ctx || (!d_in && count) || (!d_out && count)) fail("null argument");
         check(hipSetDevice(ctx->device), "hipSetDevice");
-        launch_ks_dev(ctx, d_in, d_out, count, (hipStream_t)stream);
+        launch_ks_dev(ctx, d_in, d_out, count, d_scratch, scratch_bytes, (hipStream_t)stream);
     });
 }
 
 int tfhe_mi355_keyswitch_programmable_bootstrap_scratch(TfheMi355Context *ctx, size_t count, size_t *bytes) {
     return guarded([&] {
         if (!ctx || !bytes) fail("null argument");
-        *bytes = count * (ctx->n() + 1) * 8;
+        std::lock_guard<std::mutex> g(ctx->mu);
+        *bytes = ks_pbs_scratch_bytes(ctx, count);
     });
 }
 
 int tfhe_mi355_keyswitch_programmable_bootstrap_async(TfheMi355Context *ctx, const uint64_t *d_in,
                                                       uint64_t *d_out, const uint64_t *d_luts, size_t lut_count,
                                                       const uint32_t *d_idx, size_t count, void *d_scratch,
-                                                      void *stream) {
+                                                      size_t scratch_bytes, void *stream) {
     return guarded([&] {
         if (!ctx || (!d_in && count) || (!d_out && count) || !d_luts || (!d_scratch && count))
             fail("null argument");
         check(hipSetDevice(ctx->device), "hipSetDevice");
-        launch_ks_dev(ctx, d_in, (uint64_t *)d_scratch, count, (hipStream_t)stream);
-        launch_pbs_dev(ctx, (const uint64_t *)d_scratch, d_out, d_luts, lut_count, d_idx, count,
-                       (hipStream_t)stream);
+        launch_ks_pbs_dev(ctx, d_in, d_out, d_luts, lut_count, d_idx, count, d_scratch, scratch_bytes,
+                          (hipStream_t)stream);
     });
 }
 
@@ -815,26 +1049,31 @@ int tfhe_mi355_keyswitch_programmable_bootstrap(TfheMi355Context *ctx, const uin
         check(hipSetDevice(ctx->device), "hipSetDevice");
         require_fbsk(ctx);
         require_ksk(ctx);
-        if (count == 0) return;
+        if (lut_count == 0) fail("lut_count must be >= 1");
         validate_lut_indexes(lut_indexes, count, lut_count);
-        const size_t big_b = count * (ctx->big_dim() + 1) * 8, small_b = count * (ctx->n() + 1) * 8;
-        const size_t lut_b = lut_count * ctx->glwe_len() * 8;
-        ctx->io_in.reserve(big_b);
-        ctx->io_out.reserve(big_b);
-        ctx->io_tmp.reserve(small_b);
-        ctx->io_luts.reserve(lut_b);
-        if (lut_indexes) ctx->io_idx.reserve(count * 4);
-        hipStream_t s = ctx->stream;
-        check(hipMemcpyAsync(ctx->io_in.ptr, lwe_in, big_b, hipMemcpyHostToDevice, s), "H2D in");
-        check(hipMemcpyAsync(ctx->io_luts.ptr, luts, lut_b, hipMemcpyHostToDevice, s), "H2D luts");
-        if (lut_indexes)
-            check(hipMemcpyAsync(ctx->io_idx.ptr, lut_indexes, count * 4, hipMemcpyHostToDevice, s), "H2D idx");
-        launch_ks_dev(ctx, (const uint64_t *)ctx->io_in.ptr, (uint64_t *)ctx->io_tmp.ptr, count, s);
-        launch_pbs_dev(ctx, (const uint64_t *)ctx->io_tmp.ptr, (uint64_t *)ctx->io_out.ptr,
-                       (const uint64_t *)ctx->io_luts.ptr, lut_count,
-                       lut_indexes ? (const uint32_t *)ctx->io_idx.ptr : nullptr, count, s);
-        check(hipMemcpyAsync(lwe_out, ctx->io_out.ptr, big_b, hipMemcpyDeviceToHost, s), "D2H out");
-        check(hipStreamSynchronize(s), "ks-pbs sync");
+        run_host_pipeline(ctx, lwe_in, ctx->big_dim() + 1, lwe_out, ctx->big_dim() + 1, luts, ctx->glwe_len(),
+                          lut_count, lut_indexes, count, launch_ks_pbs_dev, ks_pbs_scratch_bytes);
+    });
+}
+
+int tfhe_mi355_programmable_bootstrap_keyswitch_scratch(TfheMi355Context *ctx, size_t count, size_t *bytes) {
+    return guarded([&] {
+        if (!ctx || !bytes) fail("null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        *bytes = pbs_ks_scratch_bytes(ctx, count);
+    });
+}
+
+int tfhe_mi355_programmable_bootstrap_keyswitch_async(TfheMi355Context *ctx, const uint64_t *d_in,
+                                                      uint64_t *d_out, const uint64_t *d_luts, size_t lut_count,
+                                                      const uint32_t *d_idx, size_t count, void *d_scratch,
+                                                      size_t scratch_bytes, void *stream) {
+    return guarded([&] {
+        if (!ctx || (!d_in && count) || (!d_out && count) || !d_luts || (!d_scratch && count))
+            fail("null argument");
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        launch_pbs_ks_dev(ctx, d_in, d_out, d_luts, lut_count, d_idx, count, d_scratch, scratch_bytes,
+                          (hipStream_t)stream);
     });
 }
 
@@ -847,26 +1086,10 @@ int tfhe_mi355_programmable_bootstrap_keyswitch(TfheMi355Context *ctx, const uin
         check(hipSetDevice(ctx->device), "hipSetDevice");
         require_fbsk(ctx);
         require_ksk(ctx);
-        if (count == 0) return;
+        if (lut_count == 0) fail("lut_count must be >= 1");
         validate_lut_indexes(lut_indexes, count, lut_count);
-        const size_t big_b = count * (ctx->big_dim() + 1) * 8, small_b = count * (ctx->n() + 1) * 8;
-        const size_t lut_b = lut_count * ctx->glwe_len() * 8;
-        ctx->io_in.reserve(small_b);
-        ctx->io_out.reserve(small_b);
-        ctx->io_tmp.reserve(big_b);
-        ctx->io_luts.reserve(lut_b);
-        if (lut_indexes) ctx->io_idx.reserve(count * 4);
-        hipStream_t s = ctx->stream;
-        check(hipMemcpyAsync(ctx->io_in.ptr, lwe_in, small_b, hipMemcpyHostToDevice, s), "H2D in");
-        check(hipMemcpyAsync(ctx->io_luts.ptr, luts, lut_b, hipMemcpyHostToDevice, s), "H2D luts");
-        if (lut_indexes)
-            check(hipMemcpyAsync(ctx->io_idx.ptr, lut_indexes, count * 4, hipMemcpyHostToDevice, s), "H2D idx");
-        launch_pbs_dev(ctx, (const uint64_t *)ctx->io_in.ptr, (uint64_t *)ctx->io_tmp.ptr,
-                       (const uint64_t *)ctx->io_luts.ptr, lut_count,
-                       lut_indexes ? (const uint32_t *)ctx->io_idx.ptr : nullptr, count, s);
-        launch_ks_dev(ctx, (const uint64_t *)ctx->io_tmp.ptr, (uint64_t *)ctx->io_out.ptr, count, s);
-        check(hipMemcpyAsync(lwe_out, ctx->io_out.ptr, small_b, hipMemcpyDeviceToHost, s), "D2H out");
-        check(hipStreamSynchronize(s), "pbs-ks sync");
+        run_host_pipeline(ctx, lwe_in, ctx->n() + 1, lwe_out, ctx->n() + 1, luts, ctx->glwe_len(), lut_count,
+                          lut_indexes, count, launch_pbs_ks_dev, pbs_ks_scratch_bytes);
     });
 }
 

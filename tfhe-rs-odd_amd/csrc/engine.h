@@ -18,7 +18,8 @@ struct ClassicPbsLaunch {
     const uint64_t *lwe_in;      // [count][n+1]
     uint64_t *lwe_out;           // [count][k*N+1]
     const uint64_t *luts;        // [lut_count][(k+1)*N]
-    const uint32_t *lut_indexes; // [count] or null
+    const uint32_t *lut_indexes; // [count] or null; entries >= lut_count read LUT lut_count-1
+    uint32_t lut_count;
     const double2 *fbsk;         // engine Fourier layout
     const double2 *W, *twist;
     int n;
@@ -35,7 +36,8 @@ struct MultiBitPbsLaunch {
     const uint64_t *lwe_in;      // [count][n+1]
     uint64_t *lwe_out;           // [count][k*N+1]
     const uint64_t *luts;        // [lut_count][(k+1)*N]
-    const uint32_t *lut_indexes; // [count] or null
+    const uint32_t *lut_indexes; // [count] or null; entries >= lut_count read LUT lut_count-1
+    uint32_t lut_count;
     const double2 *fbsk;         // [n/g][2^g][L][k+1][k+1] polys, engine Fourier layout
     const double2 *W, *twist;
     int n;
@@ -51,7 +53,8 @@ struct LargePbsLaunch {
     const uint64_t *lwe_in;      // [count][n+1]
     uint64_t *lwe_out;           // [count][k*N+1]
     const uint64_t *luts;        // [lut_count][(k+1)*N]
-    const uint32_t *lut_indexes; // [count] or null
+    const uint32_t *lut_indexes; // [count] or null; entries >= lut_count read LUT lut_count-1
+    uint32_t lut_count;
     const double2 *fbsk;         // engine Fourier layout
     const double2 *W, *twist;
     const double2 *wtop;         // FftTables::wtop

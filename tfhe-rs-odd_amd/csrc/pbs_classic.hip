@@ -125,7 +125,7 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
     const __attribute__((address_space(4))) uint64_t *in_s = (const __attribute__((address_space(4))) uint64_t *)(
         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)in >> 32)) << 32) |
         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)in));
-    const uint32_t li = a.lut_indexes ? a.lut_indexes[ct] : 0u;
+    const uint32_t li = a.lut_indexes ? min(a.lut_indexes[ct], a.lut_count - 1u) : 0u;
     const uint64_t *lut = a.luts + (size_t)li * (K + 1) * N + (size_t)wave * N;
 
     // this wave's accumulator polynomial, in registers: c0[h] = position lane + 64 h

@@ -117,7 +117,7 @@ __global__ void __launch_bounds__(256) large_init_kernel(LargePbsLaunch a, int c
     const int ct = ct0 + cl;
     const uint64_t *in = a.lwe_in + (size_t)ct * (a.n + 1);
     const uint32_t bt = pbs_modulus_switch<15>(in[a.n]);
-    const uint32_t li = a.lut_indexes ? a.lut_indexes[ct] : 0u;
+    const uint32_t li = a.lut_indexes ? min(a.lut_indexes[ct], a.lut_count - 1u) : 0u;
     const uint64_t *lut = a.luts + (size_t)li * (K + 1) * LN + (size_t)p * LN;
     const int full = bt / LN, rem = bt % LN;
     const int src = j + rem;

@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
     cx *xb = xct + wave * XL;
     uint64_t *xb64 = reinterpret_cast<uint64_t *>(xb);
     const uint64_t *in = a.lwe_in + (size_t)ct * (n + 1);
-    const uint32_t li = a.lut_indexes ? a.lut_indexes[ct] : 0u;
+    const uint32_t li = a.lut_indexes ? min(a.lut_indexes[ct], a.lut_count - 1u) : 0u;
     const uint64_t *lut = a.luts + (size_t)li * (K + 1) * N + (size_t)wave * N;
 
     // acc = LUT / X^{b~}  (:635-650), position lane + 64 h

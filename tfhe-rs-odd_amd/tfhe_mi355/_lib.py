@@ -49,14 +49,19 @@ SIGNATURES = [
     ("tfhe_mi355_keyswitch_key_device", ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(sz)]),
     ("tfhe_mi355_keyswitch_key_set_ready", ctypes.c_int, [vp]),
     ("tfhe_mi355_programmable_bootstrap", ctypes.c_int, [vp, u64p, u64p, u64p, sz, u32p, sz]),
-    ("tfhe_mi355_programmable_bootstrap_async", ctypes.c_int, [vp, vp, vp, vp, sz, vp, sz, vp]),
+    ("tfhe_mi355_programmable_bootstrap_async", ctypes.c_int, [vp, vp, vp, vp, sz, vp, sz, vp, sz, vp]),
+    ("tfhe_mi355_programmable_bootstrap_scratch", ctypes.c_int, [vp, sz, ctypes.POINTER(sz)]),
     ("tfhe_mi355_keyswitch", ctypes.c_int, [vp, u64p, u64p, sz]),
-    ("tfhe_mi355_keyswitch_async", ctypes.c_int, [vp, vp, vp, sz, vp]),
+    ("tfhe_mi355_keyswitch_async", ctypes.c_int, [vp, vp, vp, sz, vp, sz, vp]),
+    ("tfhe_mi355_keyswitch_scratch", ctypes.c_int, [vp, sz, ctypes.POINTER(sz)]),
     ("tfhe_mi355_keyswitch_programmable_bootstrap", ctypes.c_int, [vp, u64p, u64p, u64p, sz, u32p, sz]),
     ("tfhe_mi355_keyswitch_programmable_bootstrap_async", ctypes.c_int,
-     [vp, vp, vp, vp, sz, vp, sz, vp, vp]),
+     [vp, vp, vp, vp, sz, vp, sz, vp, sz, vp]),
     ("tfhe_mi355_keyswitch_programmable_bootstrap_scratch", ctypes.c_int, [vp, sz, ctypes.POINTER(sz)]),
     ("tfhe_mi355_programmable_bootstrap_keyswitch", ctypes.c_int, [vp, u64p, u64p, u64p, sz, u32p, sz]),
+    ("tfhe_mi355_programmable_bootstrap_keyswitch_async", ctypes.c_int,
+     [vp, vp, vp, vp, sz, vp, sz, vp, sz, vp]),
+    ("tfhe_mi355_programmable_bootstrap_keyswitch_scratch", ctypes.c_int, [vp, sz, ctypes.POINTER(sz)]),
     ("tfhe_mi355_fill_accumulator", ctypes.c_int, [ctypes.POINTER(TfheMi355Parameters), u64p, u64p]),
     ("tfhe_mi355_client_gen_binary_key", ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, u64p, sz]),
     ("tfhe_mi355_client_gen_bootstrap_key", ctypes.c_int,
@@ -76,7 +81,8 @@ SIGNATURES = [
       ctypes.c_double, u64p]),
     ("tfhe_mi355_packing_keyswitch_key_upload", ctypes.c_int, [vp, u64p, sz, ctypes.c_uint32, ctypes.c_uint32]),
     ("tfhe_mi355_packing_keyswitch", ctypes.c_int, [vp, u64p, u64p, sz]),
-    ("tfhe_mi355_packing_keyswitch_async", ctypes.c_int, [vp, vp, vp, sz, vp]),
+    ("tfhe_mi355_packing_keyswitch_async", ctypes.c_int, [vp, vp, vp, sz, vp, sz, vp]),
+    ("tfhe_mi355_packing_keyswitch_scratch", ctypes.c_int, [vp, sz, ctypes.POINTER(sz)]),
     ("tfhe_mi355_glwe_poly_mul", ctypes.c_int, [vp, u64p, sz, u64p, sz, sz, ctypes.c_int, u64p]),
     ("tfhe_mi355_glwe_poly_mul_async", ctypes.c_int, [vp, vp, sz, vp, sz, sz, ctypes.c_int, vp, vp]),
     ("tfhe_mi355_client_gen_packing_keyswitch_key", ctypes.c_int,

@@ -231,20 +231,72 @@ class Engine:
         return out
 
     # -- device (torch) async ops -------------------------------------------------------
-    def programmable_bootstrap_async(self, d_in, d_out, d_luts, lut_count: int, count: int,
-                                     d_lut_indexes=None, stream=None) -> None:
-        _lib.call("tfhe_mi355_programmable_bootstrap_async", self._h, _dev_ptr(d_in), _dev_ptr(d_out),
-                  _dev_ptr(d_luts), lut_count, _dev_ptr(d_lut_indexes), count, _stream_ptr(stream))
+    # Every device scratch the C ABI needs comes from the caller (include/tfhe_mi355.h): pass
+    # d_scratch (>= the matching *_scratch_bytes), or let these wrappers allocate it from torch's
+    # caching allocator for the call.
+    def _scratch_query(self, fn: str, count: int) -> int:
+        b = ctypes.c_size_t()
+        _lib.call(fn, self._h, count, ctypes.byref(b))
+        return b.value
 
-    def keyswitch_async(self, d_in, d_out, count: int, stream=None) -> None:
-        _lib.call("tfhe_mi355_keyswitch_async", self._h, _dev_ptr(d_in), _dev_ptr(d_out), count,
+    def pbs_scratch_bytes(self, count: int) -> int:
+        return self._scratch_query("tfhe_mi355_programmable_bootstrap_scratch", count)
+
+    def ks_scratch_bytes(self, count: int) -> int:
+        return self._scratch_query("tfhe_mi355_keyswitch_scratch", count)
+
+    def pks_scratch_bytes(self, count: int) -> int:
+        return self._scratch_query("tfhe_mi355_packing_keyswitch_scratch", count)
+
+    def ks_pbs_scratch_bytes(self, count: int) -> int:
+        return self._scratch_query("tfhe_mi355_keyswitch_programmable_bootstrap_scratch", count)
+
+    def pbs_ks_scratch_bytes(self, count: int) -> int:
+        return self._scratch_query("tfhe_mi355_programmable_bootstrap_keyswitch_scratch", count)
+
+    def _scratch(self, d_scratch, need: int, stream):
+        """(pointer, bytes, keep-alive) of the scratch for one async call."""
+        if d_scratch is not None:
+            nbytes = d_scratch.numel() * d_scratch.element_size() if hasattr(d_scratch, "numel") else need
+            return _dev_ptr(d_scratch), nbytes, d_scratch
+        if need == 0:
+            return None, 0, None
+        import torch
+
+        t = torch.empty(need, dtype=torch.uint8, device=torch.device("cuda", self.device))
+        if stream is not None and not isinstance(stream, int) and stream != torch.cuda.current_stream():
+            t.record_stream(stream)
+        return t.data_ptr(), need, t
+
+    def programmable_bootstrap_async(self, d_in, d_out, d_luts, lut_count: int, count: int,
+                                     d_lut_indexes=None, stream=None, d_scratch=None) -> None:
+        sp, sb, _keep = self._scratch(d_scratch, self.pbs_scratch_bytes(count), stream)
+        _lib.call("tfhe_mi355_programmable_bootstrap_async", self._h, _dev_ptr(d_in), _dev_ptr(d_out),
+                  _dev_ptr(d_luts), lut_count, _dev_ptr(d_lut_indexes), count, sp, sb, _stream_ptr(stream))
+
+    def blind_rotate_async(self, d_in, d_glwe_out, d_luts, lut_count: int, count: int, d_lut_indexes=None,
+                           stream=None) -> None:
+        _lib.call("tfhe_mi355_blind_rotate_async", self._h, _dev_ptr(d_in), _dev_ptr(d_glwe_out), _dev_ptr(d_luts),
+                  lut_count, _dev_ptr(d_lut_indexes), count, _stream_ptr(stream))
+
+    def keyswitch_async(self, d_in, d_out, count: int, stream=None, d_scratch=None) -> None:
+        sp, sb, _keep = self._scratch(d_scratch, self.ks_scratch_bytes(count), stream)
+        _lib.call("tfhe_mi355_keyswitch_async", self._h, _dev_ptr(d_in), _dev_ptr(d_out), count, sp, sb,
                   _stream_ptr(stream))
 
     def keyswitch_programmable_bootstrap_async(self, d_in, d_out, d_luts, lut_count: int, count: int,
-                                               d_scratch, d_lut_indexes=None, stream=None) -> None:
+                                               d_scratch=None, d_lut_indexes=None, stream=None) -> None:
+        sp, sb, _keep = self._scratch(d_scratch, self.ks_pbs_scratch_bytes(count), stream)
         _lib.call("tfhe_mi355_keyswitch_programmable_bootstrap_async", self._h, _dev_ptr(d_in),
                   _dev_ptr(d_out), _dev_ptr(d_luts), lut_count, _dev_ptr(d_lut_indexes), count,
-                  _dev_ptr(d_scratch), _stream_ptr(stream))
+                  sp, sb, _stream_ptr(stream))
+
+    def programmable_bootstrap_keyswitch_async(self, d_in, d_out, d_luts, lut_count: int, count: int,
+                                               d_scratch=None, d_lut_indexes=None, stream=None) -> None:
+        sp, sb, _keep = self._scratch(d_scratch, self.pbs_ks_scratch_bytes(count), stream)
+        _lib.call("tfhe_mi355_programmable_bootstrap_keyswitch_async", self._h, _dev_ptr(d_in),
+                  _dev_ptr(d_out), _dev_ptr(d_luts), lut_count, _dev_ptr(d_lut_indexes), count,
+                  sp, sb, _stream_ptr(stream))
 
     def lwe_scalar_mul_add_async(self, y_ptr: int, x_ptr, scalar: int, rows: int, words: int, y_stride: int,
                                  x_stride: int = 0, stream=None) -> None:
@@ -256,19 +308,15 @@ class Engine:
         _lib.call("tfhe_mi355_trivial_pbs_async", self._h, body_ptr, rows, stride, _dev_ptr(d_lut),
                   _stream_ptr(stream))
 
-    def packing_keyswitch_async(self, d_in, d_out, count: int, stream=None) -> None:
-        _lib.call("tfhe_mi355_packing_keyswitch_async", self._h, _dev_ptr(d_in), _dev_ptr(d_out), count,
+    def packing_keyswitch_async(self, d_in, d_out, count: int, stream=None, d_scratch=None) -> None:
+        sp, sb, _keep = self._scratch(d_scratch, self.pks_scratch_bytes(count), stream)
+        _lib.call("tfhe_mi355_packing_keyswitch_async", self._h, _dev_ptr(d_in), _dev_ptr(d_out), count, sp, sb,
                   _stream_ptr(stream))
 
     def glwe_poly_mul_async(self, d_glwe, glwe_per_item: int, d_polys, npoly: int, count: int, extract: bool,
                             d_out, stream=None) -> None:
         _lib.call("tfhe_mi355_glwe_poly_mul_async", self._h, _dev_ptr(d_glwe), glwe_per_item, _dev_ptr(d_polys),
                   npoly, count, int(extract), _dev_ptr(d_out), _stream_ptr(stream))
-
-    def ks_pbs_scratch_bytes(self, count: int) -> int:
-        b = ctypes.c_size_t()
-        _lib.call("tfhe_mi355_keyswitch_programmable_bootstrap_scratch", self._h, count, ctypes.byref(b))
-        return b.value
 
 
 def fill_accumulator(params: ClassicPBSParameters, f) -> np.ndarray:
