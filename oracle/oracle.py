@@ -92,6 +92,10 @@ def lib():
                                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, u64p]
         L.orc_decompress_seeded_ksk.argtypes = [ctypes.c_uint64, ctypes.c_uint64, u64p, ctypes.c_size_t,
                                                 ctypes.c_int, ctypes.c_int, u64p]
+        L.orc_negacyclic_mul_add_exact.argtypes = [ctypes.c_int, u64p, u64p, u64p]
+        L.orc_exact_pbs_batch.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, u64p, u64p, u64p, u32p, ctypes.c_size_t, ctypes.c_int,
+                                          ctypes.c_int]
         if hasattr(L, "orc_mb_pbs_batch"):
             L.orc_mb_fbsk_create.restype = ctypes.c_void_p
             L.orc_mb_fbsk_create.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -160,6 +164,31 @@ def negacyclic_mul(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     a, b = _u64(a), _u64(b)
     out = np.zeros_like(a)
     lib().orc_negacyclic_mul_u64(len(a), _p(a), _p(b), _p(out))
+    return out
+
+
+def negacyclic_mul_add_exact(a: np.ndarray, b: np.ndarray, out: np.ndarray | None = None) -> np.ndarray:
+    """out + a * b in (Z/2^64)[X]/(X^N+1) by Karatsuba (the exact PBS's product)."""
+    a, b = _u64(a), _u64(b)
+    out = np.zeros_like(a) if out is None else _u64(out).copy()
+    lib().orc_negacyclic_mul_add_exact(len(a), _p(a), _p(b), _p(out))
+    return out
+
+
+def exact_pbs(bsk, n, k, N, base_log, level, cts, luts, lut_idx=None, threads=8, glwe_out=False) -> np.ndarray:
+    """FFT-free PBS (blind rotation + sample extraction, or the accumulators with glwe_out) with
+    exact negacyclic products over the STANDARD-domain BSK (pbs_oracle.c 'FFT-free exact PBS')."""
+    bsk = _u64(bsk)
+    x = _u64(cts).reshape(-1, n + 1)
+    L = _u64(luts)
+    if L.ndim == 1:
+        L = L.reshape(1, -1)
+    out = np.zeros((x.shape[0], (k + 1) * N if glwe_out else k * N + 1), dtype=np.uint64)
+    idx = None
+    if lut_idx is not None:
+        idx = np.ascontiguousarray(lut_idx, dtype=np.uint32)
+    lib().orc_exact_pbs_batch(_p(bsk), n, k, N, base_log, level, _p(x), _p(out), _p(L),
+                              _p(idx, u32p) if idx is not None else None, x.shape[0], threads, int(glwe_out))
     return out
 
 
@@ -240,6 +269,19 @@ class FourierBsk:
             idx = np.ascontiguousarray(lut_idx, dtype=np.uint32)
         lib().orc_pbs_batch(self.h, _p(lwe_in), _p(out), _p(luts),
                             idx.ctypes.data_as(u32p) if idx is not None else None, cnt, threads)
+        return out
+
+    def blind_rotate(self, lwe_in, luts, lut_idx=None, threads=8) -> np.ndarray:
+        """bootstrap_without_sample_extract: the accumulators [count][(k+1)N]."""
+        lwe_in = _u64(lwe_in).reshape(-1, self.n + 1)
+        luts = _u64(luts)
+        cnt = lwe_in.shape[0]
+        out = np.zeros((cnt, (self.k + 1) * self.N), dtype=np.uint64)
+        idx = None
+        if lut_idx is not None:
+            idx = np.ascontiguousarray(lut_idx, dtype=np.uint32)
+        lib().orc_blind_rotate_batch(self.h, _p(lwe_in), _p(out), _p(luts),
+                                     idx.ctypes.data_as(u32p) if idx is not None else None, cnt, threads)
         return out
 
 

@@ -1257,3 +1257,155 @@ void orc_keyswitch_batch(const uint64_t *ksk, int in_dim, int out_dim, int base_
         }
     }
 }
+
+/* ------------------------------------------------------------------------------------ */
+/* FFT-free exact PBS (second oracle).                                                    */
+/* The same blind rotation (bootstrap.rs:243-344) and external product (ggsw.rs:477-598)  */
+/* with every negacyclic product computed exactly in (Z/2^64)[X]/(X^N+1) from the          */
+/* STANDARD-domain BSK: Karatsuba over wrapping u64 (ring operations only, so exact mod    */
+/* 2^64 whatever the split), checked against the schoolbook orc_negacyclic_mul_u64.       */
+/* The reference's own tests pin its FFT only to a tolerance (fft/tests.rs:166-172); this  */
+/* oracle is what the GPU's FFT-based PBS is bounded against (tests/test_exact_pbs_gpu.py).*/
+/* ------------------------------------------------------------------------------------ */
+/* r[0 .. 2n-1) = a * b (full product, wrapping); n a power of two; t: >= 8n words */
+static void kara_mul(uint64_t *r, const uint64_t *a, const uint64_t *b, int n, uint64_t *t) {
+    if (n <= 32) {
+        for (int i = 0; i < 2 * n - 1; i++) r[i] = 0;
+        for (int i = 0; i < n; i++) {
+            const uint64_t ai = a[i];
+            for (int j = 0; j < n; j++) r[i + j] += ai * b[j];
+        }
+        return;
+    }
+    const int h = n / 2;
+    uint64_t *sa = t, *sb = t + h, *z1 = t + 2 * h, *tt = t + 4 * h;
+    for (int i = 0; i < h; i++) {
+        sa[i] = a[i] + a[i + h];
+        sb[i] = b[i] + b[i + h];
+    }
+    kara_mul(z1, sa, sb, h, tt);              /* (a0 + a1)(b0 + b1) */
+    kara_mul(r, a, b, h, tt);                 /* z0 -> r[0, 2h-1)   */
+    r[2 * h - 1] = 0;
+    kara_mul(r + 2 * h, a + h, b + h, h, tt); /* z2 -> r[2h, 4h-1)  */
+    for (int i = 0; i < 2 * h - 1; i++) z1[i] -= r[i] + r[2 * h + i];
+    for (int i = 0; i < 2 * h - 1; i++) r[h + i] += z1[i];
+}
+
+/* out += a * b  mod (X^N + 1), exact over Z/2^64.  t: >= 10 N words */
+static void negacyclic_mul_add_exact(uint64_t *out, const uint64_t *a, const uint64_t *b, int N, uint64_t *t) {
+    uint64_t *full = t, *tt = t + 2 * N;
+    kara_mul(full, a, b, N, tt);
+    for (int i = 0; i < N - 1; i++) out[i] += full[i] - full[i + N];
+    out[N - 1] += full[N - 1];
+}
+
+void orc_negacyclic_mul_add_exact(int N, const uint64_t *a, const uint64_t *b, uint64_t *out) {
+    uint64_t *t = malloc(sizeof(uint64_t) * 10 * (size_t)N);
+    negacyclic_mul_add_exact(out, a, b, N, t);
+    free(t);
+}
+
+typedef struct {
+    const uint64_t *bsk; /* standard [n][L][k+1][k+1][N], borrowed from the caller */
+    int n, k, N, base_log, level;
+} exact_bsk;
+
+typedef struct {
+    uint64_t *ct1, *state, *digits, *t;
+} exact_scratch;
+
+/* out += GGSW (x) glwe, exact (ggsw.rs:477-598 with every FFT product replaced by the exact
+ * negacyclic product; same decomposition, level order L..1 and rows 0..k) */
+static void exact_external_product_add(const exact_bsk *b, const uint64_t *ggsw, uint64_t *out,
+                                       const uint64_t *glwe, exact_scratch *s) {
+    int k = b->k, N = b->N, L = b->level, beta = b->base_log;
+    size_t gl = (size_t)(k + 1) * N;
+    uint64_t mask = (1ULL << beta) - 1;
+    for (size_t j = 0; j < gl; j++)
+        s->state[j] = orc_closest_representable(glwe[j], beta, L) >> (64 - beta * L);
+    for (int lvl = L; lvl >= 1; lvl--) {
+        const uint64_t *lm = ggsw + (size_t)(lvl - 1) * (k + 1) * (k + 1) * N;
+        for (int row = 0; row <= k; row++) {
+            uint64_t *st = s->state + (size_t)row * N;
+            for (int j = 0; j < N; j++) s->digits[j] = decompose_one_level(beta, &st[j], mask);
+            for (int col = 0; col <= k; col++)
+                negacyclic_mul_add_exact(out + (size_t)col * N, s->digits, lm + ((size_t)row * (k + 1) + col) * N, N,
+                                         s->t);
+        }
+    }
+}
+
+static void exact_pbs_one(const exact_bsk *b, const uint64_t *lwe_in, uint64_t *lwe_out, const uint64_t *lut,
+                          uint64_t *acc, exact_scratch *s, int glwe_out) {
+    int n = b->n, k = b->k, N = b->N;
+    int log2N = 0;
+    while ((1 << log2N) < N) log2N++;
+    size_t ggsw_len = (size_t)b->level * (k + 1) * (k + 1) * N;
+    uint64_t bt = orc_pbs_modulus_switch(lwe_in[n], log2N);
+    for (int p = 0; p <= k; p++) monomial_div(acc + (size_t)p * N, lut + (size_t)p * N, N, bt);
+    for (int i = 0; i < n; i++) {
+        if (lwe_in[i] == 0) continue;
+        uint64_t at = orc_pbs_modulus_switch(lwe_in[i], log2N);
+        for (int p = 0; p <= k; p++) monomial_mul_sub(s->ct1 + (size_t)p * N, acc + (size_t)p * N, N, at);
+        exact_external_product_add(b, b->bsk + (size_t)i * ggsw_len, acc, s->ct1, s);
+    }
+    if (glwe_out)
+        memcpy(lwe_out, acc, sizeof(uint64_t) * (size_t)(k + 1) * N);
+    else
+        sample_extract0(acc, lwe_out, k, N);
+}
+
+typedef struct {
+    const exact_bsk *b;
+    const uint64_t *in, *luts;
+    const uint32_t *lut_idx;
+    uint64_t *out;
+    size_t count, next;
+    pthread_mutex_t mu;
+    int glwe_out;
+} exact_job;
+
+static void *exact_worker(void *arg) {
+    exact_job *J = arg;
+    const exact_bsk *b = J->b;
+    int k = b->k, N = b->N;
+    size_t gl = (size_t)(k + 1) * N;
+    exact_scratch s;
+    s.ct1 = malloc(sizeof(uint64_t) * gl);
+    s.state = malloc(sizeof(uint64_t) * gl);
+    s.digits = malloc(sizeof(uint64_t) * N);
+    s.t = malloc(sizeof(uint64_t) * 10 * (size_t)N);
+    uint64_t *acc = malloc(sizeof(uint64_t) * gl);
+    for (;;) {
+        pthread_mutex_lock(&J->mu);
+        size_t c = J->next++;
+        pthread_mutex_unlock(&J->mu);
+        if (c >= J->count) break;
+        size_t li = J->lut_idx ? J->lut_idx[c] : 0;
+        const size_t out_len = J->glwe_out ? gl : (size_t)(k * N + 1);
+        exact_pbs_one(b, J->in + c * (size_t)(b->n + 1), J->out + c * out_len, J->luts + li * gl, acc, &s,
+                      J->glwe_out);
+    }
+    free(acc);
+    free(s.ct1);
+    free(s.state);
+    free(s.digits);
+    free(s.t);
+    return NULL;
+}
+
+/* Exact PBS (glwe_out = 0: sample-extracted LWE [count][kN+1]; 1: accumulators [count][(k+1)N]) */
+void orc_exact_pbs_batch(const uint64_t *bsk, int n, int k, int N, int base_log, int level, const uint64_t *in,
+                         uint64_t *out, const uint64_t *luts, const uint32_t *lut_idx, size_t count, int threads,
+                         int glwe_out) {
+    exact_bsk b = {bsk, n, k, N, base_log, level};
+    exact_job J = {&b, in, luts, lut_idx, out, count, 0};
+    J.glwe_out = glwe_out;
+    pthread_mutex_init(&J.mu, NULL);
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, exact_worker, &J);
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    pthread_mutex_destroy(&J.mu);
+}

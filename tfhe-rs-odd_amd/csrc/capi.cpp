@@ -117,19 +117,19 @@ struct TfheMi355Context {
     DeviceBuffer fbsk, ksk, std_staging;
     DeviceBuffer io_luts, io_tmp;
     DeviceBuffer ksk_planes;   // int8 byte planes of the KSK for the MFMA keyswitch
-    // Host-pointer entry points: a two-lane pipeline (stream, pinned staging, device buffers and
-    // scratch per lane) so that chunk i's copies overlap chunk i+-1's kernels.  Only the
+    // Host-pointer entry points: kernels run in chunk order on `stream`; each of two lanes has a
+    // copy stream, page-locked staging and device in/out buffers, so that chunk i's copies (and
+    // the host-side copies into and out of the staging) overlap chunk i+-1's kernels.  Only the
     // synchronous entry points use these, under `mu`; the _async entry points take all their
     // scratch from the caller (no shared mutable state, capturable into a hipGraph).
     struct Lane {
         hipStream_t stream = nullptr;
-        hipEvent_t done = nullptr;
+        hipEvent_t h2d = nullptr, kern = nullptr, done = nullptr;
         PinnedBuffer h_in, h_out, h_idx;
-        DeviceBuffer d_in, d_out, d_idx, scratch;
+        DeviceBuffer d_in, d_out, d_idx;
         bool pending = false;
         size_t first = 0, count = 0;
     } lanes[2];
-    hipEvent_t luts_ready = nullptr;
     bool ksk_planes_ready = false;
     bool fbsk_ready = false, ksk_ready = false;
     // LWE -> GLWE packing keyswitching key of the gadget layer (big LWE key -> GLWE key)
@@ -450,27 +450,31 @@ void validate_lut_indexes(const uint32_t *idx, size_t count, size_t lut_count) {
 }
 
 // ---- host-pointer pipeline ------------------------------------------------------------------------
-// The synchronous entry points (host buffers in and out, the form the Rust binding calls) run as a
-// two-lane pipeline over chunks of the batch: per chunk, the host input slice is copied into the
-// lane's page-locked buffer, DMA'd to the device, processed and DMA'd back on the lane's stream,
-// and its output is copied to the caller's buffer while the other lane's chunk runs on the GPU.
-// The LUTs go up once per call.  Callers are serialised by ctx->mu.
+// The synchronous entry points (host buffers in and out, the form the Rust binding calls) run the
+// batch in chunks: per chunk, the host input slice is copied into a lane's page-locked buffer and
+// DMA'd up on the lane's copy stream, the kernels run on ctx->stream (chunks in order, so the GPU
+// stays busy), and the output is DMA'd back on the copy stream and copied into the caller's
+// buffer while the next chunk's kernels run.  The LUTs go up once per call.  Callers are
+// serialised by ctx->mu.
 
 using ChunkLaunch = void (*)(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, const uint64_t *d_luts,
                              size_t lut_count, const uint32_t *d_idx, size_t count, void *scratch,
                              size_t scratch_bytes, hipStream_t s);
 using ScratchSize = size_t (*)(const TfheMi355Context *c, size_t count);
 
-size_t host_chunk(const TfheMi355Context *c, size_t out_words) {
+size_t host_chunk(const TfheMi355Context *c, size_t count) {
     static const size_t forced = [] {
         const char *e = std::getenv("TFHE_MI355_HOST_CHUNK");
         const long x = e ? std::atol(e) : 0;
         return x > 0 ? (size_t)x : (size_t)0;
     }();
     if (forced) return forced;
-    // >= one full wave of PBS slots (256 CUs x 4 ciphertexts), else ~16 MiB of output per chunk
-    const size_t min_chunk = is_large(c) ? large_chunk() : 1024;
-    return std::max(min_chunk, ((size_t)16 << 20) / (out_words * 8));
+    if (is_large(c)) return large_chunk();
+    // >= 4 chunks so that copies hide behind kernels; >= one full wave of PBS slots (256 CUs x 4
+    // ciphertexts) and <= 4 waves per launch
+    const size_t slots = 1024;
+    const size_t quarter = (count + 3) / 4;
+    return std::min<size_t>(4 * slots, std::max(slots, (quarter + slots - 1) / slots * slots));
 }
 
 void lane_finish(TfheMi355Context::Lane &L, void *out, size_t out_words) {
@@ -484,27 +488,28 @@ void run_host_pipeline(TfheMi355Context *c, const uint64_t *in, size_t in_words,
                        const uint64_t *luts, size_t lut_words, size_t lut_count, const uint32_t *idx, size_t count,
                        ChunkLaunch launch, ScratchSize scratch_size) {
     if (count == 0) return;
+    hipStream_t cs = c->stream;
     const uint64_t *d_luts = nullptr;
-    if (luts) {
+    if (luts) {  // on the kernel stream: ordered before every chunk's kernels
         c->io_luts.reserve(lut_count * lut_words * 8);
-        check(hipMemcpyAsync(c->io_luts.ptr, luts, lut_count * lut_words * 8, hipMemcpyHostToDevice, c->stream),
+        check(hipMemcpyAsync(c->io_luts.ptr, luts, lut_count * lut_words * 8, hipMemcpyHostToDevice, cs),
               "H2D luts");
-        check(hipEventRecord(c->luts_ready, c->stream), "luts event");
         d_luts = (const uint64_t *)c->io_luts.ptr;
     }
-    const size_t chunk = std::min(count, host_chunk(c, out_words));
+    const size_t chunk = std::min(count, host_chunk(c, count));
+    // kernels of consecutive chunks are ordered on cs: one scratch serves them all
     const size_t need_scratch = scratch_size ? scratch_size(c, chunk) : 0;
+    if (need_scratch) c->io_tmp.reserve(need_scratch);
     try {
         size_t next = 0;
         for (int q = 0; next < count; q ^= 1) {
             TfheMi355Context::Lane &L = c->lanes[q];
-            lane_finish(L, out, out_words);
+            lane_finish(L, out, out_words);  // this lane's previous chunk: all its device work is done
             const size_t cnt = std::min(chunk, count - next);
             L.h_in.reserve(chunk * in_words * 8);
             L.h_out.reserve(chunk * out_words * 8);
             L.d_in.reserve(chunk * in_words * 8);
             L.d_out.reserve(chunk * out_words * 8);
-            if (need_scratch) L.scratch.reserve(need_scratch);
             std::memcpy(L.h_in.ptr, in + next * in_words, cnt * in_words * 8);
             check(hipMemcpyAsync(L.d_in.ptr, L.h_in.ptr, cnt * in_words * 8, hipMemcpyHostToDevice, L.stream),
                   "H2D in");
@@ -516,9 +521,12 @@ void run_host_pipeline(TfheMi355Context *c, const uint64_t *in, size_t in_words,
                 check(hipMemcpyAsync(L.d_idx.ptr, L.h_idx.ptr, cnt * 4, hipMemcpyHostToDevice, L.stream), "H2D idx");
                 d_idx = (const uint32_t *)L.d_idx.ptr;
             }
-            if (luts) check(hipStreamWaitEvent(L.stream, c->luts_ready, 0), "wait luts");
+            check(hipEventRecord(L.h2d, L.stream), "h2d event");
+            check(hipStreamWaitEvent(cs, L.h2d, 0), "wait h2d");
             launch(c, (const uint64_t *)L.d_in.ptr, (uint64_t *)L.d_out.ptr, d_luts, lut_count, d_idx, cnt,
-                   L.scratch.ptr, L.scratch.bytes, L.stream);
+                   need_scratch ? c->io_tmp.ptr : nullptr, need_scratch ? c->io_tmp.bytes : 0, cs);
+            check(hipEventRecord(L.kern, cs), "kernel event");
+            check(hipStreamWaitEvent(L.stream, L.kern, 0), "wait kernels");
             check(hipMemcpyAsync(L.h_out.ptr, L.d_out.ptr, cnt * out_words * 8, hipMemcpyDeviceToHost, L.stream),
                   "D2H out");
             check(hipEventRecord(L.done, L.stream), "chunk event");
@@ -537,6 +545,7 @@ void run_host_pipeline(TfheMi355Context *c, const uint64_t *in, size_t in_words,
             lane_finish(b, out, out_words);
         }
     } catch (...) {
+        (void)hipStreamSynchronize(cs);
         for (auto &L : c->lanes) {
             (void)hipStreamSynchronize(L.stream);
             L.pending = false;
@@ -608,9 +617,9 @@ int tfhe_mi355_context_create(const TfheMi355Parameters *params, int device, Tfh
             check(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
             for (auto &L : c->lanes) {
                 check(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking), "hipStreamCreate(lane)");
-                check(hipEventCreateWithFlags(&L.done, hipEventDisableTiming), "hipEventCreate(lane)");
+                for (hipEvent_t *e : {&L.h2d, &L.kern, &L.done})
+                    check(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate(lane)");
             }
-            check(hipEventCreateWithFlags(&c->luts_ready, hipEventDisableTiming), "hipEventCreate(luts)");
             build_tables(c);
         } catch (...) {
             tfhe_mi355_context_destroy(c);
@@ -631,10 +640,10 @@ int tfhe_mi355_context_destroy(TfheMi355Context *ctx) {
         if (ctx->tables.twist) (void)hipFree(ctx->tables.twist);
         if (ctx->tables.wtop) (void)hipFree(ctx->tables.wtop);
         for (auto &L : ctx->lanes) {
-            if (L.done) (void)hipEventDestroy(L.done);
+            for (hipEvent_t e : {L.h2d, L.kern, L.done})
+                if (e) (void)hipEventDestroy(e);
             if (L.stream) (void)hipStreamDestroy(L.stream);
         }
-        if (ctx->luts_ready) (void)hipEventDestroy(ctx->luts_ready);
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
         delete ctx;  // device and pinned buffers free themselves
     });
