@@ -10,7 +10,7 @@ step() {  # step NAME TIMEOUT CMD...
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-step new_tests 600 python -u -m pytest tests/test_exact_pbs_gpu.py tests/test_abi_concurrency_gpu.py -x -v -s --timeout 300 --timeout-method thread
+step gpu_tests 900 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread
 step bench_2_2 400 python bench.py --steps 5 --warmup 1 --no-cpu-baseline
 for t in ${PMC_TAGS:-2_2 2_2ks mb3 4_4}; do
   step pmc_$t 900 bash scripts/pmc_workload.sh $t

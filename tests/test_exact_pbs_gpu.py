@@ -16,7 +16,7 @@ independently of the FFT DAG the engine and the FFT oracle share.
    (n CMUXes x (1 + kN/2) coefficient errors of variance <= T^2/3 each in the phase).  The
    measured excess is predicted by the single-CMUX error: excess = n (1 + kN/2) rms^2 (the FFT
    noise term of TFHE, which the reference's concrete-fft path carries too); the test checks it
-   within a factor 2 (n = 64, 2048 samples) / 2.5 (n = 742, 96 samples).
+   within a factor 2 (n = 64, 2048 samples; n = 742, 1024 samples).
 """
 import numpy as np
 import pytest
@@ -133,8 +133,11 @@ def test_pbs_noise_distribution_reduced_n_vs_exact(orc):
 
 
 def test_pbs_noise_full_2_2_vs_exact(orc, keys_2_2):
-    """The full PARAM_MESSAGE_2_CARRY_2 bootstrap (n = 742) on 96 ciphertexts: every output decrypts
-    like the exact one; with 96 samples the variance estimates carry ~15% sampling error, so the
-    variance check here is 1/4 relative (the 1/16 check runs at n = 64 with 2048 samples above)."""
+    """The full PARAM_MESSAGE_2_CARRY_2 bootstrap (n = 742) on 1024 ciphertexts: every output decrypts
+    like the exact one and the variances agree within 1/10.  The excess v_GPU - v_exact is the
+    difference of two independent sample variances (the digit paths diverge, so the two output
+    noises are uncorrelated): at B samples its standard error is about 2.6 v / sqrt(B) -- 0.27 v at
+    B = 96, where a first run measured 0.19 v against the predicted 0.65 v (1.7 sigma), 0.08 v at
+    B = 1024, which the factor-2 band holds."""
     k = keys_2_2
-    _compare_noise(orc, k.params, k.lwe_sk, k.glwe_sk, k.bsk, 96, 54, 0.25, 2.5)
+    _compare_noise(orc, k.params, k.lwe_sk, k.glwe_sk, k.bsk, 1024, 54, 0.1, 2.0)
