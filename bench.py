@@ -638,7 +638,7 @@ def run_mul32(args, P, workload, kname, R):
     from tfhe_mi355 import Engine, client, integer, shortint
     from tfhe_mi355.distributed import broadcast_u64, shard_range
 
-    K = args.batch or 256
+    K = args.batch or 1024  # K = 1024: every DAG layer a multiple of 1024 slots or close (2048-65536 PBS per layer at 256 pairs left partial rounds)
     ck = shortint.ClientKey(P, args.seed)
     eng = Engine(P, R.device.index)
     bsk_len = ggsw_count(P) * P.pbs_level * (P.glwe_dimension + 1) ** 2 * P.polynomial_size

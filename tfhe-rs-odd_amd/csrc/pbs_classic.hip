@@ -63,6 +63,12 @@ struct PbsConfig {
     // 3 at N = 512 (<= 168), 1 for the other N = 2048 shapes (~430 VGPR+AGPR at L = 2)
     static constexpr int WPE = PBS_WAVES_PER_EU > 0 ? PBS_WAVES_PER_EU
                                                     : (PACK4 ? 2 : N >= 2048 ? 1 : N == 1024 ? 2 : 3);
+    // persistent grid (needs GSYNC: slots never wait on each other), off by default.  Measured A/B
+    // (4096 PBS, static stride schedule): 2_2 116.8k -> 90.8k PBS/s, TFHE_LIB 110.1k -> 92.0k,
+    // SIMON_40 97.6k -> 93.4k, MANTICORE 99.7k -> 103.9k, ASCON_40 36.9k -> 40.6k, AES_40
+    // 52.7k -> 49.7k: a static schedule over "resident" workgroups loses whenever not every one of
+    // them is resident from the start (a late workgroup runs its whole share after the others)
+    static constexpr bool PERSIST = GSYNC && PBS_PERSIST > 0;
 };
 
 template <int N, int K, int L>
@@ -89,9 +95,6 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
     int lane = lane0;
     const int wave = wid % (K + 1);        // polynomial of the ciphertext this wave owns
     const int slot = wid / (K + 1);        // ciphertext slot in the workgroup
-    const int ct_raw = blockIdx.x * CPW + slot;
-    const bool active = ct_raw < a.count;  // idle slots compute on a valid ct, store nothing
-    const int ct = active ? ct_raw : a.count - 1;
     const int n = a.n;
     const int beta = a.base_log;
     const uint32_t dmask = (1u << beta) - 1;
@@ -120,6 +123,14 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
         xsync = {lds_addr(gflags + slot * (K + 1)), lds_addr(gflags + wid)};
     cx *xb = xct + wave * XL;
     uint64_t *xb64 = reinterpret_cast<uint64_t *>(xb);
+
+    // Ciphertext loop.  PERSIST (per-ciphertext sync: a slot's (k+1) waves never wait on the
+    // other slots): the grid is at most one resident wave of workgroups (sized by the host) and
+    // each slot walks the batch with stride gridDim.x * CPW.  Otherwise the grid covers the batch
+    // (one trip); idle slots compute on a valid ciphertext and store nothing.
+    auto run_ct = [&](const int ct_raw) {
+    const bool active = ct_raw < a.count;  // idle slots compute on a valid ct, store nothing
+    const int ct = active ? ct_raw : a.count - 1;
     const uint64_t *in = a.lwe_in + (size_t)ct * (n + 1);
     // the input row is read-only for the whole launch: constant address space -> s_load
     const __attribute__((address_space(4))) uint64_t *in_s = (const __attribute__((address_space(4))) uint64_t *)(
@@ -312,23 +323,32 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
     }
 
     if (a.glwe_out) {  // bootstrap_without_sample_extract (fork, bootstrap.rs:383-412)
-        if (!active) return;
-        uint64_t *g = a.lwe_out + ((size_t)ct * (K + 1) + wave) * N;
+        if (active) {
+            uint64_t *g = a.lwe_out + ((size_t)ct * (K + 1) + wave) * N;
 #pragma unroll
-        for (int h = 0; h < 2 * V; h++) g[lane + 64 * h] = c0[h];
+            for (int h = 0; h < 2 * V; h++) g[lane0 + 64 * h] = c0[h];
+        }
         return;
     }
     // sample extract at degree 0 (glwe_sample_extraction.rs:91-147)
     wsync();
 #pragma unroll
-    for (int h = 0; h < 2 * V; h++) xb64[lane + 64 * h] = c0[h];
+    for (int h = 0; h < 2 * V; h++) xb64[lane0 + 64 * h] = c0[h];
     wsync();
-    if (!active) return;
-    uint64_t *out = a.lwe_out + (size_t)ct * (K * N + 1);
-    if (wave < K) {
-        for (int j = lane; j < N; j += 64) out[wave * N + j] = j == 0 ? xb64[0] : 0 - xb64[N - j];
-    } else if (lane == 0) {
-        out[K * N] = c0[0];
+    if (active) {
+        uint64_t *out = a.lwe_out + (size_t)ct * (K * N + 1);
+        if (wave < K) {
+            for (int j = lane0; j < N; j += 64) out[wave * N + j] = j == 0 ? xb64[0] : 0 - xb64[N - j];
+        } else if (lane0 == 0) {
+            out[K * N] = c0[0];
+        }
+    }
+    wsync();  // the extract's reads of xb64 precede the next ciphertext's rotation writes
+    };
+    if constexpr (Cfg::PERSIST) {
+        for (int ct_raw = blockIdx.x * CPW + slot; ct_raw < a.count; ct_raw += gridDim.x * CPW) run_ct(ct_raw);
+    } else {
+        run_ct(blockIdx.x * CPW + slot);
     }
 }
 
@@ -337,8 +357,10 @@ static hipError_t launch_pbs_t(const ClassicPbsLaunch &a, hipStream_t s) {
     constexpr int CPW = PbsConfig<N, K, L>::CPW;
     const size_t lds = PbsConfig<N, K, L>::lds_bytes();
     if (a.count == 0) return hipSuccess;
-    const int blocks = (a.count + CPW - 1) / CPW;
-    hipLaunchKernelGGL((pbs_classic_kernel<N, K, L>), dim3(blocks), dim3(64 * (K + 1) * CPW), lds, s, a);
+    const int threads = 64 * (K + 1) * CPW;
+    int blocks = (a.count + CPW - 1) / CPW;
+    if (PbsConfig<N, K, L>::PERSIST) blocks = std::min(blocks, resident_blocks((const void *)pbs_classic_kernel<N, K, L>, threads, lds));
+    hipLaunchKernelGGL((pbs_classic_kernel<N, K, L>), dim3(blocks), dim3(threads), lds, s, a);
     return hipGetLastError();
 }
 

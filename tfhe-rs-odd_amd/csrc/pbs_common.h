@@ -31,7 +31,22 @@
 #define PBS_GROUP_SYNC 1  // CMUX-loop syncs between the (k+1) waves of ONE ciphertext (LDS flags), not s_barrier
 #endif
 
+#ifndef PBS_PERSIST
+#define PBS_PERSIST 0  // 1: persistent classic-PBS grid, each ciphertext slot walks the batch (A/B option)
+#endif
+
 namespace tfhe_mi355 {
+
+// Workgroups of a kernel resident at once on the current device (CUs x occupancy); the
+// persistent PBS grids are capped at this so that every workgroup is running from the start.
+inline int resident_blocks(const void *kernel, int threads, size_t lds) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, lds) != hipSuccess || cus <= 0 || per <= 0)
+        return 0x7fffffff;
+    return cus * per;
+}
 
 template <int LOG2N>
 __device__ __forceinline__ uint32_t pbs_modulus_switch(uint64_t x) {
