@@ -5,7 +5,8 @@ mkdir -p gpurun_out
 for v in ${VARIANTS:-var1 var2}; do
   lib=tfhe-rs-odd_amd/build/$v/libtfhe_mi355.so
   echo "== $v"
-  TFHE_MI355_LIB=$PWD/$lib timeout -k 10 300 python -m pytest tests/test_pbs_gpu.py -x -q -k "${TESTK:-bit_exact}" > gpurun_out/t_$v.log 2>&1
+  kexpr=${TESTK-bit_exact}
+  TFHE_MI355_LIB=$PWD/$lib timeout -k 10 300 python -m pytest ${TESTFILES:-tests/test_pbs_gpu.py} -x -q ${kexpr:+-k "$kexpr"} > gpurun_out/t_$v.log 2>&1
   rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/t_$v.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
   for bp in ${BENCH_PARAMS:-2_2}; do

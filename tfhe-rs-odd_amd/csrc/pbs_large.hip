@@ -144,24 +144,24 @@ __global__ void __launch_bounds__(256) large_init_kernel(LargePbsLaunch a, int c
 #ifndef LARGE_TOPT
 #define LARGE_TOPT 256
 #endif
+#ifndef LARGE_FUSE_TOP
+#define LARGE_FUSE_TOP 0  // 1: CMUX i's top_inv and CMUX i+1's top_fwd as one launch (large_top_fused_kernel; A/B: slower)
+#endif
+#ifndef LARGE_FUSED_T
+#define LARGE_FUSED_T 512  // threads per fused top workgroup (one workgroup per row: 1024 / T butterflies per thread)
+#endif
+#ifndef LARGE_FUSED_WPE
+#define LARGE_FUSED_WPE 4  // waves per SIMD the fused top kernel's register budget allows
+#endif
 #ifndef LARGE_MAC_SB
 #define LARGE_MAC_SB 4  // MAC slots per scheduling region of large_sub (GGSW loads in flight)
 #endif
 constexpr int TOPT = LARGE_TOPT;  // threads per top-stage workgroup
 
+// rotate, decompose, twist and top DIF radix-16 of butterfly t of row r, CMUX i -> T
 template <int K, int L>
-__global__ void __launch_bounds__(TOPT, 4) large_top_fwd_kernel(LargePbsLaunch a, int ct0, int i) {
+__device__ __forceinline__ void top_fwd_body(const LargePbsLaunch &a, int ct0, int i, int cl, int r, int t) {
     static_assert(L == 1 || L == 2, "levels L and L-1 only");
-    constexpr int BPP = 1024 / TOPT;  // workgroups per polynomial
-    // XCD-aware: workgroup w runs on XCD w % 8; all (K+1) BPP workgroups of a ciphertext share
-    // one XCD, so the rotated gather re-reads the accumulator rows from that XCD's L2
-    const int x = blockIdx.x & 7, m = blockIdx.x >> 3;
-    const int sub = m % ((K + 1) * BPP);
-    const int cl = x + 8 * (m / ((K + 1) * BPP));
-    if (cl >= a.chunk_count) return;  // whole workgroup
-    const int ab = sub % BPP;
-    const int r = sub / BPP;
-    const int t = ab * TOPT + threadIdx.x;  // butterfly a
     const uint64_t *in = a.lwe_in + (size_t)(ct0 + cl) * (a.n + 1);
     const uint32_t at = pbs_modulus_switch<15>(in[i]);
     const bool full_odd = (at / LN) & 1;
@@ -211,6 +211,18 @@ __global__ void __launch_bounds__(TOPT, 4) large_top_fwd_kernel(LargePbsLaunch a
         }
         top_and_store(L - 1);
     }
+}
+
+template <int K, int L>
+__global__ void __launch_bounds__(TOPT, 4) large_top_fwd_kernel(LargePbsLaunch a, int ct0, int i) {
+    constexpr int BPP = 1024 / TOPT;  // workgroups per polynomial
+    // XCD-aware: workgroup w runs on XCD w % 8; all (K+1) BPP workgroups of a ciphertext share
+    // one XCD, so the rotated gather re-reads the accumulator rows from that XCD's L2
+    const int x = blockIdx.x & 7, m = blockIdx.x >> 3;
+    const int sub = m % ((K + 1) * BPP);
+    const int cl = x + 8 * (m / ((K + 1) * BPP));
+    if (cl >= a.chunk_count) return;  // whole workgroup
+    top_fwd_body<K, L>(a, ct0, i, cl, sub / BPP, (sub % BPP) * TOPT + threadIdx.x);
 }
 
 // (k+1) L waves; LDS: sub-block twiddle table + one 1024-entry buffer per wave
@@ -289,13 +301,9 @@ __global__ void __launch_bounds__((LargeSubCfg<K, L>::THREADS), 2) large_sub_ker
     for (int b = 0; b < 16; b++) dst[64 * b] = make_double2(v[b].re, v[b].im);
 }
 
+// top DIT radix-16 of butterfly t of column col, backward conversion, acc += increments
 template <int K>
-__global__ void __launch_bounds__(TOPT) large_top_inv_kernel(LargePbsLaunch a, int ct0, int i) {
-    constexpr int BPP = 1024 / TOPT;
-    const int ab = blockIdx.x % BPP;
-    const int col = (blockIdx.x / BPP) % (K + 1);
-    const int cl = blockIdx.x / (BPP * (K + 1));
-    const int t = ab * TOPT + threadIdx.x;
+__device__ __forceinline__ void top_inv_body(const LargePbsLaunch &a, int cl, int col, int t) {
     const double2 *U = a.spectra + ((size_t)cl * a.levels * (K + 1) + col) * LM + t;
     cx u[16];
     u[0] = gld(U);
@@ -316,6 +324,32 @@ __global__ void __launch_bounds__(TOPT) large_top_inv_kernel(LargePbsLaunch a, i
         acc[j] = lo;
         acc[j + LM] = hi;
     }
+}
+
+template <int K>
+__global__ void __launch_bounds__(TOPT) large_top_inv_kernel(LargePbsLaunch a, int ct0, int i) {
+    constexpr int BPP = 1024 / TOPT;
+    const int col = (blockIdx.x / BPP) % (K + 1);
+    top_inv_body<K>(a, blockIdx.x / (BPP * (K + 1)), col, (blockIdx.x % BPP) * TOPT + threadIdx.x);
+}
+
+// CMUX i's top inverse stage fused with CMUX i+1's top forward stage (LARGE_FUSE_TOP=1): one
+// workgroup per (ciphertext, row r) owns all 1024 butterflies of the row, so after its inverse half
+// (acc row r updated in place) and a workgroup barrier, the rotated gather of the forward half
+// reads the row that this workgroup has just written instead of re-reading it from the Infinity
+// Cache in a separate launch.  Column c of the inverse is row c of the next CMUX.  Bit-exact, but
+// measured slower (4_4 KS+PBS: 961/s separate, 778/s at 512 threads, 549/s at 256): a whole-row
+// workgroup leaves 256 workgroups per chunk of 128, one per CU, where the separate kernels run
+// 1024 -- the gather saving does not pay for the lost memory-level parallelism.
+template <int K, int L>
+__global__ void __launch_bounds__(LARGE_FUSED_T, LARGE_FUSED_WPE) large_top_fused_kernel(LargePbsLaunch a, int ct0, int i) {
+    constexpr int BPT = 1024 / LARGE_FUSED_T;  // butterflies per thread
+    const int r = blockIdx.x % (K + 1), cl = blockIdx.x / (K + 1);
+#pragma unroll 1
+    for (int h = 0; h < BPT; h++) top_inv_body<K>(a, cl, r, threadIdx.x + h * LARGE_FUSED_T);
+    __syncthreads();  // workgroup-scope release/acquire: the row's new values are visible to every wave
+#pragma unroll 1
+    for (int h = 0; h < BPT; h++) top_fwd_body<K, L>(a, ct0, i + 1, cl, r, threadIdx.x + h * LARGE_FUSED_T);
 }
 
 // sample extract at degree 0 (glwe_sample_extraction.rs:91-147)
@@ -388,14 +422,22 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
         const size_t init_elems = (size_t)cnt * (K + 1) * LN;
         hipLaunchKernelGGL(large_init_kernel<K>, dim3((unsigned)((init_elems + 255) / 256)), dim3(256), 0, s, a,
                            ct0, cnt);
+        using Sub = LargeSubCfg<K, L>;
+        const unsigned top_blocks = (unsigned)cnt * (K + 1) * (1024 / TOPT);
+        const unsigned fwd_blocks = (unsigned)((cnt + 7) / 8) * 8 * (K + 1) * (1024 / TOPT);
+        if (a.n > 0)
+            hipLaunchKernelGGL((large_top_fwd_kernel<K, L>), dim3(fwd_blocks), dim3(TOPT), 0, s, a, ct0, 0);
         for (int i = 0; i < a.n; i++) {
-            using Sub = LargeSubCfg<K, L>;
-            const unsigned top_blocks = (unsigned)cnt * (K + 1) * (1024 / TOPT);
-            const unsigned fwd_blocks = (unsigned)((cnt + 7) / 8) * 8 * (K + 1) * (1024 / TOPT);
-            hipLaunchKernelGGL((large_top_fwd_kernel<K, L>), dim3(fwd_blocks), dim3(TOPT), 0, s, a, ct0, i);
             hipLaunchKernelGGL((large_sub_kernel<K, L>), dim3((unsigned)cnt * 16), dim3(Sub::THREADS), Sub::LDS, s, a,
                                ct0, i);
-            hipLaunchKernelGGL((large_top_inv_kernel<K>), dim3(top_blocks), dim3(TOPT), 0, s, a, ct0, i);
+            if (LARGE_FUSE_TOP && i + 1 < a.n) {
+                hipLaunchKernelGGL((large_top_fused_kernel<K, L>), dim3((unsigned)cnt * (K + 1)), dim3(LARGE_FUSED_T), 0, s, a,
+                                   ct0, i);
+            } else {
+                hipLaunchKernelGGL((large_top_inv_kernel<K>), dim3(top_blocks), dim3(TOPT), 0, s, a, ct0, i);
+                if (i + 1 < a.n)
+                    hipLaunchKernelGGL((large_top_fwd_kernel<K, L>), dim3(fwd_blocks), dim3(TOPT), 0, s, a, ct0, i + 1);
+            }
         }
         const size_t out_elems = (size_t)cnt * (K * LN + 1);
         hipLaunchKernelGGL(large_extract_kernel<K>, dim3((unsigned)((out_elems + 255) / 256)), dim3(256), 0, s, a,
