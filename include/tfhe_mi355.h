@@ -135,6 +135,41 @@ int tfhe_mi355_blind_rotate_async(TfheMi355Context *ctx, const uint64_t *d_lwe_i
                                   const uint64_t *d_luts, size_t lut_count, const uint32_t *d_lut_indexes,
                                   size_t count, void *stream);
 
+/* The parameter set a context was created with. */
+int tfhe_mi355_context_parameters(TfheMi355Context *ctx, TfheMi355Parameters *out);
+
+/* ---- serialized server keys (wire formats; csrc/serde.cpp) ----
+ * A tfhe-rs server key arrives as the bincode 1.3.3 encoding of its serde derive
+ * (`bincode::serialize(&key)`, tfhe/Cargo.toml:36,57): these entry points take those bytes.
+ *   CompressedServerKey (shortint/server_key/compressed.rs:43-55): seeded LWE keyswitching key +
+ *     ShortintCompressedBootstrappingKey (Classic / MultiBit seeded BSK) -> regenerated on the GPU
+ *     (tfhe_mi355_{keyswitch,bootstrap}_key_upload_seeded).  Replaces
+ *     CompressedServerKey::decompress (compressed.rs) + the Fourier conversion.
+ *   ServerKey (shortint/server_key/mod.rs:283-297): standard LWE keyswitching key +
+ *     Fourier bootstrapping key in concrete-fft's serialized form (FourierPolynomialList,
+ *     fft64/math/fft/mod.rs:588-717: natural DFT order), mapped into the engine layout
+ *     (N = 2048 and 32768).  Replaces the ServerKey deserialisation feeding the CPU PBS.
+ * Only native (2^64) ciphertext moduli.  *_inspect parses and validates without a GPU and
+ * reports the parameter set the key implies (create the context from info.params); *_upload
+ * requires a context with exactly that parameter set.  Truncated or inconsistent input fails
+ * with a message naming the field and byte offset. */
+typedef struct {
+    TfheMi355Parameters params;        /* implied by the key material (std devs are not serialized) */
+    uint32_t pbs_order;                /* PBSOrder: 0 KeyswitchBootstrap, 1 BootstrapKeyswitch */
+    uint32_t deterministic_execution;  /* multi-bit keys */
+    uint64_t max_degree;
+    uint64_t max_noise_level;          /* ServerKey only (a CompressedServerKey has none: 0) */
+    uint64_t ksk_seed_lo, ksk_seed_hi; /* CompressedServerKey: CompressionSeed of each key */
+    uint64_t bsk_seed_lo, bsk_seed_hi;
+} TfheMi355ServerKeyInfo;
+int tfhe_mi355_compressed_server_key_inspect(const uint8_t *bytes, size_t len, TfheMi355ServerKeyInfo *info);
+int tfhe_mi355_compressed_server_key_upload(TfheMi355Context *ctx, const uint8_t *bytes, size_t len);
+int tfhe_mi355_server_key_inspect(const uint8_t *bytes, size_t len, TfheMi355ServerKeyInfo *info);
+int tfhe_mi355_server_key_upload(TfheMi355Context *ctx, const uint8_t *bytes, size_t len);
+/* engine Fourier layout: freq[e] = natural DFT index held by element e of a polynomial
+ * (N = 2048: M = 1024 entries; N = 32768: 16384) -- host-only, no GPU needed */
+int tfhe_mi355_fourier_engine_frequency(uint32_t N, uint32_t *freq);
+
 /* Seeded (compressed) keys: the reference's SeededLweBootstrapKey / SeededLweKeyswitchKey
  * (shortint CompressedServerKey) hold only the bodies and a CompressionSeed (u128 = hi:lo); every
  * mask is regenerated on the GPU from the concrete-csprng AES-CTR stream of that seed.

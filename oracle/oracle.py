@@ -67,6 +67,7 @@ def lib():
                                       ctypes.c_int, ctypes.c_int]
         L.orc_fbsk_destroy.argtypes = [ctypes.c_void_p]
         L.orc_fbsk_copy.argtypes = [ctypes.c_void_p, f64p]
+        L.orc_mb_fbsk_copy.argtypes = [ctypes.c_void_p, f64p]
         L.orc_pbs_batch.argtypes = [ctypes.c_void_p, u64p, u64p, u64p, u32p, ctypes.c_size_t,
                                     ctypes.c_int]
         L.orc_blind_rotate_batch.argtypes = [ctypes.c_void_p, u64p, u64p, u64p, u32p, ctypes.c_size_t,
@@ -327,6 +328,12 @@ class MultiBitFourierBsk:
         if getattr(self, "h", None):
             lib().orc_mb_fbsk_destroy(self.h)
             self.h = None
+
+    def fourier(self) -> np.ndarray:
+        npoly = (self.n // self.g << self.g) * self.level * (self.k + 1) ** 2
+        out = np.zeros(npoly * self.N // 2, dtype=np.complex128)
+        lib().orc_mb_fbsk_copy(self.h, out.ctypes.data_as(f64p))
+        return out
 
     def pbs(self, lwe_in, luts, lut_idx=None, threads=8) -> np.ndarray:
         lwe_in = _u64(lwe_in).reshape(-1, self.n + 1)

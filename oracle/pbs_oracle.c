@@ -1125,6 +1125,14 @@ void *orc_mb_fbsk_create(const uint64_t *bsk, int n, int k, int N, int base_log,
     return mb;
 }
 
+/* Copies the multi-bit Fourier BSK ([n/g][2^g][L][k+1][k+1][M], position order) out. */
+void orc_mb_fbsk_copy(const void *h, double *out) {
+    const orc_mb_fbsk *mb = h;
+    const orc_fbsk *b = &mb->b;
+    size_t npoly = (size_t)(b->n / mb->g) * (1u << mb->g) * b->level * (b->k + 1) * (b->k + 1);
+    memcpy(out, b->fourier, sizeof(cplx) * npoly * (b->N / 2));
+}
+
 void orc_mb_fbsk_destroy(void *h) {
     orc_mb_fbsk *mb = h;
     if (!mb) return;

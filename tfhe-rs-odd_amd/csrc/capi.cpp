@@ -771,6 +771,13 @@ int tfhe_mi355_bootstrap_key_convert_async(TfheMi355Context *ctx, const uint64_t
     });
 }
 
+int tfhe_mi355_context_parameters(TfheMi355Context *ctx, TfheMi355Parameters *out) {
+    return guarded([&] {
+        if (!ctx || !out) fail("null argument");
+        *out = ctx->p;
+    });
+}
+
 int tfhe_mi355_bootstrap_key_fourier(TfheMi355Context *ctx, void **d_ptr, size_t *bytes) {
     return guarded([&] {
         if (!ctx || !d_ptr || !bytes) fail("null argument");

@@ -33,6 +33,22 @@ class TfheMi355Parameters(ctypes.Structure):
     ]
 
 
+class TfheMi355ServerKeyInfo(ctypes.Structure):
+    _fields_ = [
+        ("params", TfheMi355Parameters),
+        ("pbs_order", ctypes.c_uint32),
+        ("deterministic_execution", ctypes.c_uint32),
+        ("max_degree", ctypes.c_uint64),
+        ("max_noise_level", ctypes.c_uint64),
+        ("ksk_seed_lo", ctypes.c_uint64),
+        ("ksk_seed_hi", ctypes.c_uint64),
+        ("bsk_seed_lo", ctypes.c_uint64),
+        ("bsk_seed_hi", ctypes.c_uint64),
+    ]
+
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+
 # (name, restype, argtypes) -- every symbol declared in include/tfhe_mi355.h
 SIGNATURES = [
     ("tfhe_mi355_last_error", ctypes.c_char_p, []),
@@ -104,6 +120,12 @@ SIGNATURES = [
     ("tfhe_mi355_client_lwe_encrypt", ctypes.c_int,
      [ctypes.c_uint64, u64p, ctypes.c_uint32, u64p, sz, ctypes.c_double, u64p]),
     ("tfhe_mi355_client_lwe_decrypt", ctypes.c_int, [u64p, ctypes.c_uint32, u64p, sz, u64p]),
+    ("tfhe_mi355_context_parameters", ctypes.c_int, [vp, ctypes.POINTER(TfheMi355Parameters)]),
+    ("tfhe_mi355_compressed_server_key_inspect", ctypes.c_int, [u8p, sz, ctypes.POINTER(TfheMi355ServerKeyInfo)]),
+    ("tfhe_mi355_compressed_server_key_upload", ctypes.c_int, [vp, u8p, sz]),
+    ("tfhe_mi355_server_key_inspect", ctypes.c_int, [u8p, sz, ctypes.POINTER(TfheMi355ServerKeyInfo)]),
+    ("tfhe_mi355_server_key_upload", ctypes.c_int, [vp, u8p, sz]),
+    ("tfhe_mi355_fourier_engine_frequency", ctypes.c_int, [ctypes.c_uint32, u32p]),
 ]
 
 _lib = None

@@ -184,6 +184,17 @@ class Engine:
                   L.shape[0], idxp, x.shape[0])
         return out
 
+    def upload_compressed_server_key(self, data: bytes) -> None:
+        """Both keys of a bincode-serialized shortint CompressedServerKey (serialization.py)."""
+        buf = np.frombuffer(data, dtype=np.uint8)
+        _lib.call("tfhe_mi355_compressed_server_key_upload", self._h,
+                  buf.ctypes.data_as(_lib.u8p), buf.size)
+
+    def upload_server_key(self, data: bytes) -> None:
+        """Both keys of a bincode-serialized shortint ServerKey (Fourier BSK, serialization.py)."""
+        buf = np.frombuffer(data, dtype=np.uint8)
+        _lib.call("tfhe_mi355_server_key_upload", self._h, buf.ctypes.data_as(_lib.u8p), buf.size)
+
     def upload_seeded_bootstrap_key(self, bodies: np.ndarray, compression_seed: int) -> None:
         """decompress_seeded_lwe_bootstrap_key on the GPU + Fourier conversion."""
         b = _u64(bodies)

@@ -139,6 +139,17 @@ class ServerKey:
             self.engine.upload_keyswitch_key(ksk)
         self.pbs_order = KEYSWITCH_BOOTSTRAP if p.encryption_key_choice == "Big" else BOOTSTRAP_KEYSWITCH
 
+    @classmethod
+    def deserialize(cls, data: bytes, device: int = 0, parameters: ClassicPBSParameters | None = None) -> "ServerKey":
+        """A bincode-serialized shortint ServerKey (server_key/mod.rs:283-297: standard KSK +
+        Fourier BSK) straight onto the GPU (serialization.py, csrc/serde.cpp)."""
+        from .serialization import inspect_server_key
+
+        p = parameters or inspect_server_key(data).parameters()
+        eng = Engine(p, device)
+        eng.upload_server_key(data)
+        return cls(None, engine=eng, parameters=p)
+
     # -- lookup tables ---------------------------------------------------------------------
     def generate_lookup_table(self, f) -> LookupTable:
         p = self.parameters
@@ -242,6 +253,28 @@ class ServerKey:
     def carry_extract(self, ct: Ciphertext) -> Ciphertext:
         acc = self.generate_lookup_table(lambda x: x // ct.message_modulus)
         return self.apply_lookup_table(ct, acc)
+
+
+class CompressedServerKey:
+    """shortint CompressedServerKey (server_key/compressed.rs:43-55) in its serialized (bincode)
+    form: seeded keyswitching and bootstrapping keys, decompressed on the GPU."""
+
+    def __init__(self, data: bytes):
+        from .serialization import inspect_compressed_server_key
+
+        self.data = bytes(data)
+        self.info = inspect_compressed_server_key(self.data)   # validates the whole buffer
+
+    @classmethod
+    def deserialize(cls, data: bytes) -> "CompressedServerKey":
+        return cls(data)
+
+    def decompress(self, device: int = 0, parameters: ClassicPBSParameters | None = None) -> ServerKey:
+        """CompressedServerKey::decompress (compressed.rs) + the Fourier conversion, on the GPU."""
+        p = parameters or self.info.parameters()
+        eng = Engine(p, device)
+        eng.upload_compressed_server_key(self.data)
+        return ServerKey(None, engine=eng, parameters=p)
 
 
 def gen_keys(parameters: ClassicPBSParameters, seed: int = 0, device: int = 0):
