@@ -138,11 +138,30 @@ def pbs_flops(p) -> float:
     return per * p.lwe_dimension
 
 
+def large_model_bytes(p, chunk: int, with_ks: bool, units: int) -> float:
+    """Algorithmic bytes per PBS of the N = 32768 decomposition: per CMUX and
+    ciphertext the accumulator is read by large_top_fwd and read+written by large_top_inv
+    (3 (k+1) N 8 B), the top-stage spectra T (L (k+1) M 16 B) are written and read once, the
+    sub-block outputs U ((k+1) M 16 B) likewise; GGSW_i (L (k+1)^2 M 16 B) is read once per chunk.
+    Plus the LWE in/out and LUT, and with the keyswitch the KSK once per launch."""
+    M = p.polynomial_size // 2
+    k1 = p.glwe_dimension + 1
+    per_cmux = 3 * k1 * p.polynomial_size * 8 + 2 * p.pbs_level * k1 * M * 16 + 2 * k1 * M * 16
+    per_cmux += p.pbs_level * k1 * k1 * M * 16 / chunk
+    b = p.lwe_dimension * per_cmux + io_bytes(p, with_ks) + 8 * k1 * p.polynomial_size
+    if with_ks:
+        b += 8 * p.glwe_dimension * p.polynomial_size * p.ks_level * (p.lwe_dimension + 1) / units
+    return b
+
+
+PMC_ALIAS = {"mul32": "2_2ks"}  # the multiply DAG runs the 2_2 KS+PBS kernels: per-PBS traffic of that workload
+
+
 def load_pmc(tag: str):
     """Committed rocprofv3 PMC summary of this workload (scripts/pmc_workload.sh ->
     profiles/r02_pmc_<tag>.json): HBM bytes per unit (2*FETCH_SIZE + WRITE_SIZE, gfx950
     correction of MI355X_MICROARCH.md 'HBM') and the SQ VALU-busy fraction."""
-    for name in (f"r02_pmc_{tag}.json",):
+    for name in (f"r02_pmc_{PMC_ALIAS.get(tag, tag)}.json",):
         path = os.path.join(ROOT, "profiles", name)
         if os.path.exists(path):
             d = json.load(open(path))
@@ -173,11 +192,16 @@ def roofline(tag, p, units_per_launch: int, kernel_ms: float, kname: str, with_k
         "traffic_source": pmc["_file"] if pmc else None,
     }
     if p.polynomial_size > 2048:
-        achieved = stream_b * units_per_launch / secs / 1e9
+        chunk = min(units_per_launch, 128)
+        model_b = large_model_bytes(p, chunk, with_ks, units_per_launch)
+        achieved = model_b * units_per_launch / secs / 1e9
         r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-             "model": (f"BSK-streaming bytes (SURVEY.md 8d): {stream_b:,} B per PBS (incl. the keyswitch's "
-                       "KSK and big-LWE input when keyswitched) x PBS per launch / kernel time"),
+             "model": (f"N = 32768 decomposition bytes (DESIGN.md 5.3): {model_b:,.0f} B per PBS (accumulator, "
+                       f"top-stage spectra and sub-block outputs through HBM/MALL every CMUX, GGSW once per chunk "
+                       f"of {chunk}, KSK once per launch) x PBS per launch / kernel time; the PMC traffic "
+                       "(L2<->fabric, Infinity-Cache hits included) is the measured counterpart"),
+             "model_bytes_per_pbs": model_b,
              "fp64": {"achieved": fp64, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                       "frac": fp64 / FP64_PEAK_TFLOPS, "flop_per_pbs": pbs_flops(p)}}
     else:
@@ -186,10 +210,16 @@ def roofline(tag, p, units_per_launch: int, kernel_ms: float, kname: str, with_k
              "model": (f"FP64 flop model (SURVEY.md 8d): {pbs_flops(p):,.0f} flop per PBS x PBS per launch / "
                        "kernel time (HIP events on the launch stream"
                        + (", keyswitch included in the time, its int8 MFMA work not counted)" if with_ks else ")")),
-             "flop_per_pbs": pbs_flops(p),
-             "valu_busy": pmc.get("valu_busy") if pmc else None,
-             "valu_busy_note": ("SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES x waves per SIMD (fraction of each SIMD's "
-                                "issue cycles with a VALU instruction), from the PMC file" if pmc else None)}
+             "flop_per_pbs": pbs_flops(p)}
+        if pmc and "sq_active_inst_valu_per_wave_cycle" in pmc:
+            r["valu_issue"] = {
+                "per_wave_cycle": pmc["sq_active_inst_valu_per_wave_cycle"],
+                "simd_busy_grbm": pmc.get("valu_busy"),
+                "note": ("PMC of the main kernel: SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES per resident wave (x 2 "
+                         "resident waves per SIMD = the fraction of SIMD issue cycles with a VALU instruction); "
+                         "simd_busy_grbm normalises by GRBM_GUI_ACTIVE instead and reads ~0.8x lower (the SQ "
+                         "wave-cycle count implies 1.6 resident waves/SIMD where the launch holds 2)"),
+                "source": pmc["_file"]}
     r["kernel"] = kname
     r["kernel_ms"] = kernel_ms
     r["units_per_launch"] = units_per_launch

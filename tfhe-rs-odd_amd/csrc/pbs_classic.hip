@@ -11,20 +11,22 @@
 //   par_convert_polynomials_list_to_fourier           fft64/math/fft/mod.rs:719-764
 // The fork's PATTERN msgpack dump (bootstrap.rs:340-342) is deliberately not reproduced.
 //
-// Design (DESIGN.md "Kernels"): a workgroup bootstraps CPW ciphertexts (4 at 2_2, else 1),
-// one wavefront per GLWE polynomial ((k+1) waves per ciphertext).  Each wave keeps its
-// accumulator polynomial in registers (u64), rotates it through its LDS buffer, decomposes and
-// forward-FFTs it (row r = its polynomial); the (k+1) spectra of a ciphertext are exchanged
-// through LDS and wave c computes output column c = sum_r F_r * GGSW[r][c] (GGSW streamed from
-// L2/MALL, 16 B per lane, coalesced), inverse-FFTs it and adds it back.  FFT twiddles and the
-// twist live in LDS.  At N = 2048: 2 waves, 256 VGPR + ~106 AGPR (1 wave per SIMD), LDS
-// 31 KiB of tables + 2 x 16 KiB buffers -> 2 ciphertexts per CU.  Wave-private LDS reuse is
-// ordered with wave-local fences; only the spectrum exchange uses workgroup barriers.
+// Design: a workgroup bootstraps CPW ciphertexts (4 at 2_2, else 1), one wavefront
+// per GLWE polynomial ((k+1) waves per ciphertext).  Each wave keeps its accumulator polynomial in
+// registers (u64), rotates it through its LDS buffer, decomposes and forward-FFTs it (row r = its
+// polynomial); the (k+1) row spectra of a ciphertext are published to LDS and wave c computes
+// output column c = sum_r F_r * GGSW[r][c] (GGSW streamed from L2/MALL, 16 B per lane, coalesced;
+// MAC operands read back from LDS at N = 2048 and 1024), inverse-FFTs it and adds it back.  FFT
+// twiddles and the twist live in LDS.  At 2_2: 2 waves per SIMD (<= 256 VGPRs, 232 used), LDS
+// 31 KiB of tables + 8 x 16 KiB exchange buffers + sync flags = 159 KiB -> 4 ciphertexts per CU.
+// Synchronisation: wave-private LDS reuse is ordered with wave-local fences; the spectrum exchange
+// among the (k+1) waves of ONE ciphertext uses LDS flag words (GroupSync, pbs_common.h), so the
+// ciphertexts of a workgroup drift apart instead of running in lockstep behind s_barrier.
 //
-// Control flow is uniform across the workgroup (barriers): a CMUX whose mask element is 0
-// (skipped by the reference, bootstrap.rs:285) is executed as a rotation by 0, which adds
-// exactly 0 to the accumulator (ct1 = 0 -> digits 0 -> spectra +-0 -> increments 0), so the
-// output bits are unchanged.
+// Control flow is uniform within a ciphertext's waves: a CMUX whose mask element is 0 (skipped by
+// the reference, bootstrap.rs:285) is executed as a rotation by 0, which adds exactly 0 to the
+// accumulator (ct1 = 0 -> digits 0 -> spectra +-0 -> increments 0), so the output bits are
+// unchanged.
 #include "engine.h"
 #include "pbs_common.h"
 

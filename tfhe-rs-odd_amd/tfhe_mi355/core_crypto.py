@@ -2,6 +2,7 @@
 
   convert_standard_lwe_bootstrap_key_to_fourier   lwe_bootstrap_key_conversion.rs:21-151
   programmable_bootstrap_lwe_ciphertext           lwe_programmable_bootstrapping.rs:1017-1111
+  multi_bit_programmable_bootstrap_lwe_ciphertext lwe_multi_bit_programmable_bootstrapping.rs:1035-1128
   keyswitch_lwe_ciphertext                        lwe_keyswitch.rs:96-170
 
 Argument meaning and error behaviour follow the reference: output buffers are caller-owned and
@@ -83,6 +84,16 @@ def programmable_bootstrap_lwe_ciphertext_batch(inputs: np.ndarray, accumulators
                                                 fourier_bsk: FourierLweBootstrapKey,
                                                 lut_indexes=None) -> np.ndarray:
     return fourier_bsk.engine.programmable_bootstrap(inputs, accumulators, lut_indexes)
+
+
+def multi_bit_programmable_bootstrap_lwe_ciphertext(input_ct: np.ndarray, output_ct: np.ndarray,
+                                                    accumulator: np.ndarray, multi_bit_bsk: FourierLweBootstrapKey,
+                                                    thread_count: int = 0) -> None:
+    """The multi-bit PBS (deterministic group order); `thread_count` is accepted for signature
+    parity with the reference and ignored (the GPU kernel fuses the keybundle producers)."""
+    if not multi_bit_bsk.engine.params.grouping_factor:
+        raise ValueError("multi_bit_programmable_bootstrap_lwe_ciphertext needs a multi-bit key")
+    programmable_bootstrap_lwe_ciphertext(input_ct, output_ct, accumulator, multi_bit_bsk)
 
 
 def keyswitch_lwe_ciphertext(ksk: LweKeyswitchKey, input_ct: np.ndarray, output_ct: np.ndarray) -> None:
