@@ -285,6 +285,237 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
     }
 }
 
+#ifndef PBS_MB_SHARED
+#define PBS_MB_SHARED 1  // slot-split MAC phase: each GGSW element is loaded once per workgroup
+#endif
+
+// Slot-split variant (PBS_MB_SHARED, L = 1).  The kernel above streams every GGSW column once per
+// ciphertext: 2^g (k+1)^2 M 16 B = 512 KiB per group and ciphertext at g = 3 (155 MB per PBS) from
+// L2/MALL -- ~20 TB/s of L2->CU traffic at 128k PBS/s, and its waves wait on it (PMC: s_waitcnt
+// 0.48 of wave cycles, VALU 0.26).  Here the CPW ciphertexts of a workgroup share each load:
+//   phase 1  wave (ct, r): digits of its accumulator row, twist, forward FFT, publish F_ct[r]
+//   phase 2  wave w owns spectrum slots s = w SPW .. w SPW + SPW-1 for EVERY ciphertext and
+//            column: it loads G[sel][r][c][s] once and builds KB_ct and the MAC for each of the
+//            CPW ciphertexts (their monomials differ), writing out_ct[c][s] over F_ct[c][s] (no
+//            other wave touches slot s)
+//   phase 3  wave (ct, c): inverse FFT of out_ct[c], backward conversion into its accumulator
+// Two workgroup barriers per group.  Per (ciphertext, column, frequency) the arithmetic and its
+// order are those of the kernel above (keybundle in selector order, MAC over rows in order), so
+// the outputs are bit-identical; a ciphertext's GGSW traffic drops by CPW (4x).
+template <int N, int K, int L, int G>
+__global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
+    pbs_multibit_shared_kernel(MultiBitPbsLaunch a) {
+    static_assert(L == 1, "slot-split kernel: one decomposition level (every multi-bit set)");
+    constexpr int CPW = PBS_MB_CPW;
+    constexpr int W = (K + 1) * CPW;  // waves per workgroup
+    constexpr int M = N / 2;
+    constexpr int V = M / 64;
+    static_assert(V % W == 0, "spectrum slots split evenly over the waves");
+    constexpr int SPW = V / W;        // slots per wave in phase 2
+    constexpr int LOG2N = ilog2(N);
+    constexpr int LOG2M = LOG2N - 1;
+    constexpr int NSEL = 1 << G;
+    using Fft = WaveFft<M>;
+    using Lay = PbsLds<M>;
+    constexpr int XL = Lay::XL;
+    static_assert(sizeof(cx) * XL >= sizeof(uint64_t) * N, "exchange buffer holds one polynomial");
+    static_assert(Lay::twist_off == 0, "twist table at LDS offset 0");
+
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double2 *lds = reinterpret_cast<double2 *>(smem);
+    const double2 *s_twist = lds + Lay::twist_off;
+
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wave = wid % (K + 1);  // row in phase 1, column in phase 3
+    const int slot = wid / (K + 1);  // this wave's ciphertext in phases 1 and 3
+    const int lane0 = threadIdx.x & 63;
+    const int n = a.n;
+    const int beta = a.base_log;
+    const int dk1 = 31 - beta;
+    const uint32_t dc1 = (1u << beta) - 1;
+    const int32_t dh1 = (int32_t)(1u << (beta - 1)) - 1;
+    WaveLocalSync wsync;
+
+    for (int e = threadIdx.x; e < M; e += blockDim.x) lds[Lay::twist_off + e] = a.twist[e];
+    Fft::Lds::template fill<M>(lds + Lay::s1_off, lds + Lay::s2_off, a.W, threadIdx.x, blockDim.x);
+    const typename Fft::Lds tw{lds + Lay::s1_off, lds + Lay::s2_off};
+    __syncthreads();
+
+    cx *xbuf = reinterpret_cast<cx *>(lds + Lay::xbuf_off);  // buffer (ct, p) at (ct (K+1) + p) XL
+    cx *xb = xbuf + (size_t)wid * XL;
+    uint64_t *xb64 = reinterpret_cast<uint64_t *>(xb);
+    // every ciphertext of the workgroup (idle slots compute on a valid one and store nothing)
+    const int ct_raw = blockIdx.x * CPW + slot;
+    const bool active = ct_raw < a.count;
+    const int ct = active ? ct_raw : a.count - 1;
+    const uint64_t *in = a.lwe_in + (size_t)ct * (n + 1);
+    const uint32_t li = a.lut_indexes ? min(a.lut_indexes[ct], a.lut_count - 1u) : 0u;
+    const uint64_t *lut = a.luts + (size_t)li * (K + 1) * N + (size_t)wave * N;
+
+    uint64_t c0[2 * V];  // this wave's accumulator polynomial (row = wave), position lane + 64 h
+    {
+        const uint32_t bt = pbs_modulus_switch<LOG2N>(in[n]);
+        const int full = bt / N, rem = bt % N;
+#pragma unroll
+        for (int h = 0; h < 2 * V; h++) {
+            const int src = lane0 + 64 * h + rem;
+            const bool wrap = src >= N;
+            uint64_t v = lut[wrap ? src - N : src];
+            c0[h] = (wrap != (bool)(full & 1)) ? 0 - v : v;
+        }
+    }
+
+    constexpr size_t ggsw_len = (size_t)(K + 1) * (K + 1) * M;  // L = 1
+    const __amdgpu_buffer_rsrc_t gres = make_rsrc(a.fbsk);
+    const int groups = n / G;
+    const double k32 = torus_k32();
+    const int s0 = wid * SPW;  // phase-2 slots of this wave (wave-uniform)
+
+    for (int j = 0; j < groups; j++) {
+        int lane = lane0;
+        asm volatile("" : "+v"(lane));
+        // ---- phase 1: forward FFT of row `wave` of ciphertext `slot`, published to xb ----
+        {
+            cx v[V];
+#pragma unroll
+            for (int b = 0; b < V; b++) {
+                const int32_t d0 = digit_l1((uint32_t)(c0[b] >> 32), dk1, dc1, beta, dh1);
+                const int32_t d1 = digit_l1((uint32_t)(c0[V + b] >> 32), dk1, dc1, beta, dh1);
+                const double2 w = s_twist[lane + 64 * b];
+                v[b] = cmulw(cx{(double)d0, (double)d1}, w.x, w.y);
+            }
+            Fft::forward(v, xb, tw, lane, wsync);
+            wsync();
+#pragma unroll
+            for (int s = 0; s < V; s++) reinterpret_cast<double2 *>(xb)[s * 64 + lane] = make_double2(v[s].re, v[s].im);
+        }
+        __syncthreads();
+        // ---- phase 2: keybundle + MAC of slots s0 .. s0+SPW-1 for every ciphertext ----
+        {
+            // monomial degrees of the 2^g - 1 non-constant GGSWs of each ciphertext (:700-716)
+            // (16 d, wave-uniform: scalar loads through the constant address space -> SGPRs)
+            uint32_t d16[CPW][NSEL];
+#pragma unroll
+            for (int c = 0; c < CPW; c++) {
+                const int ctc = min((int)blockIdx.x * CPW + c, a.count - 1);
+                const __attribute__((address_space(4))) uint64_t *inc =
+                    (const __attribute__((address_space(4))) uint64_t *)(a.lwe_in + (size_t)ctc * (n + 1) + (size_t)j * G);
+                uint64_t av[G];
+#pragma unroll
+                for (int i = 0; i < G; i++) av[i] = inc[i];
+#pragma unroll
+                for (int sel = 1; sel < NSEL; sel++) {
+                    uint64_t deg = 0;
+#pragma unroll
+                    for (int i = 0; i < G; i++)
+                        if ((sel >> (G - 1 - i)) & 1) deg += av[i];
+                    d16[c][sel] = 16u * pbs_modulus_switch<LOG2N>(deg);
+                }
+            }
+            const uint32_t fl = Fft::freq_lane(lane);
+            const uint32_t loff = 16u * (uint32_t)lane;
+#pragma unroll
+            for (int i = 0; i < SPW; i++) {
+                const int s = s0 + i;
+                // 4 f, f = freq_lane + freq_slot(s) < M: t = d (1 - 4 f) mod 2N as 16 t = 16 d - 16 d (4 f)
+                const uint32_t f4 = 4u * (fl + 16u * (uint32_t)(s >> 2) + 256u * (uint32_t)(s & 3));
+                // out_c[col][s] overwrites F_c[col][s] (slot s is this wave's), so each column's
+                // results wait in registers until every column of slot s has read the F values
+                double2 O[CPW][K + 1];
+#pragma unroll
+                for (int col = 0; col <= K; col++) {
+                    __builtin_amdgcn_sched_barrier(0);  // one column's GGSW operands in flight at a time
+                    const uint32_t soff = (uint32_t)(((size_t)j * NSEL * ggsw_len + (size_t)col * M + (size_t)s * 64) * 16);
+                    double2 g[K + 1][NSEL];
+#pragma unroll
+                    for (int r = 0; r <= K; r++)
+#pragma unroll
+                        for (int sel = 0; sel < NSEL; sel++)
+                            g[r][sel] = buffer_ld_d2(gres, loff,
+                                                     soff + (uint32_t)(((size_t)sel * ggsw_len + (size_t)r * (K + 1) * M) * 16));
+#pragma unroll
+                    for (int c = 0; c < CPW; c++) {
+                        if (c) __builtin_amdgcn_sched_barrier(0);  // one ciphertext's monomials live at a time
+                        // monomial spectra of ciphertext c at frequency f: i^q twist[r], t = q M + r
+                        cx mono[NSEL];
+#pragma unroll
+                        for (int sel = 1; sel < NSEL; sel++) {
+                            const uint32_t t16 = d16[c][sel] - __umul24(d16[c][sel], f4);  // operands < 2^24
+                            const uint32_t are = (t16 & (uint32_t)(16 * M - 16)) | ((t16 >> (LOG2M + 1)) & 8u);
+                            const double re = lds_ld_f64(are), im = lds_ld_f64(are ^ 8u);
+                            const uint32_t sim = t16 << (31 - (LOG2M + 5));
+                            mono[sel].re = flip_sign(re, sim + 0x40000000u);
+                            mono[sel].im = flip_sign(im, sim);
+                        }
+                        cx o{0.0, 0.0};
+#pragma unroll
+                        for (int r = 0; r <= K; r++) {
+                            double2 kb = g[r][0];
+#pragma unroll
+                            for (int sel = 1; sel < NSEL; sel++) {
+                                const double2 gg = g[r][sel];
+                                kb.x = fma(gg.x, mono[sel].re, fma(-gg.y, mono[sel].im, kb.x));
+                                kb.y = fma(gg.x, mono[sel].im, fma(gg.y, mono[sel].re, kb.y));
+                            }
+                            const double2 ff = reinterpret_cast<const double2 *>(xbuf + (size_t)(c * (K + 1) + r) * XL)[s * 64 + lane];
+                            if (r == 0) {
+                                o.re = fma(kb.x, ff.x, -(kb.y * ff.y));
+                                o.im = fma(kb.x, ff.y, kb.y * ff.x);
+                            } else {
+                                o.re = fma(kb.x, ff.x, fma(-kb.y, ff.y, o.re));
+                                o.im = fma(kb.x, ff.y, fma(kb.y, ff.x, o.im));
+                            }
+                        }
+                        O[c][col] = make_double2(o.re, o.im);
+                        if (col == K) {  // the last column has read F_c[.][s]: ciphertext c's slot s is free
+#pragma unroll
+                            for (int cc = 0; cc <= K; cc++)
+                                reinterpret_cast<double2 *>(xbuf + (size_t)(c * (K + 1) + cc) * XL)[s * 64 + lane] = O[c][cc];
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // ---- phase 3: inverse FFT of column `wave` of ciphertext `slot`, into the accumulator ----
+        {
+            cx v[V];
+#pragma unroll
+            for (int s = 0; s < V; s++) {
+                const double2 t = reinterpret_cast<const double2 *>(xb)[s * 64 + lane];
+                v[s] = cx{t.x, t.y};
+            }
+            wsync();
+            Fft::inverse(v, xb, tw, lane, wsync);
+#pragma unroll
+            for (int b = 0; b < V; b++) {
+                const double2 w = s_twist[lane + 64 * b];  // the resident key carries the 1/M
+                backward_convert(v[b], cx{w.x, w.y}, c0[b], c0[V + b], k32);
+            }
+        }
+    }
+
+    if (a.glwe_out) {  // bootstrap_without_sample_extract (fork, bootstrap.rs:383-412)
+        if (!active) return;
+        uint64_t *g = a.lwe_out + ((size_t)ct * (K + 1) + wave) * N;
+#pragma unroll
+        for (int h = 0; h < 2 * V; h++) g[lane0 + 64 * h] = c0[h];
+        return;
+    }
+    // sample extract at degree 0 (glwe_sample_extraction.rs:91-147)
+    wsync();
+#pragma unroll
+    for (int h = 0; h < 2 * V; h++) xb64[lane0 + 64 * h] = c0[h];
+    wsync();
+    if (!active) return;
+    uint64_t *out = a.lwe_out + (size_t)ct * (K * N + 1);
+    if (wave < K) {
+        for (int jj = lane0; jj < N; jj += 64) out[wave * N + jj] = jj == 0 ? xb64[0] : 0 - xb64[N - jj];
+    } else if (lane0 == 0) {
+        out[K * N] = c0[0];
+    }
+}
+
 template <int N, int K, int L, int G>
 static hipError_t launch_mb_t(const MultiBitPbsLaunch &a, hipStream_t s) {
     constexpr int M = N / 2;
@@ -293,7 +524,10 @@ static hipError_t launch_mb_t(const MultiBitPbsLaunch &a, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
     if (a.n % G) return hipErrorInvalidValue;
     const int blocks = (a.count + PBS_MB_CPW - 1) / PBS_MB_CPW;
-    hipLaunchKernelGGL((pbs_multibit_kernel<N, K, L, G>), dim3(blocks), dim3(64 * (K + 1) * PBS_MB_CPW), lds, s, a);
+    if constexpr (PBS_MB_SHARED && L == 1)
+        hipLaunchKernelGGL((pbs_multibit_shared_kernel<N, K, L, G>), dim3(blocks), dim3(64 * (K + 1) * PBS_MB_CPW), lds, s, a);
+    else
+        hipLaunchKernelGGL((pbs_multibit_kernel<N, K, L, G>), dim3(blocks), dim3(64 * (K + 1) * PBS_MB_CPW), lds, s, a);
     return hipGetLastError();
 }
 
