@@ -288,6 +288,10 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
 #ifndef PBS_MB_SHARED
 #define PBS_MB_SHARED 1  // slot-split MAC phase: each GGSW element is loaded once per workgroup
 #endif
+#ifndef PBS_MB_RSPLIT
+#define PBS_MB_RSPLIT 0  // 1: phase 2 loads one GGSW row at a time, monomials rebuilt per row (no spills at g = 3,
+                          // but measured slower: g3 141.1k -> 97.7k, g2 158.4k -> 120.0k PBS/s)
+#endif
 
 // Slot-split variant (PBS_MB_SHARED, L = 1).  The kernel above streams every GGSW column once per
 // ciphertext: 2^g (k+1)^2 M 16 B = 512 KiB per group and ciphertext at g = 3 (155 MB per PBS) from
@@ -312,6 +316,9 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
     constexpr int V = M / 64;
     static_assert(V % W == 0, "spectrum slots split evenly over the waves");
     constexpr int SPW = V / W;        // slots per wave in phase 2
+    // both rows' 2^g GGSW operands (2^g (k+1) double2) plus the accumulator need ~256 VGPRs at g = 3
+    // (11 spilled); the row-split alternative rebuilds the monomials per row and is slower
+    constexpr bool RSPLIT = (bool)PBS_MB_RSPLIT;
     constexpr int LOG2N = ilog2(N);
     constexpr int LOG2M = LOG2N - 1;
     constexpr int NSEL = 1 << G;
@@ -422,50 +429,77 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
                 // out_c[col][s] overwrites F_c[col][s] (slot s is this wave's), so each column's
                 // results wait in registers until every column of slot s has read the F values
                 double2 O[CPW][K + 1];
+                // monomial spectra of ciphertext c at frequency f: i^q twist[r], t = q M + r
+                auto monomials = [&](int c, cx(&mono)[NSEL]) {
+#pragma unroll
+                    for (int sel = 1; sel < NSEL; sel++) {
+                        const uint32_t t16 = d16[c][sel] - __umul24(d16[c][sel], f4);  // operands < 2^24
+                        const uint32_t are = (t16 & (uint32_t)(16 * M - 16)) | ((t16 >> (LOG2M + 1)) & 8u);
+                        const double re = lds_ld_f64(are), im = lds_ld_f64(are ^ 8u);
+                        const uint32_t sim = t16 << (31 - (LOG2M + 5));
+                        mono[sel].re = flip_sign(re, sim + 0x40000000u);
+                        mono[sel].im = flip_sign(im, sim);
+                    }
+                };
+                // KB[r][col] at this frequency (keybundle, oracle mb_keybundle order) into o (MAC over rows)
+                auto mac_row = [&](int c, int r, const double2 (&g)[NSEL], const cx (&mono)[NSEL], cx &o) {
+                    double2 kb = g[0];
+#pragma unroll
+                    for (int sel = 1; sel < NSEL; sel++) {
+                        const double2 gg = g[sel];
+                        kb.x = fma(gg.x, mono[sel].re, fma(-gg.y, mono[sel].im, kb.x));
+                        kb.y = fma(gg.x, mono[sel].im, fma(gg.y, mono[sel].re, kb.y));
+                    }
+                    const double2 ff = reinterpret_cast<const double2 *>(xbuf + (size_t)(c * (K + 1) + r) * XL)[s * 64 + lane];
+                    if (r == 0) {
+                        o.re = fma(kb.x, ff.x, -(kb.y * ff.y));
+                        o.im = fma(kb.x, ff.y, kb.y * ff.x);
+                    } else {
+                        o.re = fma(kb.x, ff.x, fma(-kb.y, ff.y, o.re));
+                        o.im = fma(kb.x, ff.y, fma(kb.y, ff.x, o.im));
+                    }
+                };
 #pragma unroll
                 for (int col = 0; col <= K; col++) {
-                    __builtin_amdgcn_sched_barrier(0);  // one column's GGSW operands in flight at a time
                     const uint32_t soff = (uint32_t)(((size_t)j * NSEL * ggsw_len + (size_t)col * M + (size_t)s * 64) * 16);
-                    double2 g[K + 1][NSEL];
-#pragma unroll
-                    for (int r = 0; r <= K; r++)
+                    auto load_g = [&](int r, double2(&g)[NSEL]) {
 #pragma unroll
                         for (int sel = 0; sel < NSEL; sel++)
-                            g[r][sel] = buffer_ld_d2(gres, loff,
-                                                     soff + (uint32_t)(((size_t)sel * ggsw_len + (size_t)r * (K + 1) * M) * 16));
-#pragma unroll
-                    for (int c = 0; c < CPW; c++) {
-                        if (c) __builtin_amdgcn_sched_barrier(0);  // one ciphertext's monomials live at a time
-                        // monomial spectra of ciphertext c at frequency f: i^q twist[r], t = q M + r
-                        cx mono[NSEL];
-#pragma unroll
-                        for (int sel = 1; sel < NSEL; sel++) {
-                            const uint32_t t16 = d16[c][sel] - __umul24(d16[c][sel], f4);  // operands < 2^24
-                            const uint32_t are = (t16 & (uint32_t)(16 * M - 16)) | ((t16 >> (LOG2M + 1)) & 8u);
-                            const double re = lds_ld_f64(are), im = lds_ld_f64(are ^ 8u);
-                            const uint32_t sim = t16 << (31 - (LOG2M + 5));
-                            mono[sel].re = flip_sign(re, sim + 0x40000000u);
-                            mono[sel].im = flip_sign(im, sim);
-                        }
-                        cx o{0.0, 0.0};
+                            g[sel] = buffer_ld_d2(gres, loff, soff + (uint32_t)(((size_t)sel * ggsw_len + (size_t)r * (K + 1) * M) * 16));
+                    };
+                    cx oc[CPW];
+                    if constexpr (RSPLIT) {
+                        // one row's 2^g GGSW operands live at a time; the monomials are rebuilt per row
 #pragma unroll
                         for (int r = 0; r <= K; r++) {
-                            double2 kb = g[r][0];
+                            __builtin_amdgcn_sched_barrier(0);
+                            double2 g[NSEL];
+                            load_g(r, g);
 #pragma unroll
-                            for (int sel = 1; sel < NSEL; sel++) {
-                                const double2 gg = g[r][sel];
-                                kb.x = fma(gg.x, mono[sel].re, fma(-gg.y, mono[sel].im, kb.x));
-                                kb.y = fma(gg.x, mono[sel].im, fma(gg.y, mono[sel].re, kb.y));
-                            }
-                            const double2 ff = reinterpret_cast<const double2 *>(xbuf + (size_t)(c * (K + 1) + r) * XL)[s * 64 + lane];
-                            if (r == 0) {
-                                o.re = fma(kb.x, ff.x, -(kb.y * ff.y));
-                                o.im = fma(kb.x, ff.y, kb.y * ff.x);
-                            } else {
-                                o.re = fma(kb.x, ff.x, fma(-kb.y, ff.y, o.re));
-                                o.im = fma(kb.x, ff.y, fma(kb.y, ff.x, o.im));
+                            for (int c = 0; c < CPW; c++) {
+                                if (c) __builtin_amdgcn_sched_barrier(0);
+                                cx mono[NSEL];
+                                monomials(c, mono);
+                                mac_row(c, r, g, mono, oc[c]);
                             }
                         }
+                    } else {
+                        __builtin_amdgcn_sched_barrier(0);  // one column's GGSW operands in flight at a time
+                        double2 g[K + 1][NSEL];
+#pragma unroll
+                        for (int r = 0; r <= K; r++) load_g(r, g[r]);
+#pragma unroll
+                        for (int c = 0; c < CPW; c++) {
+                            if (c) __builtin_amdgcn_sched_barrier(0);  // one ciphertext's monomials live at a time
+                            cx mono[NSEL];
+                            monomials(c, mono);
+#pragma unroll
+                            for (int r = 0; r <= K; r++) mac_row(c, r, g[r], mono, oc[c]);
+                        }
+                    }
+#pragma unroll
+                    for (int c = 0; c < CPW; c++) {
+                        const cx o = oc[c];
                         O[c][col] = make_double2(o.re, o.im);
                         if (col == K) {  // the last column has read F_c[.][s]: ciphertext c's slot s is free
 #pragma unroll
