@@ -319,6 +319,13 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
     // both rows' 2^g GGSW operands (2^g (k+1) double2) plus the accumulator need ~256 VGPRs at g = 3
     // (11 spilled); the row-split alternative rebuilds the monomials per row and is slower
     constexpr bool RSPLIT = (bool)PBS_MB_RSPLIT;
+    // every GGSW operand of a slot ((k+1)^2 2^g double2: 64 / 128 VGPRs at g = 2 / 3) loaded
+    // together, so each ciphertext's monomials are built once per slot for both columns (the
+    // compiler streams them: 219 VGPRs at g = 3 without spills, where the per-column form spills 11)
+#ifndef PBS_MB_BOTHCOL
+#define PBS_MB_BOTHCOL 1
+#endif
+    constexpr bool BOTHCOL = PBS_MB_BOTHCOL && (K + 1) * (K + 1) * (1 << G) <= 32;
     constexpr int LOG2N = ilog2(N);
     constexpr int LOG2M = LOG2N - 1;
     constexpr int NSEL = 1 << G;
@@ -459,6 +466,37 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
                         o.im = fma(kb.x, ff.y, fma(kb.y, ff.x, o.im));
                     }
                 };
+                if constexpr (BOTHCOL) {
+                    // every GGSW operand of slot s (both columns) in registers: each ciphertext's
+                    // monomials are built once and serve both columns
+                    double2 g[K + 1][K + 1][NSEL];
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int col = 0; col <= K; col++)
+#pragma unroll
+                        for (int r = 0; r <= K; r++)
+#pragma unroll
+                            for (int sel = 0; sel < NSEL; sel++)
+                                g[col][r][sel] = buffer_ld_d2(
+                                    gres, loff,
+                                    (uint32_t)((((size_t)j * NSEL + sel) * ggsw_len + (size_t)r * (K + 1) * M + (size_t)col * M +
+                                                (size_t)s * 64) * 16));
+#pragma unroll
+                    for (int c = 0; c < CPW; c++) {
+                        if (c) __builtin_amdgcn_sched_barrier(0);
+                        cx mono[NSEL];
+                        monomials(c, mono);
+                        cx oc[K + 1];
+#pragma unroll
+                        for (int col = 0; col <= K; col++)
+#pragma unroll
+                            for (int r = 0; r <= K; r++) mac_row(c, r, g[col][r], mono, oc[col]);
+#pragma unroll
+                        for (int col = 0; col <= K; col++)
+                            reinterpret_cast<double2 *>(xbuf + (size_t)(c * (K + 1) + col) * XL)[s * 64 + lane] =
+                                make_double2(oc[col].re, oc[col].im);
+                    }
+                } else
 #pragma unroll
                 for (int col = 0; col <= K; col++) {
                     const uint32_t soff = (uint32_t)(((size_t)j * NSEL * ggsw_len + (size_t)col * M + (size_t)s * 64) * 16);
