@@ -288,10 +288,6 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
 #ifndef PBS_MB_SHARED
 #define PBS_MB_SHARED 1  // slot-split MAC phase: each GGSW element is loaded once per workgroup
 #endif
-#ifndef PBS_MB_RSPLIT
-#define PBS_MB_RSPLIT 0  // 1: phase 2 loads one GGSW row at a time, monomials rebuilt per row (no spills at g = 3,
-                          // but measured slower: g3 141.1k -> 97.7k, g2 158.4k -> 120.0k PBS/s)
-#endif
 
 // Slot-split variant (PBS_MB_SHARED, L = 1).  The kernel above streams every GGSW column once per
 // ciphertext: 2^g (k+1)^2 M 16 B = 512 KiB per group and ciphertext at g = 3 (155 MB per PBS) from
@@ -316,19 +312,10 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
     constexpr int V = M / 64;
     static_assert(V % W == 0, "spectrum slots split evenly over the waves");
     constexpr int SPW = V / W;        // slots per wave in phase 2
-    // both rows' 2^g GGSW operands (2^g (k+1) double2) plus the accumulator need ~256 VGPRs at g = 3
-    // (11 spilled); the row-split alternative rebuilds the monomials per row and is slower
-    constexpr bool RSPLIT = (bool)PBS_MB_RSPLIT;
-    // every GGSW operand of a slot ((k+1)^2 2^g double2: 64 / 128 VGPRs at g = 2 / 3) loaded
-    // together, so each ciphertext's monomials are built once per slot for both columns (the
-    // compiler streams them: 219 VGPRs at g = 3 without spills, where the per-column form spills 11)
-#ifndef PBS_MB_BOTHCOL
-#define PBS_MB_BOTHCOL 1
-#endif
-    constexpr bool BOTHCOL = PBS_MB_BOTHCOL && (K + 1) * (K + 1) * (1 << G) <= 32;
     constexpr int LOG2N = ilog2(N);
     constexpr int LOG2M = LOG2N - 1;
     constexpr int NSEL = 1 << G;
+    static_assert((K + 1) * (K + 1) * NSEL <= 32, "a slot's GGSW operands must fit the register budget");
     using Fft = WaveFft<M>;
     using Lay = PbsLds<M>;
     constexpr int XL = Lay::XL;
@@ -403,147 +390,102 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
 #pragma unroll
             for (int s = 0; s < V; s++) reinterpret_cast<double2 *>(xb)[s * 64 + lane] = make_double2(v[s].re, v[s].im);
         }
-        __syncthreads();
         // ---- phase 2: keybundle + MAC of slots s0 .. s0+SPW-1 for every ciphertext ----
-        {
-            // monomial degrees of the 2^g - 1 non-constant GGSWs of each ciphertext (:700-716)
-            // (16 d, wave-uniform: scalar loads through the constant address space -> SGPRs)
-            uint32_t d16[CPW][NSEL];
+        // Every GGSW operand of a slot ((k+1)^2 2^g double2: 64 / 128 VGPRs at g = 2 / 3) is held
+        // at once, so each ciphertext's monomials are built once per slot for both columns.  The
+        // first slot's operands and the mask elements are loaded BEFORE the barrier that publishes
+        // the row spectra (they do not depend on it), so their latency hides behind the wait.
+        const uint32_t loff = 16u * (uint32_t)lane;
+        double2 g[K + 1][K + 1][NSEL];
+        auto load_slot = [&](int s) {
 #pragma unroll
-            for (int c = 0; c < CPW; c++) {
-                const int ctc = min((int)blockIdx.x * CPW + c, a.count - 1);
-                const __attribute__((address_space(4))) uint64_t *inc =
-                    (const __attribute__((address_space(4))) uint64_t *)(a.lwe_in + (size_t)ctc * (n + 1) + (size_t)j * G);
-                uint64_t av[G];
+            for (int col = 0; col <= K; col++)
 #pragma unroll
-                for (int i = 0; i < G; i++) av[i] = inc[i];
+                for (int r = 0; r <= K; r++)
 #pragma unroll
-                for (int sel = 1; sel < NSEL; sel++) {
-                    uint64_t deg = 0;
+                    for (int sel = 0; sel < NSEL; sel++)
+                        g[col][r][sel] = buffer_ld_d2(gres, loff,
+                                                      (uint32_t)((((size_t)j * NSEL + sel) * ggsw_len + (size_t)r * (K + 1) * M +
+                                                                  (size_t)col * M + (size_t)s * 64) * 16));
+        };
+        load_slot(s0);
+        // monomial degrees d of the 2^g - 1 non-constant GGSWs of each ciphertext (:700-716),
+        // wave-uniform: scalar loads through the constant address space -> SGPRs
+        int32_t dd[CPW][NSEL];
 #pragma unroll
-                    for (int i = 0; i < G; i++)
-                        if ((sel >> (G - 1 - i)) & 1) deg += av[i];
-                    d16[c][sel] = 16u * pbs_modulus_switch<LOG2N>(deg);
-                }
+        for (int c = 0; c < CPW; c++) {
+            const int ctc = min((int)blockIdx.x * CPW + c, a.count - 1);
+            const __attribute__((address_space(4))) uint64_t *inc =
+                (const __attribute__((address_space(4))) uint64_t *)(a.lwe_in + (size_t)ctc * (n + 1) + (size_t)j * G);
+            uint64_t av[G];
+#pragma unroll
+            for (int i = 0; i < G; i++) av[i] = inc[i];
+#pragma unroll
+            for (int sel = 1; sel < NSEL; sel++) {
+                uint64_t deg = 0;
+#pragma unroll
+                for (int i = 0; i < G; i++)
+                    if ((sel >> (G - 1 - i)) & 1) deg += av[i];
+                dd[c][sel] = (int32_t)pbs_modulus_switch<LOG2N>(deg);  // <= 2N
             }
-            const uint32_t fl = Fft::freq_lane(lane);
-            const uint32_t loff = 16u * (uint32_t)lane;
+        }
+        __syncthreads();
+        {
+            const int32_t fl = (int32_t)Fft::freq_lane(lane);
 #pragma unroll
             for (int i = 0; i < SPW; i++) {
                 const int s = s0 + i;
-                // 4 f, f = freq_lane + freq_slot(s) < M: t = d (1 - 4 f) mod 2N as 16 t = 16 d - 16 d (4 f)
-                const uint32_t f4 = 4u * (fl + 16u * (uint32_t)(s >> 2) + 256u * (uint32_t)(s & 3));
-                // out_c[col][s] overwrites F_c[col][s] (slot s is this wave's), so each column's
-                // results wait in registers until every column of slot s has read the F values
-                double2 O[CPW][K + 1];
-                // monomial spectra of ciphertext c at frequency f: i^q twist[r], t = q M + r
-                auto monomials = [&](int c, cx(&mono)[NSEL]) {
+                if (i) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    load_slot(s);
+                }
+                // t = d (1 - 4 f) mod 2N, f = freq_lane + freq_slot(s) < M: |1 - 4 f| < 2^12 and
+                // d <= 2^12, so a 24-bit signed multiply is exact; 16 t mod 2^32 is a shift of it
+                const int32_t w = 1 - 4 * (fl + 16 * (s >> 2) + 256 * (s & 3));
+#pragma unroll
+                for (int c = 0; c < CPW; c++) {
+                    if (c) __builtin_amdgcn_sched_barrier(0);  // one ciphertext's monomials live at a time
+                    // monomial spectra of ciphertext c at frequency f: i^q twist[r], t = q M + r
+                    cx mono[NSEL];
 #pragma unroll
                     for (int sel = 1; sel < NSEL; sel++) {
-                        const uint32_t t16 = d16[c][sel] - __umul24(d16[c][sel], f4);  // operands < 2^24
+                        const uint32_t t16 = (uint32_t)__mul24(dd[c][sel], w) << 4;
                         const uint32_t are = (t16 & (uint32_t)(16 * M - 16)) | ((t16 >> (LOG2M + 1)) & 8u);
                         const double re = lds_ld_f64(are), im = lds_ld_f64(are ^ 8u);
                         const uint32_t sim = t16 << (31 - (LOG2M + 5));
                         mono[sel].re = flip_sign(re, sim + 0x40000000u);
                         mono[sel].im = flip_sign(im, sim);
                     }
-                };
-                // KB[r][col] at this frequency (keybundle, oracle mb_keybundle order) into o (MAC over rows)
-                auto mac_row = [&](int c, int r, const double2 (&g)[NSEL], const cx (&mono)[NSEL], cx &o) {
-                    double2 kb = g[0];
+                    double2 ff[K + 1];
 #pragma unroll
-                    for (int sel = 1; sel < NSEL; sel++) {
-                        const double2 gg = g[sel];
-                        kb.x = fma(gg.x, mono[sel].re, fma(-gg.y, mono[sel].im, kb.x));
-                        kb.y = fma(gg.x, mono[sel].im, fma(gg.y, mono[sel].re, kb.y));
-                    }
-                    const double2 ff = reinterpret_cast<const double2 *>(xbuf + (size_t)(c * (K + 1) + r) * XL)[s * 64 + lane];
-                    if (r == 0) {
-                        o.re = fma(kb.x, ff.x, -(kb.y * ff.y));
-                        o.im = fma(kb.x, ff.y, kb.y * ff.x);
-                    } else {
-                        o.re = fma(kb.x, ff.x, fma(-kb.y, ff.y, o.re));
-                        o.im = fma(kb.x, ff.y, fma(kb.y, ff.x, o.im));
-                    }
-                };
-                if constexpr (BOTHCOL) {
-                    // every GGSW operand of slot s (both columns) in registers: each ciphertext's
-                    // monomials are built once and serve both columns
-                    double2 g[K + 1][K + 1][NSEL];
-                    __builtin_amdgcn_sched_barrier(0);
+                    for (int r = 0; r <= K; r++)
+                        ff[r] = reinterpret_cast<const double2 *>(xbuf + (size_t)(c * (K + 1) + r) * XL)[s * 64 + lane];
 #pragma unroll
-                    for (int col = 0; col <= K; col++)
-#pragma unroll
-                        for (int r = 0; r <= K; r++)
-#pragma unroll
-                            for (int sel = 0; sel < NSEL; sel++)
-                                g[col][r][sel] = buffer_ld_d2(
-                                    gres, loff,
-                                    (uint32_t)((((size_t)j * NSEL + sel) * ggsw_len + (size_t)r * (K + 1) * M + (size_t)col * M +
-                                                (size_t)s * 64) * 16));
-#pragma unroll
-                    for (int c = 0; c < CPW; c++) {
-                        if (c) __builtin_amdgcn_sched_barrier(0);
-                        cx mono[NSEL];
-                        monomials(c, mono);
-                        cx oc[K + 1];
-#pragma unroll
-                        for (int col = 0; col <= K; col++)
-#pragma unroll
-                            for (int r = 0; r <= K; r++) mac_row(c, r, g[col][r], mono, oc[col]);
-#pragma unroll
-                        for (int col = 0; col <= K; col++)
-                            reinterpret_cast<double2 *>(xbuf + (size_t)(c * (K + 1) + col) * XL)[s * 64 + lane] =
-                                make_double2(oc[col].re, oc[col].im);
-                    }
-                } else
-#pragma unroll
-                for (int col = 0; col <= K; col++) {
-                    const uint32_t soff = (uint32_t)(((size_t)j * NSEL * ggsw_len + (size_t)col * M + (size_t)s * 64) * 16);
-                    auto load_g = [&](int r, double2(&g)[NSEL]) {
-#pragma unroll
-                        for (int sel = 0; sel < NSEL; sel++)
-                            g[sel] = buffer_ld_d2(gres, loff, soff + (uint32_t)(((size_t)sel * ggsw_len + (size_t)r * (K + 1) * M) * 16));
-                    };
-                    cx oc[CPW];
-                    if constexpr (RSPLIT) {
-                        // one row's 2^g GGSW operands live at a time; the monomials are rebuilt per row
+                    for (int col = 0; col <= K; col++) {
+                        cx o;
 #pragma unroll
                         for (int r = 0; r <= K; r++) {
-                            __builtin_amdgcn_sched_barrier(0);
-                            double2 g[NSEL];
-                            load_g(r, g);
+                            // KB[r][col] at this frequency (keybundle, oracle mb_keybundle order)
+                            double2 kb = g[col][r][0];
 #pragma unroll
-                            for (int c = 0; c < CPW; c++) {
-                                if (c) __builtin_amdgcn_sched_barrier(0);
-                                cx mono[NSEL];
-                                monomials(c, mono);
-                                mac_row(c, r, g, mono, oc[c]);
+                            for (int sel = 1; sel < NSEL; sel++) {
+                                const double2 gg = g[col][r][sel];
+                                kb.x = fma(gg.x, mono[sel].re, fma(-gg.y, mono[sel].im, kb.x));
+                                kb.y = fma(gg.x, mono[sel].im, fma(gg.y, mono[sel].re, kb.y));
+                            }
+                            // MAC over rows (update_with_fmadd order)
+                            if (r == 0) {
+                                o.re = fma(kb.x, ff[r].x, -(kb.y * ff[r].y));
+                                o.im = fma(kb.x, ff[r].y, kb.y * ff[r].x);
+                            } else {
+                                o.re = fma(kb.x, ff[r].x, fma(-kb.y, ff[r].y, o.re));
+                                o.im = fma(kb.x, ff[r].y, fma(kb.y, ff[r].x, o.im));
                             }
                         }
-                    } else {
-                        __builtin_amdgcn_sched_barrier(0);  // one column's GGSW operands in flight at a time
-                        double2 g[K + 1][NSEL];
-#pragma unroll
-                        for (int r = 0; r <= K; r++) load_g(r, g[r]);
-#pragma unroll
-                        for (int c = 0; c < CPW; c++) {
-                            if (c) __builtin_amdgcn_sched_barrier(0);  // one ciphertext's monomials live at a time
-                            cx mono[NSEL];
-                            monomials(c, mono);
-#pragma unroll
-                            for (int r = 0; r <= K; r++) mac_row(c, r, g[r], mono, oc[c]);
-                        }
-                    }
-#pragma unroll
-                    for (int c = 0; c < CPW; c++) {
-                        const cx o = oc[c];
-                        O[c][col] = make_double2(o.re, o.im);
-                        if (col == K) {  // the last column has read F_c[.][s]: ciphertext c's slot s is free
-#pragma unroll
-                            for (int cc = 0; cc <= K; cc++)
-                                reinterpret_cast<double2 *>(xbuf + (size_t)(c * (K + 1) + cc) * XL)[s * 64 + lane] = O[c][cc];
-                        }
+                        // out_c[col][s] over F_c[col][s]: ciphertext c's F of slot s is in registers
+                        // and slot s is this wave's alone
+                        reinterpret_cast<double2 *>(xbuf + (size_t)(c * (K + 1) + col) * XL)[s * 64 + lane] =
+                            make_double2(o.re, o.im);
                     }
                 }
             }
