@@ -228,7 +228,8 @@ size_t large_chunk() {
 }
 
 size_t pbs_scratch_bytes(const TfheMi355Context *c, size_t count) {
-    if (!is_large(c) || count == 0) return 0;
+    if (count == 0 || c->p.grouping_factor) return 0;
+    if (!is_large(c)) return classic_pbs_ticket_bytes((int)c->N(), (int)c->k(), (int)c->p.pbs_level);
     const size_t per_ct = large_pbs_scratch_per_ct((int)c->N(), (int)c->k(), (int)c->p.pbs_level);
     return per_ct * std::min(count, large_chunk());
 }
@@ -327,6 +328,11 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
     a.base_log = (int)c->p.pbs_base_log;
     a.count = (int)count;
     a.glwe_out = glwe_out;
+    // persistent grid: a zeroed ticket word from the caller's scratch (none given: one pass)
+    if (classic_pbs_ticket_bytes((int)c->N(), (int)c->k(), (int)c->p.pbs_level) && scratch && scratch_bytes >= 4) {
+        a.ticket = reinterpret_cast<uint32_t *>(scratch);
+        check(hipMemsetAsync(a.ticket, 0, sizeof(uint32_t), s), "zero pbs ticket");
+    }
     check(launch_classic_pbs((int)c->N(), (int)c->k(), (int)c->p.pbs_level, a, s), "launch pbs");
 }
 

@@ -26,10 +26,13 @@ struct ClassicPbsLaunch {
     int base_log;
     int count;
     int glwe_out;                // 1: write the rotated accumulator [count][(k+1)N] (no sample extract)
+    uint32_t *ticket = nullptr;  // zeroed device word: dynamic ciphertext queue of the persistent grid (null: one pass)
 };
 
 // Returns false if (N, k, L) has no compiled specialisation.
 bool classic_pbs_supported(int N, int k, int L);
+// device scratch (zeroed by the caller before each launch) for the persistent grid's ticket
+size_t classic_pbs_ticket_bytes(int N, int k, int L);
 hipError_t launch_classic_pbs(int N, int k, int L, const ClassicPbsLaunch &a, hipStream_t s);
 
 struct MultiBitPbsLaunch {

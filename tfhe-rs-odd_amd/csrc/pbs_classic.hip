@@ -59,18 +59,27 @@ struct PbsConfig {
     static constexpr int CPW = PBS_CPW > 0 ? PBS_CPW : STAGE ? 2 : PACK4 ? 4 : 1;
     static constexpr bool GSYNC = PBS_GROUP_SYNC && !STAGE;  // the staged GGSW is shared by the workgroup
     static constexpr size_t flags_off() { return PbsLds<M>::bytes((K + 1) * CPW) + (STAGE ? GGSW_ELEMS * 16 : 0); }
-    static constexpr size_t lds_bytes() { return flags_off() + (GSYNC ? 4 * (K + 1) * CPW : 0); }
+    static constexpr size_t lds_bytes() { return flags_off() + (GSYNC ? 4 * (K + 1) * CPW + 4 * CPW : 0); }
     static_assert(lds_bytes() <= 160 * 1024, "LDS per workgroup exceeds a CU");
     // register budget per wave: 2 waves/SIMD for the packed 2_2 shape and N = 1024 (<= 256),
     // 3 at N = 512 (<= 168), 1 for the other N = 2048 shapes (~430 VGPR+AGPR at L = 2)
     static constexpr int WPE = PBS_WAVES_PER_EU > 0 ? PBS_WAVES_PER_EU
                                                     : (PACK4 ? 2 : N >= 2048 ? 1 : N == 1024 ? 2 : 3);
-    // persistent grid (needs GSYNC: slots never wait on each other), off by default.  Measured A/B
-    // (4096 PBS, static stride schedule): 2_2 116.8k -> 90.8k PBS/s, TFHE_LIB 110.1k -> 92.0k,
-    // SIMON_40 97.6k -> 93.4k, MANTICORE 99.7k -> 103.9k, ASCON_40 36.9k -> 40.6k, AES_40
-    // 52.7k -> 49.7k: a static schedule over "resident" workgroups loses whenever not every one of
-    // them is resident from the start (a late workgroup runs its whole share after the others)
-    static constexpr bool PERSIST = GSYNC && PBS_PERSIST > 0;
+    // Persistent grid with a dynamic ciphertext queue (needs GSYNC: slots never wait on each other).
+    // With one ciphertext per slot and launch, a workgroup holds its CU until its slowest slot is
+    // done; its ciphertexts drift apart (per-ciphertext sync), so on average only 1.6 of the 2
+    // waves per SIMD are resident (PMC).  Here a slot that finishes takes the next ciphertext from
+    // a global ticket (one atomic per ciphertext), and the grid is one resident wave of workgroups.
+    // Measured A/B (4096 PBS, `profiles/r02_ab_persistent_ticket.json`, PMC: 1.6 -> 1.88 resident
+    // waves/SIMD at 2_2): 2_2 115.0k -> 125.3k PBS/s, 2_2 KS+PBS 111.4k -> 121.2k, MANTICORE
+    // 98.0k -> 108.7k, SHA3_40 99.3k -> 114.8k, ASCON_40 37.3k -> 40.6k; slower for TFHE_LIB
+    // (1024, 2, 1) 108.9k -> 104.5k and SIMON_40 (512, 3, 2) 97.5k -> 91.9k, even for AES_40:
+    // on for the shapes where it measured faster (PBS_PERSIST = 0/1 forces it off/on).
+    static constexpr bool PERSIST_DEFAULT =
+        (N == 2048 && K == 1 && L == 1) || (N == 1024 && K == 1 && L == 2) || (N == 256 && K == 5 && L == 1) ||
+        (N == 1024 && K == 2 && L == 3);
+    static constexpr bool PERSIST = GSYNC && (PBS_PERSIST >= 0 ? (bool)PBS_PERSIST : PERSIST_DEFAULT);
+    static constexpr size_t ticket_off() { return flags_off() + (GSYNC ? 4 * (K + 1) * CPW : 0); }
 };
 
 template <int N, int K, int L>
@@ -94,9 +103,11 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
     // wave-uniform ids in SGPRs: per-ciphertext pointers and the mask element loads stay scalar
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane0 = threadIdx.x & 63;
-    int lane = lane0;
-    const int wave = wid % (K + 1);        // polynomial of the ciphertext this wave owns
-    const int slot = wid / (K + 1);        // ciphertext slot in the workgroup
+    // wave -> (ciphertext slot, polynomial).  PBS_SLOT_MAJOR: wave w = r CPW + slot, so with the
+    // workgroup's waves placed round-robin on the CU's 4 SIMDs each SIMD hosts the (k+1) waves of
+    // ONE ciphertext (CPW = 4, k = 1) instead of rows of two different ciphertexts
+    const int wave = PBS_SLOT_MAJOR ? wid / CPW : wid % (K + 1);  // polynomial of the ciphertext this wave owns
+    const int slot = PBS_SLOT_MAJOR ? wid % CPW : wid / (K + 1);  // ciphertext slot in the workgroup
     const int n = a.n;
     const int beta = a.base_log;
     const uint32_t dmask = (1u << beta) - 1;
@@ -122,7 +133,7 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
     // spectrum exchange among this ciphertext's waves
     std::conditional_t<Cfg::GSYNC, GroupSync<K + 1>, BlockSync> xsync;
     if constexpr (Cfg::GSYNC)
-        xsync = {lds_addr(gflags + slot * (K + 1)), lds_addr(gflags + wid)};
+        xsync = {lds_addr(gflags + slot * (K + 1)), lds_addr(gflags + slot * (K + 1) + wave)};
     cx *xb = xct + wave * XL;
     uint64_t *xb64 = reinterpret_cast<uint64_t *>(xb);
 
@@ -130,16 +141,25 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
     // other slots): the grid is at most one resident wave of workgroups (sized by the host) and
     // each slot walks the batch with stride gridDim.x * CPW.  Otherwise the grid covers the batch
     // (one trip); idle slots compute on a valid ciphertext and store nothing.
+    // The launch arguments are read inside the per-ciphertext routine through a kernarg-segment
+    // pointer laundered per call: in the persistent loop the compiler would otherwise keep every
+    // argument in SGPRs across the CMUX loop (SGPR spills into VGPR lanes, +24 VGPRs, 3 spilled).
+    using KArg = const __attribute__((address_space(4))) ClassicPbsLaunch;
     auto run_ct = [&](const int ct_raw) {
-    const bool active = ct_raw < a.count;  // idle slots compute on a valid ct, store nothing
-    const int ct = active ? ct_raw : a.count - 1;
-    const uint64_t *in = a.lwe_in + (size_t)ct * (n + 1);
+    KArg *ka = (KArg *)__builtin_amdgcn_kernarg_segment_ptr();
+    if constexpr (Cfg::PERSIST) asm volatile("" : "+s"(ka));
+    const ClassicPbsLaunch &A = *(const ClassicPbsLaunch *)ka;
+    int lane = lane0;  // per-ciphertext opaque copy: lane-derived addresses are not hoisted across ciphertexts
+    if constexpr (Cfg::PERSIST) asm volatile("" : "+v"(lane));
+    const bool active = ct_raw < A.count;  // idle slots compute on a valid ct, store nothing
+    const int ct = active ? ct_raw : A.count - 1;
+    const uint64_t *in = A.lwe_in + (size_t)ct * (n + 1);
     // the input row is read-only for the whole launch: constant address space -> s_load
     const __attribute__((address_space(4))) uint64_t *in_s = (const __attribute__((address_space(4))) uint64_t *)(
         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)in >> 32)) << 32) |
         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)in));
-    const uint32_t li = a.lut_indexes ? min(a.lut_indexes[ct], a.lut_count - 1u) : 0u;
-    const uint64_t *lut = a.luts + (size_t)li * (K + 1) * N + (size_t)wave * N;
+    const uint32_t li = A.lut_indexes ? min(A.lut_indexes[ct], A.lut_count - 1u) : 0u;
+    const uint64_t *lut = A.luts + (size_t)li * (K + 1) * N + (size_t)wave * N;
 
     // this wave's accumulator polynomial, in registers: c0[h] = position lane + 64 h
     // (h < V: j < M; h >= V: j = M + lane + 64 (h - V)).  ct0 = LUT / X^{b~}
@@ -158,7 +178,7 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
     }
 
     constexpr size_t ggsw_stride = (size_t)L * (K + 1) * (K + 1) * M;
-    const double2 *gcol = a.fbsk + (size_t)wave * M + lane;  // column c = wave, this lane
+    const double2 *gcol = A.fbsk + (size_t)wave * M + lane;  // column c = wave, this lane
     // staged GGSW: LDS image identical to the global one (lane-linear 1 KiB chunks)
     double2 *s_ggsw = lds + Lay::xbuf_off + (size_t)CPW * (K + 1) * XL;
     // The LDS-DMA is issued from inline asm: issued through the builtin, hipcc makes every later
@@ -167,7 +187,7 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
     // barrier that precedes its reader (stage_ggsw_wait); the loop issues no other vector loads.
     const uint32_t s_ggsw_addr = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char *)(s_ggsw));
     auto stage_ggsw = [&](int i) {
-        const double2 *src = a.fbsk + (size_t)i * ggsw_stride + lane0;
+        const double2 *src = A.fbsk + (size_t)i * ggsw_stride + lane0;
         for (int q = wid; q < (int)(ggsw_stride / 64); q += CPW * (K + 1)) {
             const uint32_t dst = __builtin_amdgcn_readfirstlane(s_ggsw_addr + (uint32_t)q * 1024u);
             uint32_t keep;
@@ -324,9 +344,9 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
         }
     }
 
-    if (a.glwe_out) {  // bootstrap_without_sample_extract (fork, bootstrap.rs:383-412)
+    if (A.glwe_out) {  // bootstrap_without_sample_extract (fork, bootstrap.rs:383-412)
         if (active) {
-            uint64_t *g = a.lwe_out + ((size_t)ct * (K + 1) + wave) * N;
+            uint64_t *g = A.lwe_out + ((size_t)ct * (K + 1) + wave) * N;
 #pragma unroll
             for (int h = 0; h < 2 * V; h++) g[lane0 + 64 * h] = c0[h];
         }
@@ -338,7 +358,7 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
     for (int h = 0; h < 2 * V; h++) xb64[lane0 + 64 * h] = c0[h];
     wsync();
     if (active) {
-        uint64_t *out = a.lwe_out + (size_t)ct * (K * N + 1);
+        uint64_t *out = A.lwe_out + (size_t)ct * (K * N + 1);
         if (wave < K) {
             for (int j = lane0; j < N; j += 64) out[wave * N + j] = j == 0 ? xb64[0] : 0 - xb64[N - j];
         } else if (lane0 == 0) {
@@ -348,7 +368,25 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
     wsync();  // the extract's reads of xb64 precede the next ciphertext's rotation writes
     };
     if constexpr (Cfg::PERSIST) {
-        for (int ct_raw = blockIdx.x * CPW + slot; ct_raw < a.count; ct_raw += gridDim.x * CPW) run_ct(ct_raw);
+        // first ciphertext: the slot's static index; then tickets (none without a ticket word: one
+        // pass).  Row 0 of the slot takes the ticket (one lane, a vector atomic) and hands it to
+        // its partner waves through LDS; the GroupSyncs that every wave of the slot executes once
+        // per ciphertext order the handover.
+        uint32_t *tslot = reinterpret_cast<uint32_t *>(smem + Cfg::ticket_off()) + slot;
+        int ct_raw = blockIdx.x * CPW + slot;
+        while (ct_raw < a.count) {
+            run_ct(ct_raw);
+            if (!a.ticket) break;
+            if (wave == 0) {
+                uint32_t t = 0;
+                if (lane0 == 0) t = atomicAdd(a.ticket, 1u);
+                t = __builtin_amdgcn_readfirstlane(t);
+                if (lane0 == 0) *tslot = t;
+            }
+            xsync();
+            ct_raw = (int)gridDim.x * CPW + (int)__builtin_amdgcn_readfirstlane(*(volatile uint32_t *)tslot);
+            xsync();  // every wave has read the ticket before row 0 may overwrite it
+        }
     } else {
         run_ct(blockIdx.x * CPW + slot);
     }
@@ -361,7 +399,8 @@ static hipError_t launch_pbs_t(const ClassicPbsLaunch &a, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
     const int threads = 64 * (K + 1) * CPW;
     int blocks = (a.count + CPW - 1) / CPW;
-    if (PbsConfig<N, K, L>::PERSIST) blocks = std::min(blocks, resident_blocks((const void *)pbs_classic_kernel<N, K, L>, threads, lds));
+    if (PbsConfig<N, K, L>::PERSIST && a.ticket)
+        blocks = std::min(blocks, resident_blocks((const void *)pbs_classic_kernel<N, K, L>, threads, lds));
     hipLaunchKernelGGL((pbs_classic_kernel<N, K, L>), dim3(blocks), dim3(threads), lds, s, a);
     return hipGetLastError();
 }
@@ -377,6 +416,14 @@ static hipError_t launch_pbs_t(const ClassicPbsLaunch &a, hipStream_t s) {
     X(512, 2, 1) X(512, 2, 2) X(512, 2, 3) X(512, 2, 4) \
     X(512, 3, 1) X(512, 3, 2) X(512, 3, 3) X(512, 3, 4) \
     X(256, 5, 1)
+
+// bytes of zeroed device scratch the launch wants for its ciphertext ticket (0: no persistent grid)
+size_t classic_pbs_ticket_bytes(int N, int k, int L) {
+#define PBS_TICKET(n_, k_, l_) if (N == n_ && k == k_ && L == l_) return PbsConfig<n_, k_, l_>::PERSIST ? 256 : 0;
+    PBS_CLASSIC_SHAPES(PBS_TICKET)
+#undef PBS_TICKET
+    return 0;
+}
 
 bool classic_pbs_supported(int N, int k, int L) {
 #define PBS_SUPPORTED(n_, k_, l_) if (N == n_ && k == k_ && L == l_) return true;

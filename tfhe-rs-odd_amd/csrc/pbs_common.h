@@ -31,8 +31,11 @@
 #define PBS_GROUP_SYNC 1  // CMUX-loop syncs between the (k+1) waves of ONE ciphertext (LDS flags), not s_barrier
 #endif
 
+#ifndef PBS_SLOT_MAJOR
+#define PBS_SLOT_MAJOR 0  // classic kernel: 1 = wave w serves (row w / CPW, ciphertext w % CPW) -- one ciphertext per SIMD
+#endif
 #ifndef PBS_PERSIST
-#define PBS_PERSIST 0  // 1: persistent classic-PBS grid, each ciphertext slot walks the batch (A/B option)
+#define PBS_PERSIST -1  // classic PBS persistent grid + ticket queue: -1 per-shape default (PbsConfig), 0/1 force
 #endif
 
 namespace tfhe_mi355 {
