@@ -56,10 +56,10 @@ PARAMS = {  # --params choice -> (parameter set name, workload text, kernel name
               "pbs_classic_kernel<2048,1,1> (+ ks_digits_kernel + ks_mfma_kernel)"),
     "mb3": ("PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS",
             "BASELINE config 5: batch of 4096 independent multi-bit (grouping 3) PBS per GPU, identity LUT",
-            "pbs_multibit_kernel<2048,1,1,3>"),
+            "pbs_multibit_shared_kernel<2048,1,1,3>"),
     "4_4": ("PARAM_MESSAGE_4_CARRY_4_KS_PBS",
             "BASELINE config 3: shortint apply_lookup_table (keyswitch -> PBS) at N=32768 per GPU batch",
-            "large_top_fwd_kernel<1,2> + large_sub_kernel<1,2> + large_top_inv_kernel<1> (+ ks_mfma_kernel)"),
+            "large_digits_kernel + large_group_cmux_kernel + large_top_inv_kernel<1> (+ ks_mfma_kernel)"),
     "mul32": ("PARAM_MESSAGE_2_CARRY_2_KS_PBS",
               "BASELINE config 4: FheUint32 multiply (16-block radix DAG, radix_parallel/mul.rs), "
               "K independent pairs per GPU, every DAG layer one batched KS+PBS launch, the whole DAG "
@@ -139,14 +139,15 @@ def pbs_flops(p) -> float:
 
 
 def large_model_bytes(p, chunk: int, with_ks: bool, units: int) -> float:
-    """Algorithmic bytes per PBS of the N = 32768 decomposition: per CMUX and
-    ciphertext the accumulator is read by large_top_fwd and read+written by large_top_inv
-    (3 (k+1) N 8 B), the top-stage spectra T (L (k+1) M 16 B) are written and read once, the
-    sub-block outputs U ((k+1) M 16 B) likewise; GGSW_i (L (k+1)^2 M 16 B) is read once per chunk.
-    Plus the LWE in/out and LUT, and with the keyswitch the KSK once per launch."""
+    """Algorithmic bytes per PBS of the N = 32768 grouped CMUX: per CMUX and
+    ciphertext the accumulator is read by large_digits and read+written by large_top_inv
+    (3 (k+1) N 8 B), the packed digits ((k+1) M 8 B) are written and read once, the sub-block
+    outputs U ((k+1) M 16 B) likewise (the 4 group workgroups of a ciphertext re-read its digits
+    from L2, not counted); GGSW_i (L (k+1)^2 M 16 B) is read once per chunk.  Plus the LWE in/out
+    and LUT, and with the keyswitch the KSK once per launch."""
     M = p.polynomial_size // 2
     k1 = p.glwe_dimension + 1
-    per_cmux = 3 * k1 * p.polynomial_size * 8 + 2 * p.pbs_level * k1 * M * 16 + 2 * k1 * M * 16
+    per_cmux = 3 * k1 * p.polynomial_size * 8 + 2 * k1 * M * 8 + 2 * k1 * M * 16
     per_cmux += p.pbs_level * k1 * k1 * M * 16 / chunk
     b = p.lwe_dimension * per_cmux + io_bytes(p, with_ks) + 8 * k1 * p.polynomial_size
     if with_ks:
@@ -197,8 +198,8 @@ def roofline(tag, p, units_per_launch: int, kernel_ms: float, kname: str, with_k
         achieved = model_b * units_per_launch / secs / 1e9
         r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-             "model": (f"N = 32768 decomposition bytes (DESIGN.md 5.3): {model_b:,.0f} B per PBS (accumulator, "
-                       f"top-stage spectra and sub-block outputs through HBM/MALL every CMUX, GGSW once per chunk "
+             "model": (f"N = 32768 grouped-CMUX bytes (DESIGN.md 5.3): {model_b:,.0f} B per PBS (accumulator, "
+                       f"packed digits and sub-block outputs through HBM/MALL every CMUX, GGSW once per chunk "
                        f"of {chunk}, KSK once per launch) x PBS per launch / kernel time; the PMC traffic "
                        "(L2<->fabric, Infinity-Cache hits included) is the measured counterpart"),
              "model_bytes_per_pbs": model_b,

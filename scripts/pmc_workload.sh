@@ -10,7 +10,7 @@ case $tag in
   2_2ks) K='pbs_classic_kernel|ks_digits|ks_mfma'; U='pbs_classic_kernel'; UPD=4096; M='pbs_classic_kernel'; ARGS="--params 2_2ks" ;;
   mb3)   K='pbs_multibit'; U='pbs_multibit'; UPD=4096; M='pbs_multibit'; ARGS="--params mb3" ;;
   mb2)   K='pbs_multibit'; U='pbs_multibit'; UPD=4096; M='pbs_multibit'; ARGS="--params mb2" ;;
-  4_4)   K='large_(init|top|sub|extract)|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=128; M='large_sub_kernel'; ARGS="--params 4_4 --batch 128" ;;
+  4_4)   K='large_(init|top|sub|extract|group|digits)|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=128; M='large_group_cmux_kernel'; ARGS="--params 4_4 --batch 128" ;;
   *) echo "unknown tag $tag"; exit 2 ;;
 esac
 B="$ARGS --steps 2 --warmup 1 --no-cpu-baseline --no-host-abi"
