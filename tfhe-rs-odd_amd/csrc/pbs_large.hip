@@ -417,6 +417,71 @@ __device__ __forceinline__ void group_compute(const GroupLd &d, uint32_t u, bool
     for (int l = 0; l < 2; l++) y[l][A] = tw16_fwd<A * G>(r4_out<G>(z[l][0], z[l][1], z[l][2], z[l][3]));
 }
 
+#ifndef LARGE_MAC_SPLIT
+#define LARGE_MAC_SPLIT 1  // 1: grouped-CMUX MAC split by slots (both levels per wave); 0: level chain
+#endif
+#ifndef LARGE_GRP_MAC_SB
+#define LARGE_GRP_MAC_SB 1  // slots per scheduling region of the split MAC (8 GGSW loads per slot; 2 spills)
+#endif
+// wave (LI, kk) of the slot-split MAC; on exit v = column 1 - LI of the sub-block, all 16 slots
+template <int LI>
+__device__ __forceinline__ void group_mac_split(cx (&f)[2][16], cx (&v)[16], double2 *lds, int lane, int kk,
+                                                const double2 *Gb) {
+    constexpr int K = 1, L = 2;
+    double2 *X = lds + lane;  // X[((kk * 2 + li) * 2 + r) * 512 + s' * 64]: the half the partner needs
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+#pragma unroll
+        for (int sp = 0; sp < 8; sp++) {
+            const cx t = f[r][8 * (1 - LI) + sp];
+            X[((kk * 2 + LI) * 2 + r) * 512 + sp * 64] = make_double2(t.re, t.im);
+        }
+    __syncthreads();
+    const double2 *Xp = lds + lane + (kk * 2 + (1 - LI)) * 2 * 512;  // partner's rows
+    cx o[2][8];
+#pragma unroll
+    for (int sp = 0; sp < 8; sp++) {
+        if (sp % LARGE_GRP_MAC_SB == 0) __builtin_amdgcn_sched_barrier(0);  // bound loads in flight
+        const int s = 8 * LI + sp;
+        cx fl[2], fm[2];  // level L / level L-1 spectra of rows 0, 1 at slot s
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            const cx own = f[r][8 * LI + sp];
+            const cx oth = gld(Xp + r * 512 + sp * 64);
+            fl[r] = LI ? oth : own;
+            fm[r] = LI ? own : oth;
+        }
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            const double2 g0 = Gb[(size_t)((L - 1) * (K + 1) * (K + 1) + c) * LM + s * 64];
+            const double2 g1 = Gb[(size_t)(((L - 1) * (K + 1) + 1) * (K + 1) + c) * LM + s * 64];
+            const double2 g2 = Gb[(size_t)c * LM + s * 64];
+            const double2 g3 = Gb[(size_t)((K + 1) + c) * LM + s * 64];
+            cx t;
+            t.re = fma(g0.x, fl[0].re, -(g0.y * fl[0].im));
+            t.im = fma(g0.x, fl[0].im, g0.y * fl[0].re);
+            t.re = fma(g1.x, fl[1].re, fma(-g1.y, fl[1].im, t.re));
+            t.im = fma(g1.x, fl[1].im, fma(g1.y, fl[1].re, t.im));
+            t.re = fma(g2.x, fm[0].re, fma(-g2.y, fm[0].im, t.re));
+            t.im = fma(g2.x, fm[0].im, fma(g2.y, fm[0].re, t.im));
+            t.re = fma(g3.x, fm[1].re, fma(-g3.y, fm[1].im, t.re));
+            t.im = fma(g3.x, fm[1].im, fma(g3.y, fm[1].re, t.im));
+            o[c][sp] = t;
+        }
+    }
+    __syncthreads();  // every X read done
+    // column 1 - LI is this wave's inverse; the partner gets column LI of this half
+    double2 *Y = lds + lane;
+#pragma unroll
+    for (int sp = 0; sp < 8; sp++) Y[(kk * 2 + LI) * 512 + sp * 64] = make_double2(o[LI][sp].re, o[LI][sp].im);
+    __syncthreads();
+    const double2 *Yp = lds + lane + (kk * 2 + (1 - LI)) * 512;
+#pragma unroll
+    for (int sp = 0; sp < 8; sp++) {
+        v[8 * LI + sp] = o[1 - LI][sp];
+        v[8 * (1 - LI) + sp] = gld(Yp + sp * 64);
+    }
+}
 #ifndef LARGE_GROUP_DIGITS
 #define LARGE_GROUP_DIGITS 1  // 1: rotation + decomposition once per ciphertext in large_digits_kernel
 #endif
@@ -572,10 +637,17 @@ __device__ __forceinline__ void group_cmux_body(const LargePbsLaunch &a, int ct0
     for (int r = 0; r < 2; r++) SubFft::forward(f[r], xb, tw, lane, wsync);
     __syncthreads();  // every wave's exchange buffer is free: the region carries the MAC chain
 
-    // MAC chain, oracle order (ggsw.rs:524-567): p = (lvl - 1)(k + 1) + r, lvl = L..1, r = 0..k
     const double2 *Gb = a.fbsk + (size_t)i * L * (K + 1) * (K + 1) * LM + 1024 * sblk + lane;
-    double2 *C = lds + lane;  // C[(kk * 2 + c) * 1024 + s * 64]
     cx v[16];
+#if LARGE_MAC_SPLIT
+    // MAC split by slots: wave (li, k) computes both columns for slots 8 li .. 8 li + 7, every row
+    // in oracle order (ggsw.rs:524-567: p = (lvl - 1)(k + 1) + r, lvl = L..1, r = 0..k); its own
+    // level's spectra are in registers, the partner's (1 - li, k) half comes through LDS.
+    if (li) group_mac_split<1>(f, v, lds, lane, kk, Gb);
+    else group_mac_split<0>(f, v, lds, lane, kk, Gb);
+#else
+    // MAC chain, oracle order (ggsw.rs:524-567): p = (lvl - 1)(k + 1) + r, lvl = L..1, r = 0..k
+    double2 *C = lds + lane;  // C[(kk * 2 + c) * 1024 + s * 64]
     if (li == 0) {
 #pragma unroll
         for (int s = 0; s < 16; s++) {
@@ -620,6 +692,7 @@ __device__ __forceinline__ void group_cmux_body(const LargePbsLaunch &a, int ct0
         for (int s = 0; s < 16; s++) v[s] = gld(C + (kk * 2 + 1) * 1024 + s * 64);
     }
     __syncthreads();  // chain read: the blocks are exchange buffers again
+#endif
     SubFft::inverse(v, xb, tw, lane, wsync);
     const int col = 1 - li;
     double2 *dst = a.spectra + ((size_t)cl * L * (K + 1) + col) * LM + 1024 * sblk + lane;
@@ -718,6 +791,7 @@ __global__ void __launch_bounds__(TOPT) large_top_inv_kernel(LargePbsLaunch a, i
 #ifndef LARGE_TD_UNROLL
 #define LARGE_TD_UNROLL 4  // digit positions per scheduling batch of the fused kernel
 #endif
+constexpr int TD_UNROLL = LARGE_TD_UNROLL;
 // top inverse stage of CMUX i and the digits of CMUX i+1 for one accumulator row (= inverse column
 // col): one 1024-thread workgroup per (ciphertext, row) owns all 1024 butterflies, so after the
 // workgroup barrier the rotated reads see the row it has just written (same CU: workgroup-scope
@@ -728,7 +802,7 @@ __global__ void __launch_bounds__(1024) large_top_inv_digits_kernel(LargePbsLaun
     if (cl >= a.chunk_count) return;  // whole workgroup
     top_inv_body<1>(a, cl, col, threadIdx.x);
     __syncthreads();  // the row's new values are visible to every wave of the workgroup
-#pragma unroll LARGE_TD_UNROLL
+#pragma unroll TD_UNROLL
     for (int b = 0; b < 16; b++) group_digits_body(a, ct0, i + 1, cl, col, (int)threadIdx.x + 1024 * b);
 }
 
