@@ -302,30 +302,35 @@ __global__ void __launch_bounds__((LargeSubCfg<K, L>::THREADS), 2) large_sub_ker
 }
 
 // ---------------------------------------------------------------------------------------
-// Grouped CMUX (LARGE_GROUP_SUB=1, k = 1, L = 2): the top DIF radix-16 is R4 over stride 4,
-// twiddles omega_16^{A c}, R4 (dft16_fwd), and its outputs c = G, G+4, G+8, G+12 come from ONE
-// second-layer R4 -- which needs only output G of each first-layer R4.  So one workgroup per
-// (ciphertext, group G) can build its four sub-blocks straight from the accumulator (rotation,
-// digits, twist, a quarter of the radix-16) with no f64 spectra written between launches: the
-// accumulator is read by the 4 workgroups of a ciphertext (same XCD, L2 hits after the first),
-// and what crosses the launch boundary is only the inverse sub-FFT output U (read by
-// large_top_inv).  Per ciphertext and CMUX that is 2.5 MiB through the Infinity Cache instead of
-// 4.5 MiB for top_fwd + sub + top_inv.  The operations are the oracle's, in its order, so the
-// outputs stay bit-exact.
-//   wave w = li * 4 + k (8 waves): level L - li, sub-block s = G + 4 k.
-//   1. per half h of the butterflies a (a = 512 h + tid): for both rows, rotate + decompose the
-//      32 positions a + 1024 b', twist, the group's quarter of the radix-16 for both levels, top
-//      twiddle W[a c] -> LDS [w][row][a - 512 h];  wave w picks up slots 8h..8h+7 of both rows.
-//   2. wave w: WaveFft<1024> forward of both rows (spectra stay in registers).
-//   3. MAC as a chain in the oracle's order (levels L..1, rows 0..k): waves li = 0 add the level-L
-//      terms for both columns and pass the partial sums through LDS; waves li = 1 add level L-1;
-//      column 0 stays with li = 1, column 1 goes back to li = 0.
-//   4. each wave: inverse sub-FFT of its column -> U[col][1024 s + position] (read by top_inv).
-// LDS: 8 x 16 KiB blocks (phase-1 staging, per-wave FFT exchange, MAC chain) + the sub-FFT
-// twiddle table = 143 KiB: one 512-thread workgroup per CU, 2 waves per SIMD.
+// Grouped CMUX (k = 1, L = 2).  The top DIF radix-16 is R4 over stride 4, twiddles
+// omega_16^{A c}, R4 (dft16_fwd): its outputs c = G, G+4, G+8, G+12 come from ONE second-layer
+// R4, which needs only output G of each first-layer R4.  So a workgroup per (ciphertext, group G,
+// part) builds KW of the group's sub-blocks straight from the CMUX's packed digits (twist + its
+// share of every radix-16 butterfly), and no f64 spectra cross a launch boundary.  Per CMUX:
+//   large_digits_kernel     rotation + both decomposition levels -> packed int16 digits
+//   large_group_cmux_kernel per (ct, G, part), 2 KW waves = level li x sub-block s = G + 4 k:
+//     1. per half h of the butterflies a: digits -> twist -> the group's radix-16 share for both
+//        rows and levels -> top twiddle W[a c] -> LDS [w][row][a - 512 h]; wave w picks up slots
+//        8h..8h+7 of both rows (WaveFft<1024> natural layout);
+//     2. wave w: forward sub-FFTs of both rows (spectra in registers);
+//     3. MAC split by slots: wave (li, k) computes both columns for slots 8 li .. 8 li + 7, rows and
+//        levels in the oracle's order, the partner level's spectra through LDS;
+//     4. wave (li, k): inverse sub-FFT of column 1 - li -> U[col][1024 s + position].
+//   large_top_inv_kernel    top DIT radix-16, backward conversion, accumulator update.
+// The operations are the oracle's, in its order, so the outputs stay bit-exact.  LDS: 2 KW blocks
+// of 16 KiB (phase-1 staging, per-wave FFT exchange, MAC exchange) + the sub-FFT twiddle table.
+// KW = 4: 512 threads, 143 KiB, one workgroup per CU; KW = 2: 256 threads, 79 KiB, two per CU
+// (the digits are read by twice as many workgroups, but one workgroup's memory phase overlaps
+// the other's FFTs).
 // ---------------------------------------------------------------------------------------
 #ifndef LARGE_GROUP_SUB
 #define LARGE_GROUP_SUB 1
+#endif
+#ifndef LARGE_GROUP_KW
+#define LARGE_GROUP_KW 4  // sub-blocks per level per group workgroup (4: all of group G; 2: half)
+#endif
+#ifndef LARGE_GRP_MAC_SB
+#define LARGE_GRP_MAC_SB 1  // slots per scheduling region of the split MAC (8 GGSW loads per slot; 2 spills)
 #endif
 
 // output G of r4_fwd(x0, x1, x2, x3), same expressions
@@ -340,104 +345,120 @@ __device__ __forceinline__ cx r4_out(cx x0, cx x1, cx x2, cx x3) {
     }
 }
 
+template <int KW>
 struct LargeGroupCfg {
-    static constexpr int THREADS = 512;
-    static constexpr int REGION = 8 * 1024;  // double2 entries: 8 blocks of 16 KiB
+    static_assert(KW == 2 || KW == 4, "2 or 4 sub-blocks per level per workgroup");
+    static constexpr int WAVES = 2 * KW;
+    static constexpr int THREADS = 64 * WAVES;
+    static constexpr int PARTS = 4 / KW;     // workgroups per (ciphertext, group)
+    static constexpr int REGION = WAVES * 1024;  // double2 entries: one 16 KiB block per wave
     static constexpr size_t LDS = sizeof(double2) * (REGION + SubFft::Lds::s1_len);
 };
 
-// Phase 1 streams the accumulator: a step is (row r, column A) of butterfly ap -- the inputs
-// b = A + 4m (m = 0..3) of the radix-16, own and rotated words at positions j and j + M.  All of a
-// step's loads are issued together and the next step's before this one's arithmetic, so 16-20
-// gathers per wave are in flight (one workgroup per CU: nothing else hides their latency).
-struct GroupLd {
-    uint64_t xo[4][2], xr[4][2];  // own / rotated source words [m][half]
-    cx tv[4];                     // twist at a + 1024 b
-};
-// per-thread constants of phase 1; loads go through buffer resources with the per-(b, half)
-// offset in an SGPR, so a step costs 1-2 VGPRs of addressing instead of one per load
-struct GroupAddr {
-    __amdgpu_buffer_rsrc_t acc[2];  // the ciphertext's two accumulator rows
-    __amdgpu_buffer_rsrc_t twist;
-    uint32_t own;    // 8 ap
-    uint32_t rot;    // u = ap - rem + N: source index u + c (c = 1024 b + M half) before the wrap
-    uint32_t tw;     // 16 ap
-};
 __device__ __forceinline__ uint64_t buffer_ld_u64(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     typedef unsigned v2u __attribute__((ext_vector_type(2)));
     const v2u t = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
     return ((uint64_t)t.y << 32) | t.x;
 }
-// the rotated source position of j = ap + c is jj = ap + c - rem = u + c - N: it wraps (jj >= 0,
-// source u + c - N, no sign flip) iff u + c >= N, else source u + c with the sign flip
-__device__ __forceinline__ bool rot_wraps(uint32_t u, int c) { return u + (uint32_t)c >= (uint32_t)LN; }
+
+// Packed digits of one position pair (j, j + M) of a row: int16 fields (level L at j, level L at
+// j + M, level L-1 at j, level L-1 at j + M); |digit| <= 2^(beta-1) = 2^14.  They live in the
+// chunk's spectra scratch behind U: [ct][poly 2..3 region] as [row][j] u64.
+__device__ __forceinline__ uint64_t *group_digits(const LargePbsLaunch &a, int cl) {
+    return reinterpret_cast<uint64_t *>(a.spectra + ((size_t)cl * 2 * 2 + 2) * LM);
+}
+
+// Phase 1 step = (row r, column A) of butterfly ap: the inputs b = A + 4m (m = 0..3).  All of a
+// step's loads are issued together and the next step's before this one's arithmetic (a
+// sched_barrier after each load group), so ~20 loads per wave are in flight.
+struct GroupDg {
+    uint64_t dg[4];
+    cx tv[4];  // twist at a + 1024 b
+};
 template <int A>
-__device__ __forceinline__ void group_load(GroupLd &d, const GroupAddr &g, int r) {
+__device__ __forceinline__ void group_load_dg(GroupDg &d, __amdgpu_buffer_rsrc_t dig, __amdgpu_buffer_rsrc_t twist,
+                                              int ap, int r) {
 #pragma unroll
     for (int m = 0; m < 4; m++) {
         const int b = A + 4 * m;
-        d.tv[m] = [&] {
-            const double2 t = buffer_ld_d2(g.twist, g.tw, 16u * 1024u * b);
-            return cx{t.x, t.y};
-        }();
-#pragma unroll
-        for (int half = 0; half < 2; half++) {
-            const int c = 1024 * b + half * LM;
-            // the whole offset in the VGPR: a raw buffer's range check sees the VGPR offset alone,
-            // so it must not go negative (u - N can)
-            const uint32_t src = g.rot + (uint32_t)c - (rot_wraps(g.rot, c) ? (uint32_t)LN : 0u);
-            d.xr[m][half] = buffer_ld_u64(g.acc[r], 8u * src, 0u);
-            d.xo[m][half] = buffer_ld_u64(g.acc[r], g.own, 8u * c);
-        }
+        d.dg[m] = buffer_ld_u64(dig, 8u * ap, 8u * (r * LM + 1024 * b));
+        const double2 t = buffer_ld_d2(twist, 16u * ap, 16u * 1024u * b);
+        d.tv[m] = cx{t.x, t.y};
     }
 }
-// digits, twist, first-layer R4 output G of column A and omega_16^{A G}, both levels
+// twist of both levels' digits, first-layer R4 output G of column A, omega_16^{A G}
 template <int A, int G>
-__device__ __forceinline__ void group_compute(const GroupLd &d, uint32_t u, bool full_odd, int beta, uint32_t dmask,
-                                              cx (&y)[2][4]) {
-    constexpr int L = 2;
+__device__ __forceinline__ void group_compute_dg(const GroupDg &d, cx (&y)[2][4]) {
     cx z[2][4];  // [li][m]
 #pragma unroll
     for (int m = 0; m < 4; m++) {
-        int32_t dg[2], dl[2];
-#pragma unroll
-        for (int half = 0; half < 2; half++) {
-            // ct1 = X^{a~} acc - acc  (polynomial_wrapping_monic_monomial_mul_and_subtract)
-            const bool neg = !rot_wraps(u, 1024 * (A + 4 * m) + half * LM) != full_odd;
-            const uint64_t x = d.xr[m][half];
-            const uint64_t dd = (neg ? 0 - x : x) - d.xo[m][half];
-            uint32_t st = decomp_state32_hi<L>((uint32_t)(dd >> 32), beta);
-            dg[half] = decomp_digit32(st, beta, dmask);  // level L
-            dl[half] = decomp_digit32(st, beta, dmask);  // level L-1
-        }
-        z[0][m] = cmulw(cx{(double)dg[0], (double)dg[1]}, d.tv[m].re, d.tv[m].im);
-        z[1][m] = cmulw(cx{(double)dl[0], (double)dl[1]}, d.tv[m].re, d.tv[m].im);
+        const uint64_t w = d.dg[m];
+        const double g0 = (double)(int16_t)(w & 0xffffu), g1 = (double)(int16_t)((w >> 16) & 0xffffu);
+        const double l0 = (double)(int16_t)((w >> 32) & 0xffffu), l1 = (double)(int16_t)(w >> 48);
+        z[0][m] = cmulw(cx{g0, g1}, d.tv[m].re, d.tv[m].im);
+        z[1][m] = cmulw(cx{l0, l1}, d.tv[m].re, d.tv[m].im);
     }
 #pragma unroll
     for (int l = 0; l < 2; l++) y[l][A] = tw16_fwd<A * G>(r4_out<G>(z[l][0], z[l][1], z[l][2], z[l][3]));
 }
 
-#ifndef LARGE_MAC_SPLIT
-#define LARGE_MAC_SPLIT 1  // 1: grouped-CMUX MAC split by slots (both levels per wave); 0: level chain
-#endif
-#ifndef LARGE_GRP_MAC_SB
-#define LARGE_GRP_MAC_SB 1  // slots per scheduling region of the split MAC (8 GGSW loads per slot; 2 spills)
-#endif
-// wave (LI, kk) of the slot-split MAC; on exit v = column 1 - LI of the sub-block, all 16 slots
-template <int LI>
-__device__ __forceinline__ void group_mac_split(cx (&f)[2][16], cx (&v)[16], double2 *lds, int lane, int kk,
+// phase 1 for butterfly ap of half h: both rows -> LDS staging [w][row][ap - 512 h]
+template <int KW, int G>
+__device__ __forceinline__ void group_phase1(const LargePbsLaunch &a, int cl, int part, int ap, int h, double2 *lds) {
+    const __amdgpu_buffer_rsrc_t rdig = make_rsrc(group_digits(a, cl)), rtw = make_rsrc(a.twist);
+    GroupDg e0, e1;
+    group_load_dg<0>(e0, rdig, rtw, ap, 0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        cx y[2][4];  // [li][A]: first-layer outputs, then X[G + 4k]
+        group_load_dg<1>(e1, rdig, rtw, ap, r);
+        __builtin_amdgcn_sched_barrier(0);  // issue the step's loads here, not at their uses
+        group_compute_dg<0, G>(e0, y);
+        group_load_dg<2>(e0, rdig, rtw, ap, r);
+        __builtin_amdgcn_sched_barrier(0);
+        group_compute_dg<1, G>(e1, y);
+        group_load_dg<3>(e1, rdig, rtw, ap, r);
+        __builtin_amdgcn_sched_barrier(0);
+        group_compute_dg<2, G>(e0, y);
+        if (r == 0) group_load_dg<0>(e0, rdig, rtw, ap, 1);  // next row's first step
+        __builtin_amdgcn_sched_barrier(0);
+        group_compute_dg<3, G>(e1, y);
+        cx wt[KW];
+#pragma unroll
+        for (int k = 0; k < KW; k++) {
+            const int c = G + 4 * (KW * part + k);
+            wt[k] = c ? gld(a.wtop + (c - 1) * 1024 + ap) : cx{1.0, 0.0};  // = W[a c]
+        }
+#pragma unroll
+        for (int l = 0; l < 2; l++) {
+            r4_fwd(y[l][0], y[l][1], y[l][2], y[l][3]);  // y[l][k] = X[G + 4k]
+#pragma unroll
+            for (int k = 0; k < KW; k++) {
+                const int kg = KW * part + k;  // uniform: part is per workgroup
+                const cx x = KW == 4 ? y[l][k] : (part ? y[l][2 + k] : y[l][k]);
+                const cx v = (G + 4 * kg) ? cmulw(x, wt[k].re, wt[k].im) : x;
+                lds[((l * KW + k) * 2 + r) * 512 + (ap - 512 * h)] = make_double2(v.re, v.im);
+            }
+        }
+    }
+}
+
+// wave (LI, k) of the slot-split MAC; on exit v = column 1 - LI of the sub-block, all 16 slots
+template <int KW, int LI>
+__device__ __forceinline__ void group_mac_split(cx (&f)[2][16], cx (&v)[16], double2 *lds, int lane, int k,
                                                 const double2 *Gb) {
     constexpr int K = 1, L = 2;
-    double2 *X = lds + lane;  // X[((kk * 2 + li) * 2 + r) * 512 + s' * 64]: the half the partner needs
+    double2 *X = lds + lane;  // X[((k * 2 + li) * 2 + r) * 512 + s' * 64]: the half the partner needs
 #pragma unroll
     for (int r = 0; r < 2; r++)
 #pragma unroll
         for (int sp = 0; sp < 8; sp++) {
             const cx t = f[r][8 * (1 - LI) + sp];
-            X[((kk * 2 + LI) * 2 + r) * 512 + sp * 64] = make_double2(t.re, t.im);
+            X[((k * 2 + LI) * 2 + r) * 512 + sp * 64] = make_double2(t.re, t.im);
         }
     __syncthreads();
-    const double2 *Xp = lds + lane + (kk * 2 + (1 - LI)) * 2 * 512;  // partner's rows
+    const double2 *Xp = lds + lane + (k * 2 + (1 - LI)) * 2 * 512;  // partner's rows
     cx o[2][8];
 #pragma unroll
     for (int sp = 0; sp < 8; sp++) {
@@ -453,6 +474,7 @@ __device__ __forceinline__ void group_mac_split(cx (&f)[2][16], cx (&v)[16], dou
         }
 #pragma unroll
         for (int c = 0; c < 2; c++) {
+            // ggsw.rs:524-567: p = (lvl - 1)(k + 1) + r, lvl = L..1, r = 0..k; GGSW poly p (k+1) + c
             const double2 g0 = Gb[(size_t)((L - 1) * (K + 1) * (K + 1) + c) * LM + s * 64];
             const double2 g1 = Gb[(size_t)(((L - 1) * (K + 1) + 1) * (K + 1) + c) * LM + s * 64];
             const double2 g2 = Gb[(size_t)c * LM + s * 64];
@@ -473,62 +495,24 @@ __device__ __forceinline__ void group_mac_split(cx (&f)[2][16], cx (&v)[16], dou
     // column 1 - LI is this wave's inverse; the partner gets column LI of this half
     double2 *Y = lds + lane;
 #pragma unroll
-    for (int sp = 0; sp < 8; sp++) Y[(kk * 2 + LI) * 512 + sp * 64] = make_double2(o[LI][sp].re, o[LI][sp].im);
+    for (int sp = 0; sp < 8; sp++) Y[(k * 2 + LI) * 512 + sp * 64] = make_double2(o[LI][sp].re, o[LI][sp].im);
     __syncthreads();
-    const double2 *Yp = lds + lane + (kk * 2 + (1 - LI)) * 512;
+    const double2 *Yp = lds + lane + (k * 2 + (1 - LI)) * 512;
 #pragma unroll
     for (int sp = 0; sp < 8; sp++) {
         v[8 * LI + sp] = o[1 - LI][sp];
         v[8 * (1 - LI) + sp] = gld(Yp + sp * 64);
     }
 }
-#ifndef LARGE_GROUP_DIGITS
-#define LARGE_GROUP_DIGITS 1  // 1: rotation + decomposition once per ciphertext in large_digits_kernel
-#endif
-// Packed digits of one position pair (j, j + M) of a row: int16 fields (level L at j, level L at
-// j + M, level L-1 at j, level L-1 at j + M); |digit| <= 2^(beta-1) = 2^14.  They live in the
-// chunk's spectra scratch behind U: [ct][poly 2..3 region] as [row][j] u64.
-__device__ __forceinline__ uint64_t *group_digits(const LargePbsLaunch &a, int cl) {
-    return reinterpret_cast<uint64_t *>(a.spectra + ((size_t)cl * 2 * 2 + 2) * LM);
-}
-struct GroupDg {
-    uint64_t dg[4];
-    cx tv[4];
-};
-template <int A>
-__device__ __forceinline__ void group_load_dg(GroupDg &d, __amdgpu_buffer_rsrc_t dig, __amdgpu_buffer_rsrc_t twist,
-                                              int ap, int r) {
-#pragma unroll
-    for (int m = 0; m < 4; m++) {
-        const int b = A + 4 * m;
-        d.dg[m] = buffer_ld_u64(dig, 8u * ap, 8u * (r * LM + 1024 * b));
-        const double2 t = buffer_ld_d2(twist, 16u * ap, 16u * 1024u * b);
-        d.tv[m] = cx{t.x, t.y};
-    }
-}
-template <int A, int G>
-__device__ __forceinline__ void group_compute_dg(const GroupDg &d, cx (&y)[2][4]) {
-    cx z[2][4];  // [li][m]
-#pragma unroll
-    for (int m = 0; m < 4; m++) {
-        const uint64_t w = d.dg[m];
-        const double g0 = (double)(int16_t)(w & 0xffffu), g1 = (double)(int16_t)((w >> 16) & 0xffffu);
-        const double l0 = (double)(int16_t)((w >> 32) & 0xffffu), l1 = (double)(int16_t)(w >> 48);
-        z[0][m] = cmulw(cx{g0, g1}, d.tv[m].re, d.tv[m].im);
-        z[1][m] = cmulw(cx{l0, l1}, d.tv[m].re, d.tv[m].im);
-    }
-#pragma unroll
-    for (int l = 0; l < 2; l++) y[l][A] = tw16_fwd<A * G>(r4_out<G>(z[l][0], z[l][1], z[l][2], z[l][3]));
-}
 
-template <int G>
-__device__ __forceinline__ void group_cmux_body(const LargePbsLaunch &a, int ct0, int i, int cl, double2 *lds) {
+template <int KW, int G>
+__device__ __forceinline__ void group_cmux_body(const LargePbsLaunch &a, int i, int cl, int part, double2 *lds) {
     constexpr int K = 1, L = 2;
-    using Cfg = LargeGroupCfg;
+    using Cfg = LargeGroupCfg<KW>;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int li = wave >> 2, kk = wave & 3;
-    const int sblk = G + 4 * kk;
+    const int li = wave / KW, k = wave % KW;
+    const int sblk = G + 4 * (KW * part + k);
     double2 *s1 = lds + Cfg::REGION;
     // sub-block stage twiddles W_1024[lane c] = W_M[16 lane c]  (oracle dif_rec tstride 16)
     for (int e = tid; e < SubFft::Lds::s1_len; e += Cfg::THREADS) s1[e] = a.W[16 * (e & 63) * ((e >> 6) + 1)];
@@ -536,163 +520,28 @@ __device__ __forceinline__ void group_cmux_body(const LargePbsLaunch &a, int ct0
     cx *xb = reinterpret_cast<cx *>(lds) + wave * 1024;
     WaveLocalSync wsync;
 
-    const uint64_t *in = a.lwe_in + (size_t)(ct0 + cl) * (a.n + 1);
-    const uint32_t at = pbs_modulus_switch<15>(in[i]);
-    const bool full_odd = (at / LN) & 1;
-    const int rem = at % LN;
-    const int beta = a.base_log;
-    const uint32_t dmask = (1u << beta) - 1;
-    const uint64_t *acc0 = a.acc + (size_t)cl * (K + 1) * LN;
-
     cx f[2][16];  // per row: this wave's sub-block input (natural layout), then its spectrum
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-        const int ap = 512 * h + tid;  // butterfly a
-        if (h) __syncthreads();        // every wave has picked up half 0
-#if defined(GRP_EXP) && GRP_EXP == 1
-        for (int w8 = 0; w8 < 16; w8++) lds[w8 * 512 + tid] = make_double2((double)ap, (double)w8);
-        if (0) {
-#endif
-#if LARGE_GROUP_DIGITS
-        const __amdgpu_buffer_rsrc_t rdig = make_rsrc(group_digits(a, cl)), rtw = make_rsrc(a.twist);
-        GroupDg e0, e1;
-        group_load_dg<0>(e0, rdig, rtw, ap, 0);
-        __builtin_amdgcn_sched_barrier(0);
+        if (h) __syncthreads();  // every wave has picked up half 0
 #pragma unroll
-        for (int r = 0; r < 2; r++) {
-            cx y[2][4];  // [li][A]: first-layer outputs, then X[G + 4k]
-            group_load_dg<1>(e1, rdig, rtw, ap, r);
-            __builtin_amdgcn_sched_barrier(0);  // issue the step's loads here, not at their uses
-            group_compute_dg<0, G>(e0, y);
-            group_load_dg<2>(e0, rdig, rtw, ap, r);
-            __builtin_amdgcn_sched_barrier(0);
-            group_compute_dg<1, G>(e1, y);
-            group_load_dg<3>(e1, rdig, rtw, ap, r);
-            __builtin_amdgcn_sched_barrier(0);
-            group_compute_dg<2, G>(e0, y);
-            if (r == 0) group_load_dg<0>(e0, rdig, rtw, ap, 1);  // next row's first step
-            __builtin_amdgcn_sched_barrier(0);
-            group_compute_dg<3, G>(e1, y);
-#else
-        GroupAddr ga;
-        ga.acc[0] = make_rsrc(acc0);
-        ga.acc[1] = make_rsrc(acc0 + LN);
-        ga.twist = make_rsrc(a.twist);
-        ga.own = 8u * ap;
-        ga.rot = (uint32_t)(ap - rem + LN);
-        ga.tw = 16u * ap;
-        GroupLd d0, d1;
-        group_load<0>(d0, ga, 0);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int r = 0; r < 2; r++) {
-            cx y[2][4];  // [li][A]: first-layer outputs, then X[G + 4k]
-            group_load<1>(d1, ga, r);
-            __builtin_amdgcn_sched_barrier(0);  // issue the step's loads here, not at their uses
-            group_compute<0, G>(d0, ga.rot, full_odd, beta, dmask, y);
-            group_load<2>(d0, ga, r);
-            __builtin_amdgcn_sched_barrier(0);  // issue the step's loads here, not at their uses
-            group_compute<1, G>(d1, ga.rot, full_odd, beta, dmask, y);
-            group_load<3>(d1, ga, r);
-            __builtin_amdgcn_sched_barrier(0);  // issue the step's loads here, not at their uses
-            group_compute<2, G>(d0, ga.rot, full_odd, beta, dmask, y);
-            if (r == 0) group_load<0>(d0, ga, 1);  // next row's first step
-            __builtin_amdgcn_sched_barrier(0);  // issue the step's loads here, not at their uses
-            group_compute<3, G>(d1, ga.rot, full_odd, beta, dmask, y);
-#endif
-            cx wt[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const int c = G + 4 * k;
-                wt[k] = c ? gld(a.wtop + (c - 1) * 1024 + ap) : cx{1.0, 0.0};  // = W[a c]
-            }
-#pragma unroll
-            for (int l = 0; l < 2; l++) {
-                r4_fwd(y[l][0], y[l][1], y[l][2], y[l][3]);  // y[l][k] = X[G + 4k]
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const cx v = (G + 4 * k) ? cmulw(y[l][k], wt[k].re, wt[k].im) : y[l][k];
-                    lds[((l * 4 + k) * 2 + r) * 512 + tid] = make_double2(v.re, v.im);
-                }
-            }
-        }
-#if defined(GRP_EXP) && GRP_EXP == 1
-        }
-#endif
+        for (int q = 0; q < 512 / Cfg::THREADS; q++) group_phase1<KW, G>(a, cl, part, 512 * h + Cfg::THREADS * q + tid, h, lds);
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < 2; r++)
 #pragma unroll
             for (int b = 0; b < 8; b++) f[r][8 * h + b] = gld(lds + (wave * 2 + r) * 512 + lane + 64 * b);
     }
-#if defined(GRP_EXP) && GRP_EXP == 2
-    {
-        double2 *dst = a.spectra + ((size_t)cl * L * (K + 1) + (1 - li)) * LM + 1024 * sblk + lane;
-        for (int b = 0; b < 16; b++) dst[64 * b] = make_double2(f[0][b].re + f[1][b].im, f[1][b].re);
-        return;
-    }
-#endif
     __syncthreads();  // the region now serves as the per-wave exchange buffers
 #pragma unroll
     for (int r = 0; r < 2; r++) SubFft::forward(f[r], xb, tw, lane, wsync);
-    __syncthreads();  // every wave's exchange buffer is free: the region carries the MAC chain
+    __syncthreads();  // every wave's exchange buffer is free: the region carries the MAC exchange
 
     const double2 *Gb = a.fbsk + (size_t)i * L * (K + 1) * (K + 1) * LM + 1024 * sblk + lane;
     cx v[16];
-#if LARGE_MAC_SPLIT
-    // MAC split by slots: wave (li, k) computes both columns for slots 8 li .. 8 li + 7, every row
-    // in oracle order (ggsw.rs:524-567: p = (lvl - 1)(k + 1) + r, lvl = L..1, r = 0..k); its own
-    // level's spectra are in registers, the partner's (1 - li, k) half comes through LDS.
-    if (li) group_mac_split<1>(f, v, lds, lane, kk, Gb);
-    else group_mac_split<0>(f, v, lds, lane, kk, Gb);
-#else
-    // MAC chain, oracle order (ggsw.rs:524-567): p = (lvl - 1)(k + 1) + r, lvl = L..1, r = 0..k
-    double2 *C = lds + lane;  // C[(kk * 2 + c) * 1024 + s * 64]
-    if (li == 0) {
-#pragma unroll
-        for (int s = 0; s < 16; s++) {
-            if (s % LARGE_MAC_SB == 0) __builtin_amdgcn_sched_barrier(0);  // bound loads in flight
-#pragma unroll
-            for (int c = 0; c < 2; c++) {
-                const double2 g0 = Gb[(size_t)((L - 1) * (K + 1) * (K + 1) + c) * LM + s * 64];
-                const double2 g1 = Gb[(size_t)(((L - 1) * (K + 1) + 1) * (K + 1) + c) * LM + s * 64];
-                const cx f0 = f[0][s], f1 = f[1][s];
-                cx o;
-                o.re = fma(g0.x, f0.re, -(g0.y * f0.im));
-                o.im = fma(g0.x, f0.im, g0.y * f0.re);
-                o.re = fma(g1.x, f1.re, fma(-g1.y, f1.im, o.re));
-                o.im = fma(g1.x, f1.im, fma(g1.y, f1.re, o.im));
-                C[(kk * 2 + c) * 1024 + s * 64] = make_double2(o.re, o.im);
-            }
-        }
-    }
-    __syncthreads();
-    if (li == 1) {
-#pragma unroll
-        for (int s = 0; s < 16; s++) {
-            if (s % LARGE_MAC_SB == 0) __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int c = 0; c < 2; c++) {
-                const double2 g0 = Gb[(size_t)c * LM + s * 64];
-                const double2 g1 = Gb[(size_t)((K + 1) + c) * LM + s * 64];
-                const cx f0 = f[0][s], f1 = f[1][s];
-                cx o = gld(C + (kk * 2 + c) * 1024 + s * 64);
-                o.re = fma(g0.x, f0.re, fma(-g0.y, f0.im, o.re));
-                o.im = fma(g0.x, f0.im, fma(g0.y, f0.re, o.im));
-                o.re = fma(g1.x, f1.re, fma(-g1.y, f1.im, o.re));
-                o.im = fma(g1.x, f1.im, fma(g1.y, f1.re, o.im));
-                if (c == 0) v[s] = o;
-                else C[(kk * 2 + 1) * 1024 + s * 64] = make_double2(o.re, o.im);
-            }
-        }
-    }
-    __syncthreads();
-    if (li == 0) {
-#pragma unroll
-        for (int s = 0; s < 16; s++) v[s] = gld(C + (kk * 2 + 1) * 1024 + s * 64);
-    }
-    __syncthreads();  // chain read: the blocks are exchange buffers again
-#endif
+    if (li) group_mac_split<KW, 1>(f, v, lds, lane, k, Gb);
+    else group_mac_split<KW, 0>(f, v, lds, lane, k, Gb);
+    __syncthreads();  // the blocks are exchange buffers again
     SubFft::inverse(v, xb, tw, lane, wsync);
     const int col = 1 - li;
     double2 *dst = a.spectra + ((size_t)cl * L * (K + 1) + col) * LM + 1024 * sblk + lane;
@@ -726,8 +575,7 @@ __device__ __forceinline__ void group_digits_body(const LargePbsLaunch &a, int c
     group_digits(a, cl)[(size_t)r * LM + j] = w;
 }
 
-// digits of CMUX i (the first CMUX, or every CMUX when LARGE_GROUP_FUSE_TD=0): one thread per
-// (ciphertext, row, j < M)
+// digits of CMUX i: one thread per (ciphertext, row, j < M)
 __global__ void __launch_bounds__(256) large_digits_kernel(LargePbsLaunch a, int ct0, int i) {
     constexpr int PER = 2 * (LM / 256);  // workgroups per ciphertext
     // XCD-aware: ciphertext cl on XCD group cl % 8, as its grouped-CMUX workgroups
@@ -737,19 +585,23 @@ __global__ void __launch_bounds__(256) large_digits_kernel(LargePbsLaunch a, int
     group_digits_body(a, ct0, i, cl, sub / (LM / 256), (sub % (LM / 256)) * 256 + threadIdx.x);
 }
 
-__global__ void __launch_bounds__(LargeGroupCfg::THREADS, 2) large_group_cmux_kernel(LargePbsLaunch a, int ct0, int i) {
+using GroupCfg = LargeGroupCfg<LARGE_GROUP_KW>;
+__global__ void __launch_bounds__(GroupCfg::THREADS, 2) large_group_cmux_kernel(LargePbsLaunch a, int ct0, int i) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double2 *lds = reinterpret_cast<double2 *>(smem);
-    // XCD-aware: the 4 group workgroups of a ciphertext are blocks 8 m + x, m = 4 q .. 4 q + 3
-    // (one XCD), so the accumulator they all read comes from the Infinity Cache once
+    constexpr int KW = LARGE_GROUP_KW, PARTS = GroupCfg::PARTS;
+    // XCD-aware: the 4 PARTS workgroups of a ciphertext are blocks 8 m + x with the same x (one
+    // XCD), so the digits they all read come from the Infinity Cache once
     const int x = blockIdx.x & 7, m = blockIdx.x >> 3;
-    const int cl = x + 8 * (m >> 2);
+    const int cl = x + 8 * (m / (4 * PARTS));
     if (cl >= a.chunk_count) return;  // whole workgroup
+    const int part = (m >> 2) % PARTS;
+    (void)ct0;
     switch (m & 3) {
-        case 0: group_cmux_body<0>(a, ct0, i, cl, lds); break;
-        case 1: group_cmux_body<1>(a, ct0, i, cl, lds); break;
-        case 2: group_cmux_body<2>(a, ct0, i, cl, lds); break;
-        default: group_cmux_body<3>(a, ct0, i, cl, lds); break;
+        case 0: group_cmux_body<KW, 0>(a, i, cl, part, lds); break;
+        case 1: group_cmux_body<KW, 1>(a, i, cl, part, lds); break;
+        case 2: group_cmux_body<KW, 2>(a, i, cl, part, lds); break;
+        default: group_cmux_body<KW, 3>(a, i, cl, part, lds); break;
     }
 }
 
@@ -783,27 +635,6 @@ __global__ void __launch_bounds__(TOPT) large_top_inv_kernel(LargePbsLaunch a, i
     constexpr int BPP = 1024 / TOPT;
     const int col = (blockIdx.x / BPP) % (K + 1);
     top_inv_body<K>(a, blockIdx.x / (BPP * (K + 1)), col, (blockIdx.x % BPP) * TOPT + threadIdx.x);
-}
-
-#ifndef LARGE_GROUP_FUSE_TD
-#define LARGE_GROUP_FUSE_TD 0  // 1: top_inv of CMUX i and the digits of CMUX i+1 in one launch (A/B: 1100 vs 1107 KS+PBS/s separate)
-#endif
-#ifndef LARGE_TD_UNROLL
-#define LARGE_TD_UNROLL 4  // digit positions per scheduling batch of the fused kernel
-#endif
-constexpr int TD_UNROLL = LARGE_TD_UNROLL;
-// top inverse stage of CMUX i and the digits of CMUX i+1 for one accumulator row (= inverse column
-// col): one 1024-thread workgroup per (ciphertext, row) owns all 1024 butterflies, so after the
-// workgroup barrier the rotated reads see the row it has just written (same CU: workgroup-scope
-// visibility), and the accumulator is not read again from the Infinity Cache by a separate launch.
-__global__ void __launch_bounds__(1024) large_top_inv_digits_kernel(LargePbsLaunch a, int ct0, int i) {
-    const int x = blockIdx.x & 7, m = blockIdx.x >> 3;
-    const int cl = x + 8 * (m >> 1), col = m & 1;
-    if (cl >= a.chunk_count) return;  // whole workgroup
-    top_inv_body<1>(a, cl, col, threadIdx.x);
-    __syncthreads();  // the row's new values are visible to every wave of the workgroup
-#pragma unroll TD_UNROLL
-    for (int b = 0; b < 16; b++) group_digits_body(a, ct0, i + 1, cl, col, (int)threadIdx.x + 1024 * b);
 }
 
 // CMUX i's top inverse stage fused with CMUX i+1's top forward stage (LARGE_FUSE_TOP=1): one
@@ -900,18 +731,13 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
         const unsigned fwd_blocks = (unsigned)((cnt + 7) / 8) * 8 * (K + 1) * (1024 / TOPT);
         if constexpr (K == 1 && L == 2) {
             if (LARGE_GROUP_SUB) {
-                const unsigned grp_blocks = (unsigned)((cnt + 7) / 8) * 8 * 4;
+                const unsigned grp_blocks = (unsigned)((cnt + 7) / 8) * 8 * 4 * GroupCfg::PARTS;
                 const unsigned dig_blocks = (unsigned)((cnt + 7) / 8) * 8 * 2 * (LM / 256);
-                const unsigned td_blocks = (unsigned)((cnt + 7) / 8) * 8 * 2;
                 for (int i = 0; i < a.n; i++) {
-                    if (LARGE_GROUP_DIGITS && (i == 0 || !LARGE_GROUP_FUSE_TD))
-                        hipLaunchKernelGGL(large_digits_kernel, dim3(dig_blocks), dim3(256), 0, s, a, ct0, i);
-                    hipLaunchKernelGGL(large_group_cmux_kernel, dim3(grp_blocks), dim3(LargeGroupCfg::THREADS),
-                                       LargeGroupCfg::LDS, s, a, ct0, i);
-                    if (LARGE_GROUP_DIGITS && LARGE_GROUP_FUSE_TD && i + 1 < a.n)
-                        hipLaunchKernelGGL(large_top_inv_digits_kernel, dim3(td_blocks), dim3(1024), 0, s, a, ct0, i);
-                    else
-                        hipLaunchKernelGGL((large_top_inv_kernel<K>), dim3(top_blocks), dim3(TOPT), 0, s, a, ct0, i);
+                    hipLaunchKernelGGL(large_digits_kernel, dim3(dig_blocks), dim3(256), 0, s, a, ct0, i);
+                    hipLaunchKernelGGL(large_group_cmux_kernel, dim3(grp_blocks), dim3(GroupCfg::THREADS), GroupCfg::LDS,
+                                       s, a, ct0, i);
+                    hipLaunchKernelGGL((large_top_inv_kernel<K>), dim3(top_blocks), dim3(TOPT), 0, s, a, ct0, i);
                 }
                 const size_t out_elems = (size_t)cnt * (K * LN + 1);
                 hipLaunchKernelGGL(large_extract_kernel<K>, dim3((unsigned)((out_elems + 255) / 256)), dim3(256), 0,
