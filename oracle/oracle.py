@@ -241,6 +241,38 @@ def fill_accumulator(N, k, msg_mod, carry_mod, f) -> np.ndarray:
 
 
 # ---- PBS / KS ----------------------------------------------------------------------------
+_simd = None
+
+
+def simd_variant() -> str:
+    """'v4' (AVX-512, 8 lanes) when the host has avx512f+avx512dq, else 'v3' (AVX2, 4 lanes)."""
+    flags = set()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("flags"):
+                flags = set(line.split(":", 1)[1].split())
+                break
+    except OSError:
+        pass
+    return "v4" if {"avx512f", "avx512dq"} <= flags else "v3"
+
+
+def simd_lib():
+    """libpbs_simd_<v>.so: the CPU baseline's SIMD-across-ciphertexts build of the oracle PBS."""
+    global _simd
+    if _simd is None:
+        path = os.path.join(_HERE, f"libpbs_simd_{simd_variant()}.so")
+        if not os.path.exists(path):
+            build(force=True)
+        L = ctypes.CDLL(path)
+        L.simd_width.restype = ctypes.c_int
+        L.simd_pbs_batch.restype = ctypes.c_int
+        L.simd_pbs_batch.argtypes = [f64p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     u64p, u64p, u64p, u32p, ctypes.c_size_t, ctypes.c_int]
+        _simd = L
+    return _simd
+
+
 class FourierBsk:
     """fbsk = Fourier BSK built with the oracle FFT (lwe_bootstrap_key_conversion.rs)."""
 
@@ -270,6 +302,24 @@ class FourierBsk:
             idx = np.ascontiguousarray(lut_idx, dtype=np.uint32)
         lib().orc_pbs_batch(self.h, _p(lwe_in), _p(out), _p(luts),
                             idx.ctypes.data_as(u32p) if idx is not None else None, cnt, threads)
+        return out
+
+    def pbs_simd(self, lwe_in, luts, lut_idx=None, threads=8) -> np.ndarray:
+        """Same PBS as `pbs` through pbs_simd.c (W ciphertexts per SIMD register, bit-identical):
+        the CPU baseline's throughput form."""
+        lwe_in = _u64(lwe_in).reshape(-1, self.n + 1)
+        luts = _u64(luts)
+        if getattr(self, "_fourier", None) is None:
+            self._fourier = self.fourier()
+        cnt = lwe_in.shape[0]
+        out = np.zeros((cnt, self.k * self.N + 1), dtype=np.uint64)
+        idx = None
+        if lut_idx is not None:
+            idx = np.ascontiguousarray(lut_idx, dtype=np.uint32)
+        rc = simd_lib().simd_pbs_batch(self._fourier.ctypes.data_as(f64p), self.n, self.k, self.N, self.base_log,
+                                       self.level, _p(lwe_in), _p(out), _p(luts),
+                                       idx.ctypes.data_as(u32p) if idx is not None else None, cnt, threads)
+        assert rc == 0, "pbs_simd: unsupported polynomial size"
         return out
 
     def blind_rotate(self, lwe_in, luts, lut_idx=None, threads=8) -> np.ndarray:
