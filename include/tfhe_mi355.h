@@ -70,6 +70,14 @@ const char *tfhe_mi355_last_error(void);
 /* Number of visible GPUs. */
 int tfhe_mi355_device_count(int *out_count);
 
+/* Page-locked (pinned) host memory for batch buffers.  The synchronous host-pointer entry points
+ * detect pinned input/output buffers and DMA them directly, chunk by chunk, overlapped with the
+ * kernels (no host staging copies); pageable buffers go through the engine's pinned staging.
+ * A Rust binding allocates its LWE batch Vecs here to get the device rate over PCIe.
+ * (No reference counterpart: the reference is CPU-only; the buffers replace Vec<u64> batches.) */
+int tfhe_mi355_host_alloc(size_t bytes, void **out_ptr);
+int tfhe_mi355_host_free(void *ptr);
+
 /* Create / destroy an engine context on `device`.
  * Replaces Fft::new + the shortint engine's thread-local buffers
  * (fft64/math/fft/mod.rs:146-193, shortint/engine/mod.rs:23-70,163-235). */

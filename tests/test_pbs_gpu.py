@@ -179,3 +179,33 @@ def test_shortint_api_end_to_end():
     triv = sk.create_trivial(2)
     sk.apply_lookup_table_assign(triv, acc)
     assert ck.decrypt(triv) == 0
+
+
+def test_pinned_host_buffers_direct_dma(orc, keys_2_2, engine_2_2):
+    """Page-locked caller buffers (tfhe_mi355_host_alloc) take the direct-DMA path of the
+    host-pointer entry points: same outputs as pageable buffers, over several pipeline chunks and
+    a ragged last chunk, for PBS and KS->PBS."""
+    from tfhe_mi355 import pinned_empty
+
+    p = keys_2_2.params
+    B = 2500  # > 2 chunks of 1024 with a ragged tail
+    msgs = np.random.default_rng(11).integers(0, 16, B)
+    cts = _small_cts(orc, keys_2_2, msgs, 11, p.delta)
+    acc = orc.fill_accumulator(2048, 1, 4, 4, lambda x: (x + 3) % 16)
+    exp = engine_2_2.programmable_bootstrap(cts, acc)
+    p_in = pinned_empty(cts.shape)
+    p_in[...] = cts
+    p_out = pinned_empty(exp.shape)
+    p_out[...] = 0
+    got = engine_2_2.programmable_bootstrap(p_in, acc, out=p_out)
+    assert got is p_out
+    assert np.array_equal(p_out, exp)
+    # pinned input, pageable output and the reverse
+    assert np.array_equal(engine_2_2.programmable_bootstrap(p_in, acc), exp)
+    assert np.array_equal(engine_2_2.programmable_bootstrap(cts, acc, out=pinned_empty(exp.shape)), exp)
+    big = orc.lwe_encrypt(12, keys_2_2.glwe_sk, msgs[:300].astype(np.uint64) * np.uint64(p.delta),
+                          p.glwe_modular_std_dev)
+    pb = pinned_empty(big.shape)
+    pb[...] = big
+    assert np.array_equal(engine_2_2.keyswitch_programmable_bootstrap(pb, acc, out=pinned_empty(big.shape)),
+                          engine_2_2.keyswitch_programmable_bootstrap(big, acc))

@@ -5,6 +5,6 @@ No CPU fallback: every compute call goes through the HIP engine.
 """
 from . import parameters
 from ._lib import EngineError, LIB_PATH, load
-from .engine import Engine, device_count, fill_accumulator
+from .engine import Engine, device_count, fill_accumulator, pinned_empty
 
 __all__ = ["parameters", "Engine", "EngineError", "LIB_PATH", "load", "device_count", "fill_accumulator"]

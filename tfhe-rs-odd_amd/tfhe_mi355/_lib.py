@@ -53,6 +53,8 @@ u8p = ctypes.POINTER(ctypes.c_uint8)
 SIGNATURES = [
     ("tfhe_mi355_last_error", ctypes.c_char_p, []),
     ("tfhe_mi355_device_count", ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    ("tfhe_mi355_host_alloc", ctypes.c_int, [sz, ctypes.POINTER(vp)]),
+    ("tfhe_mi355_host_free", ctypes.c_int, [vp]),
     ("tfhe_mi355_context_create", ctypes.c_int,
      [ctypes.POINTER(TfheMi355Parameters), ctypes.c_int, ctypes.POINTER(vp)]),
     ("tfhe_mi355_context_destroy", ctypes.c_int, [vp]),

@@ -48,6 +48,26 @@ def c_params(p: ClassicPBSParameters) -> TfheMi355Parameters:
                                p.carry_modulus, p.grouping_factor)
 
 
+def _free_host(ptr: int) -> None:
+    try:
+        _lib.load().tfhe_mi355_host_free(vp(ptr))
+    except Exception:  # interpreter shutdown
+        pass
+
+
+def pinned_empty(shape, dtype=np.uint64) -> np.ndarray:
+    """An uninitialised numpy array in page-locked host memory (tfhe_mi355_host_alloc), freed with
+    the array.  Batches passed to the host-pointer entry points in such arrays are DMA'd directly."""
+    import weakref
+
+    n = int(np.prod(shape)) * np.dtype(dtype).itemsize
+    p = vp()
+    _lib.call("tfhe_mi355_host_alloc", max(n, 1), ctypes.byref(p))
+    buf = (ctypes.c_uint8 * max(n, 1)).from_address(p.value)
+    weakref.finalize(buf, _free_host, p.value)
+    return np.frombuffer(buf, dtype=np.uint8, count=n).view(dtype).reshape(shape)
+
+
 def device_count() -> int:
     n = ctypes.c_int(0)
     _lib.call("tfhe_mi355_device_count", ctypes.byref(n))
@@ -141,11 +161,21 @@ class Engine:
             raise ValueError("lut_indexes must have one entry per ciphertext")
         return idx, idx.ctypes.data_as(u32p)
 
-    def programmable_bootstrap(self, lwe_in, luts, lut_indexes=None) -> np.ndarray:
+    @staticmethod
+    def _out(out, shape):
+        if out is None:
+            return np.empty(shape, dtype=np.uint64)
+        if out.dtype != np.uint64 or out.shape != shape or not out.flags.c_contiguous:
+            raise ValueError(f"out must be a C-contiguous uint64 array of shape {shape}")
+        return out
+
+    def programmable_bootstrap(self, lwe_in, luts, lut_indexes=None, out=None) -> np.ndarray:
+        """`out` (optional): the caller's output array; in and out arrays from `pinned_empty` are
+        DMA'd directly by the ABI (no staging copies)."""
         x = _u64(lwe_in).reshape(-1, self.n + 1)
         L = self._luts(luts)
         idx, idxp = self._idx(lut_indexes, x.shape[0], L.shape[0])
-        out = np.empty((x.shape[0], self.big_dim + 1), dtype=np.uint64)
+        out = self._out(out, (x.shape[0], self.big_dim + 1))
         _lib.call("tfhe_mi355_programmable_bootstrap", self._h, _ptr(x), _ptr(out), _ptr(L), L.shape[0],
                   idxp, x.shape[0])
         return out
@@ -166,11 +196,11 @@ class Engine:
         _lib.call("tfhe_mi355_keyswitch", self._h, _ptr(x), _ptr(out), x.shape[0])
         return out
 
-    def keyswitch_programmable_bootstrap(self, lwe_in, luts, lut_indexes=None) -> np.ndarray:
+    def keyswitch_programmable_bootstrap(self, lwe_in, luts, lut_indexes=None, out=None) -> np.ndarray:
         x = _u64(lwe_in).reshape(-1, self.big_dim + 1)
         L = self._luts(luts)
         idx, idxp = self._idx(lut_indexes, x.shape[0], L.shape[0])
-        out = np.empty((x.shape[0], self.big_dim + 1), dtype=np.uint64)
+        out = self._out(out, (x.shape[0], self.big_dim + 1))
         _lib.call("tfhe_mi355_keyswitch_programmable_bootstrap", self._h, _ptr(x), _ptr(out), _ptr(L),
                   L.shape[0], idxp, x.shape[0])
         return out
