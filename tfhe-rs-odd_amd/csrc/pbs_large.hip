@@ -403,9 +403,64 @@ __device__ __forceinline__ void group_compute_dg(const GroupDg &d, cx (&y)[2][4]
 }
 
 // phase 1 for butterfly ap of half h: both rows -> LDS staging [w][row][ap - 512 h]
+#ifndef LARGE_GRP_TW_SHARED
+#define LARGE_GRP_TW_SHARED 1  // 1: a phase-1 step is a column A for both rows (twist loaded once per a, not per row)
+#endif
+// both rows of column A: the twist is shared
+struct GroupDg2 {
+    uint64_t dg[2][4];
+    cx tv[4];
+};
+template <int A>
+__device__ __forceinline__ void group_load_dg2(GroupDg2 &d, __amdgpu_buffer_rsrc_t dig, __amdgpu_buffer_rsrc_t twist,
+                                               int ap) {
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        const int b = A + 4 * m;
+#pragma unroll
+        for (int r = 0; r < 2; r++) d.dg[r][m] = buffer_ld_u64(dig, 8u * ap, 8u * (r * LM + 1024 * b));
+        const double2 t = buffer_ld_d2(twist, 16u * ap, 16u * 1024u * b);
+        d.tv[m] = cx{t.x, t.y};
+    }
+}
+template <int A, int G>
+__device__ __forceinline__ void group_compute_dg2(const GroupDg2 &d, cx (&y)[2][2][4]) {
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        GroupDg e;
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            e.dg[m] = d.dg[r][m];
+            e.tv[m] = d.tv[m];
+        }
+        group_compute_dg<A, G>(e, y[r]);
+    }
+}
+
 template <int KW, int G>
 __device__ __forceinline__ void group_phase1(const LargePbsLaunch &a, int cl, int part, int ap, int h, double2 *lds) {
     const __amdgpu_buffer_rsrc_t rdig = make_rsrc(group_digits(a, cl)), rtw = make_rsrc(a.twist);
+#if LARGE_GRP_TW_SHARED
+    cx yy[2][2][4];  // [row][li][A]
+    {
+        GroupDg2 e0, e1;
+        group_load_dg2<0>(e0, rdig, rtw, ap);
+        __builtin_amdgcn_sched_barrier(0);
+        group_load_dg2<1>(e1, rdig, rtw, ap);
+        __builtin_amdgcn_sched_barrier(0);  // issue the step's loads here, not at their uses
+        group_compute_dg2<0, G>(e0, yy);
+        group_load_dg2<2>(e0, rdig, rtw, ap);
+        __builtin_amdgcn_sched_barrier(0);
+        group_compute_dg2<1, G>(e1, yy);
+        group_load_dg2<3>(e1, rdig, rtw, ap);
+        __builtin_amdgcn_sched_barrier(0);
+        group_compute_dg2<2, G>(e0, yy);
+        group_compute_dg2<3, G>(e1, yy);
+    }
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        cx (&y)[2][4] = yy[r];
+#else
     GroupDg e0, e1;
     group_load_dg<0>(e0, rdig, rtw, ap, 0);
     __builtin_amdgcn_sched_barrier(0);
@@ -424,6 +479,7 @@ __device__ __forceinline__ void group_phase1(const LargePbsLaunch &a, int cl, in
         if (r == 0) group_load_dg<0>(e0, rdig, rtw, ap, 1);  // next row's first step
         __builtin_amdgcn_sched_barrier(0);
         group_compute_dg<3, G>(e1, y);
+#endif
         cx wt[KW];
 #pragma unroll
         for (int k = 0; k < KW; k++) {
