@@ -157,3 +157,19 @@ def test_full_4_4_pbs_and_keyswitch(orc):
     assert np.array_equal(out[:2], keys.fbsk.pbs(small[:2], acc, threads=2))
     both = eng.keyswitch_programmable_bootstrap(big, acc)
     assert np.array_equal(both, out)
+
+
+def test_large_pbs_two_chunks_ragged(orc, small_n_4_4):
+    """200 ciphertexts: two passes of the chunked N = 32768 CMUX (128 + a ragged 72, not a multiple
+    of the 8-XCD block grouping); every output decrypts, a sample from each chunk is bit-exact."""
+    keys, eng = small_n_4_4
+    p = keys.params
+    N = p.polynomial_size
+    msgs = np.random.default_rng(21).integers(0, 256, 200)
+    cts = keys.encrypt(orc, msgs, 321)
+    acc = orc.fill_accumulator(N, 1, 16, 16, lambda x: (x * 5 + 1) % 256)
+    got = eng.programmable_bootstrap(cts, acc)
+    dec = decode(orc.lwe_decrypt(keys.glwe_sk, got), p.delta) % 256
+    assert np.array_equal(dec, (msgs * 5 + 1) % 256)
+    sample = np.array([0, 127, 128, 199])
+    assert np.array_equal(got[sample], keys.fbsk.pbs(cts[sample], acc, threads=4))
