@@ -352,7 +352,8 @@ struct LargeGroupCfg {
     static constexpr int THREADS = 64 * WAVES;
     static constexpr int PARTS = 4 / KW;     // workgroups per (ciphertext, group)
     static constexpr int REGION = WAVES * 1024;  // double2 entries: one 16 KiB block per wave
-    static constexpr size_t LDS = sizeof(double2) * (REGION + SubFft::Lds::s1_len);
+    static constexpr int FLAGS = REGION + SubFft::Lds::s1_len;  // double2 offset of the pair-sync flags
+    static constexpr size_t LDS = sizeof(double2) * FLAGS + 8 * KW;  // + one 8-byte flag pair per k
 };
 
 __device__ __forceinline__ uint64_t buffer_ld_u64(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
@@ -561,6 +562,72 @@ __device__ __forceinline__ void group_mac_split(cx (&f)[2][16], cx (&v)[16], dou
     }
 }
 
+#ifndef LARGE_GRP_PAIRSYNC
+#define LARGE_GRP_PAIRSYNC 1  // 1: the MAC exchange is ordered per wave pair (flags), not by workgroup barriers
+#endif
+// Slot-split MAC with the exchange in the pair's own two exchange blocks, ordered by the pair's
+// LDS flags (GroupSync<2>): wave (LI, k) writes the half of its spectra that the partner needs into
+// its own block, the pair syncs, each reads the other's block; then the same for the column
+// halves.  The four pairs of a workgroup drift independently (no workgroup barrier).
+template <int KW, int LI>
+__device__ __forceinline__ void group_mac_pair(cx (&f)[2][16], cx (&v)[16], double2 *lds, int lane, int k,
+                                               const double2 *Gb, GroupSync<2> &ps) {
+    constexpr int K = 1, L = 2;
+    double2 *own = lds + (LI * KW + k) * 1024 + lane;               // this wave's block
+    const double2 *oth = lds + ((1 - LI) * KW + k) * 1024 + lane;   // the partner's block
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+#pragma unroll
+        for (int sp = 0; sp < 8; sp++) {
+            const cx t = f[r][8 * (1 - LI) + sp];
+            own[r * 512 + sp * 64] = make_double2(t.re, t.im);
+        }
+    ps();  // both halves published
+    cx o[2][8];
+#pragma unroll
+    for (int sp = 0; sp < 8; sp++) {
+        __builtin_amdgcn_sched_barrier(0);  // bound loads in flight
+        const int s = 8 * LI + sp;
+        cx fl[2], fm[2];  // level L / level L-1 spectra of rows 0, 1 at slot s
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            const cx mine = f[r][8 * LI + sp];
+            const cx other = gld(oth + r * 512 + sp * 64);
+            fl[r] = LI ? other : mine;
+            fm[r] = LI ? mine : other;
+        }
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            // ggsw.rs:524-567: p = (lvl - 1)(k + 1) + r, lvl = L..1, r = 0..k; GGSW poly p (k+1) + c
+            const double2 g0 = Gb[(size_t)((L - 1) * (K + 1) * (K + 1) + c) * LM + s * 64];
+            const double2 g1 = Gb[(size_t)(((L - 1) * (K + 1) + 1) * (K + 1) + c) * LM + s * 64];
+            const double2 g2 = Gb[(size_t)c * LM + s * 64];
+            const double2 g3 = Gb[(size_t)((K + 1) + c) * LM + s * 64];
+            cx t;
+            t.re = fma(g0.x, fl[0].re, -(g0.y * fl[0].im));
+            t.im = fma(g0.x, fl[0].im, g0.y * fl[0].re);
+            t.re = fma(g1.x, fl[1].re, fma(-g1.y, fl[1].im, t.re));
+            t.im = fma(g1.x, fl[1].im, fma(g1.y, fl[1].re, t.im));
+            t.re = fma(g2.x, fm[0].re, fma(-g2.y, fm[0].im, t.re));
+            t.im = fma(g2.x, fm[0].im, fma(g2.y, fm[0].re, t.im));
+            t.re = fma(g3.x, fm[1].re, fma(-g3.y, fm[1].im, t.re));
+            t.im = fma(g3.x, fm[1].im, fma(g3.y, fm[1].re, t.im));
+            o[c][sp] = t;
+        }
+    }
+    ps();  // both have read the other's spectra: the blocks are free for the column halves
+    // column 1 - LI is this wave's inverse; the partner gets column LI of this half
+#pragma unroll
+    for (int sp = 0; sp < 8; sp++) own[sp * 64] = make_double2(o[LI][sp].re, o[LI][sp].im);
+    ps();
+#pragma unroll
+    for (int sp = 0; sp < 8; sp++) {
+        v[8 * LI + sp] = o[1 - LI][sp];
+        v[8 * (1 - LI) + sp] = gld(oth + sp * 64);
+    }
+    ps();  // the partner has read this block: it is this wave's FFT exchange buffer again
+}
+
 template <int KW, int G>
 __device__ __forceinline__ void group_cmux_body(const LargePbsLaunch &a, int i, int cl, int part, double2 *lds) {
     constexpr int K = 1, L = 2;
@@ -572,6 +639,7 @@ __device__ __forceinline__ void group_cmux_body(const LargePbsLaunch &a, int i, 
     double2 *s1 = lds + Cfg::REGION;
     // sub-block stage twiddles W_1024[lane c] = W_M[16 lane c]  (oracle dif_rec tstride 16)
     for (int e = tid; e < SubFft::Lds::s1_len; e += Cfg::THREADS) s1[e] = a.W[16 * (e & 63) * ((e >> 6) + 1)];
+    if (tid < 2 * KW) reinterpret_cast<uint32_t *>(lds + Cfg::FLAGS)[tid] = 0;  // pair-sync flags
     const SubFft::Lds tw{s1, s1};
     cx *xb = reinterpret_cast<cx *>(lds) + wave * 1024;
     WaveLocalSync wsync;
@@ -591,13 +659,20 @@ __device__ __forceinline__ void group_cmux_body(const LargePbsLaunch &a, int i, 
     __syncthreads();  // the region now serves as the per-wave exchange buffers
 #pragma unroll
     for (int r = 0; r < 2; r++) SubFft::forward(f[r], xb, tw, lane, wsync);
-    __syncthreads();  // every wave's exchange buffer is free: the region carries the MAC exchange
 
     const double2 *Gb = a.fbsk + (size_t)i * L * (K + 1) * (K + 1) * LM + 1024 * sblk + lane;
     cx v[16];
+#if LARGE_GRP_PAIRSYNC
+    GroupSync<2> ps;
+    ps.mine = lds_addr(lds + Cfg::FLAGS) + 8u * k + 4u * li;
+    if (li) group_mac_pair<KW, 1>(f, v, lds, lane, k, Gb, ps);
+    else group_mac_pair<KW, 0>(f, v, lds, lane, k, Gb, ps);
+#else
+    __syncthreads();  // every wave's exchange buffer is free: the region carries the MAC exchange
     if (li) group_mac_split<KW, 1>(f, v, lds, lane, k, Gb);
     else group_mac_split<KW, 0>(f, v, lds, lane, k, Gb);
     __syncthreads();  // the blocks are exchange buffers again
+#endif
     SubFft::inverse(v, xb, tw, lane, wsync);
     const int col = 1 - li;
     double2 *dst = a.spectra + ((size_t)cl * L * (K + 1) + col) * LM + 1024 * sblk + lane;
