@@ -314,23 +314,20 @@ __global__ void __launch_bounds__((LargeSubCfg<K, L>::THREADS), 2) large_sub_ker
 //        8h..8h+7 of both rows (WaveFft<1024> natural layout);
 //     2. wave w: forward sub-FFTs of both rows (spectra in registers);
 //     3. MAC split by slots: wave (li, k) computes both columns for slots 8 li .. 8 li + 7, rows and
-//        levels in the oracle's order, the partner level's spectra through LDS;
+//        levels in the oracle's order; the partner level's spectra and the column halves go
+//        through the pair's own exchange blocks, ordered by pair flags (no workgroup barrier);
 //     4. wave (li, k): inverse sub-FFT of column 1 - li -> U[col][1024 s + position].
 //   large_top_inv_kernel    top DIT radix-16, backward conversion, accumulator update.
 // The operations are the oracle's, in its order, so the outputs stay bit-exact.  LDS: 2 KW blocks
 // of 16 KiB (phase-1 staging, per-wave FFT exchange, MAC exchange) + the sub-FFT twiddle table.
 // KW = 4: 512 threads, 143 KiB, one workgroup per CU; KW = 2: 256 threads, 79 KiB, two per CU
-// (the digits are read by twice as many workgroups, but one workgroup's memory phase overlaps
-// the other's FFTs).
+// (the digits are read by twice as many workgroups; measured slower: 1016 vs 1116 KS+PBS/s).
 // ---------------------------------------------------------------------------------------
 #ifndef LARGE_GROUP_SUB
 #define LARGE_GROUP_SUB 1
 #endif
 #ifndef LARGE_GROUP_KW
 #define LARGE_GROUP_KW 4  // sub-blocks per level per group workgroup (4: all of group G; 2: half)
-#endif
-#ifndef LARGE_GRP_MAC_SB
-#define LARGE_GRP_MAC_SB 1  // slots per scheduling region of the split MAC (8 GGSW loads per slot; 2 spills)
 #endif
 
 // output G of r4_fwd(x0, x1, x2, x3), same expressions
@@ -501,70 +498,6 @@ __device__ __forceinline__ void group_phase1(const LargePbsLaunch &a, int cl, in
     }
 }
 
-// wave (LI, k) of the slot-split MAC; on exit v = column 1 - LI of the sub-block, all 16 slots
-template <int KW, int LI>
-__device__ __forceinline__ void group_mac_split(cx (&f)[2][16], cx (&v)[16], double2 *lds, int lane, int k,
-                                                const double2 *Gb) {
-    constexpr int K = 1, L = 2;
-    double2 *X = lds + lane;  // X[((k * 2 + li) * 2 + r) * 512 + s' * 64]: the half the partner needs
-#pragma unroll
-    for (int r = 0; r < 2; r++)
-#pragma unroll
-        for (int sp = 0; sp < 8; sp++) {
-            const cx t = f[r][8 * (1 - LI) + sp];
-            X[((k * 2 + LI) * 2 + r) * 512 + sp * 64] = make_double2(t.re, t.im);
-        }
-    __syncthreads();
-    const double2 *Xp = lds + lane + (k * 2 + (1 - LI)) * 2 * 512;  // partner's rows
-    cx o[2][8];
-#pragma unroll
-    for (int sp = 0; sp < 8; sp++) {
-        if (sp % LARGE_GRP_MAC_SB == 0) __builtin_amdgcn_sched_barrier(0);  // bound loads in flight
-        const int s = 8 * LI + sp;
-        cx fl[2], fm[2];  // level L / level L-1 spectra of rows 0, 1 at slot s
-#pragma unroll
-        for (int r = 0; r < 2; r++) {
-            const cx own = f[r][8 * LI + sp];
-            const cx oth = gld(Xp + r * 512 + sp * 64);
-            fl[r] = LI ? oth : own;
-            fm[r] = LI ? own : oth;
-        }
-#pragma unroll
-        for (int c = 0; c < 2; c++) {
-            // ggsw.rs:524-567: p = (lvl - 1)(k + 1) + r, lvl = L..1, r = 0..k; GGSW poly p (k+1) + c
-            const double2 g0 = Gb[(size_t)((L - 1) * (K + 1) * (K + 1) + c) * LM + s * 64];
-            const double2 g1 = Gb[(size_t)(((L - 1) * (K + 1) + 1) * (K + 1) + c) * LM + s * 64];
-            const double2 g2 = Gb[(size_t)c * LM + s * 64];
-            const double2 g3 = Gb[(size_t)((K + 1) + c) * LM + s * 64];
-            cx t;
-            t.re = fma(g0.x, fl[0].re, -(g0.y * fl[0].im));
-            t.im = fma(g0.x, fl[0].im, g0.y * fl[0].re);
-            t.re = fma(g1.x, fl[1].re, fma(-g1.y, fl[1].im, t.re));
-            t.im = fma(g1.x, fl[1].im, fma(g1.y, fl[1].re, t.im));
-            t.re = fma(g2.x, fm[0].re, fma(-g2.y, fm[0].im, t.re));
-            t.im = fma(g2.x, fm[0].im, fma(g2.y, fm[0].re, t.im));
-            t.re = fma(g3.x, fm[1].re, fma(-g3.y, fm[1].im, t.re));
-            t.im = fma(g3.x, fm[1].im, fma(g3.y, fm[1].re, t.im));
-            o[c][sp] = t;
-        }
-    }
-    __syncthreads();  // every X read done
-    // column 1 - LI is this wave's inverse; the partner gets column LI of this half
-    double2 *Y = lds + lane;
-#pragma unroll
-    for (int sp = 0; sp < 8; sp++) Y[(k * 2 + LI) * 512 + sp * 64] = make_double2(o[LI][sp].re, o[LI][sp].im);
-    __syncthreads();
-    const double2 *Yp = lds + lane + (k * 2 + (1 - LI)) * 512;
-#pragma unroll
-    for (int sp = 0; sp < 8; sp++) {
-        v[8 * LI + sp] = o[1 - LI][sp];
-        v[8 * (1 - LI) + sp] = gld(Yp + sp * 64);
-    }
-}
-
-#ifndef LARGE_GRP_PAIRSYNC
-#define LARGE_GRP_PAIRSYNC 1  // 1: the MAC exchange is ordered per wave pair (flags), not by workgroup barriers
-#endif
 // Slot-split MAC with the exchange in the pair's own two exchange blocks, ordered by the pair's
 // LDS flags (GroupSync<2>): wave (LI, k) writes the half of its spectra that the partner needs into
 // its own block, the pair syncs, each reads the other's block; then the same for the column
@@ -662,17 +595,12 @@ __device__ __forceinline__ void group_cmux_body(const LargePbsLaunch &a, int i, 
 
     const double2 *Gb = a.fbsk + (size_t)i * L * (K + 1) * (K + 1) * LM + 1024 * sblk + lane;
     cx v[16];
-#if LARGE_GRP_PAIRSYNC
+    // pair flags instead of workgroup barriers (A/B with two barriers around a region-wide
+    // exchange: 64.4 -> 61.4 us per chunk)
     GroupSync<2> ps;
     ps.mine = lds_addr(lds + Cfg::FLAGS) + 8u * k + 4u * li;
     if (li) group_mac_pair<KW, 1>(f, v, lds, lane, k, Gb, ps);
     else group_mac_pair<KW, 0>(f, v, lds, lane, k, Gb, ps);
-#else
-    __syncthreads();  // every wave's exchange buffer is free: the region carries the MAC exchange
-    if (li) group_mac_split<KW, 1>(f, v, lds, lane, k, Gb);
-    else group_mac_split<KW, 0>(f, v, lds, lane, k, Gb);
-    __syncthreads();  // the blocks are exchange buffers again
-#endif
     SubFft::inverse(v, xb, tw, lane, wsync);
     const int col = 1 - li;
     double2 *dst = a.spectra + ((size_t)cl * L * (K + 1) + col) * LM + 1024 * sblk + lane;
