@@ -97,6 +97,9 @@ def lib():
         L.orc_exact_pbs_batch.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, u64p, u64p, u64p, u32p, ctypes.c_size_t, ctypes.c_int,
                                           ctypes.c_int]
+        L.orc_exact_mb_pbs_batch.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_int, u64p, u64p, u64p, u32p, ctypes.c_size_t,
+                                             ctypes.c_int, ctypes.c_int]
         if hasattr(L, "orc_mb_pbs_batch"):
             L.orc_mb_fbsk_create.restype = ctypes.c_void_p
             L.orc_mb_fbsk_create.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -190,6 +193,23 @@ def exact_pbs(bsk, n, k, N, base_log, level, cts, luts, lut_idx=None, threads=8,
         idx = np.ascontiguousarray(lut_idx, dtype=np.uint32)
     lib().orc_exact_pbs_batch(_p(bsk), n, k, N, base_log, level, _p(x), _p(out), _p(L),
                               _p(idx, u32p) if idx is not None else None, x.shape[0], threads, int(glwe_out))
+    return out
+
+
+def exact_mb_pbs(bsk, n, k, N, base_log, level, g, cts, luts, lut_idx=None, threads=8, glwe_out=False) -> np.ndarray:
+    """FFT-free multi-bit PBS: exact standard-domain keybundles and exact external products
+    (pbs_oracle.c 'exact multi-bit PBS'), deterministic group order."""
+    bsk = _u64(bsk)
+    x = _u64(cts).reshape(-1, n + 1)
+    L = _u64(luts)
+    if L.ndim == 1:
+        L = L.reshape(1, -1)
+    out = np.zeros((x.shape[0], (k + 1) * N if glwe_out else k * N + 1), dtype=np.uint64)
+    idx = None
+    if lut_idx is not None:
+        idx = np.ascontiguousarray(lut_idx, dtype=np.uint32)
+    lib().orc_exact_mb_pbs_batch(_p(bsk), n, k, N, base_log, level, g, _p(x), _p(out), _p(L),
+                                 _p(idx, u32p) if idx is not None else None, x.shape[0], threads, int(glwe_out))
     return out
 
 

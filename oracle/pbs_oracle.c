@@ -1417,3 +1417,111 @@ void orc_exact_pbs_batch(const uint64_t *bsk, int n, int k, int N, int base_log,
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
     pthread_mutex_destroy(&J.mu);
 }
+
+/* ---- exact multi-bit PBS ---------------------------------------------------------------- */
+/* out = X^d p  (d in [0, 2N]; negacyclic: a full N flips the sign) */
+static void monomial_mul(uint64_t *out, const uint64_t *p, int N, uint64_t d) {
+    uint64_t full = d / N, rem = d % N;
+    for (int j = 0; j < N; j++) {
+        uint64_t v = (uint64_t)j >= rem ? p[j - rem] : 0 - p[j - rem + N];
+        out[j] = (full & 1) ? 0 - v : v;
+    }
+}
+
+/* FFT-free counterpart of mb_pbs_one (lwe_multi_bit_programmable_bootstrapping.rs:548-828,
+ * 18-84): per group j in order, the keybundle KB = GGSW_{j,0} + sum_sel X^{deg_sel} GGSW_{j,sel}
+ * exactly in the standard domain (a monomial product is a signed rotation; the sum is ring
+ * arithmetic, so its order is immaterial), then acc <- ExtProd(KB, acc) exactly into a zeroed
+ * GLWE.  Standard multi-bit BSK [n/g][2^g][L][k+1][k+1][N]. */
+static void exact_mb_pbs_one(const exact_bsk *b, int g, const uint64_t *lwe_in, uint64_t *lwe_out, const uint64_t *lut,
+                             uint64_t *acc, uint64_t *tmp, uint64_t *kb, uint64_t *rot, exact_scratch *s, int glwe_out) {
+    int n = b->n, k = b->k, N = b->N;
+    int log2N = 0;
+    while ((1 << log2N) < N) log2N++;
+    const size_t npoly = (size_t)b->level * (k + 1) * (k + 1);
+    const size_t ggsw_len = npoly * N;
+    const size_t gl = (size_t)(k + 1) * N;
+    uint64_t bt = orc_pbs_modulus_switch(lwe_in[n], log2N);
+    for (int p = 0; p <= k; p++) monomial_div(acc + (size_t)p * N, lut + (size_t)p * N, N, bt);
+    for (int j = 0; j < n / g; j++) {
+        const uint64_t *grp = b->bsk + (size_t)j * ((size_t)1 << g) * ggsw_len;
+        memcpy(kb, grp, sizeof(uint64_t) * ggsw_len);
+        for (int sel = 1; sel < (1 << g); sel++) {
+            uint64_t deg = 0;
+            for (int i = 0; i < g; i++)
+                if ((sel >> (g - 1 - i)) & 1) deg += lwe_in[(size_t)j * g + i];
+            const uint64_t d = orc_pbs_modulus_switch(deg, log2N);
+            const uint64_t *G = grp + (size_t)sel * ggsw_len;
+            for (size_t q = 0; q < npoly; q++) {
+                monomial_mul(rot, G + q * N, N, d);
+                for (int t = 0; t < N; t++) kb[q * N + t] += rot[t];
+            }
+        }
+        memset(tmp, 0, sizeof(uint64_t) * gl);
+        exact_external_product_add(b, kb, tmp, acc, s);
+        memcpy(acc, tmp, sizeof(uint64_t) * gl);
+    }
+    if (glwe_out)
+        memcpy(lwe_out, acc, sizeof(uint64_t) * gl);
+    else
+        sample_extract0(acc, lwe_out, k, N);
+}
+
+typedef struct {
+    const exact_bsk *b;
+    int g;
+    const uint64_t *in, *luts;
+    const uint32_t *lut_idx;
+    uint64_t *out;
+    size_t count, next;
+    pthread_mutex_t mu;
+    int glwe_out;
+} exact_mb_job;
+
+static void *exact_mb_worker(void *arg) {
+    exact_mb_job *J = arg;
+    const exact_bsk *b = J->b;
+    int k = b->k, N = b->N;
+    size_t gl = (size_t)(k + 1) * N;
+    exact_scratch s;
+    s.ct1 = NULL;
+    s.state = malloc(sizeof(uint64_t) * gl);
+    s.digits = malloc(sizeof(uint64_t) * N);
+    s.t = malloc(sizeof(uint64_t) * 10 * (size_t)N);
+    uint64_t *acc = malloc(sizeof(uint64_t) * gl), *tmp = malloc(sizeof(uint64_t) * gl);
+    uint64_t *kb = malloc(sizeof(uint64_t) * (size_t)b->level * (k + 1) * (k + 1) * N);
+    uint64_t *rot = malloc(sizeof(uint64_t) * N);
+    for (;;) {
+        pthread_mutex_lock(&J->mu);
+        size_t c = J->next++;
+        pthread_mutex_unlock(&J->mu);
+        if (c >= J->count) break;
+        size_t li = J->lut_idx ? J->lut_idx[c] : 0;
+        const size_t out_len = J->glwe_out ? gl : (size_t)(k * N + 1);
+        exact_mb_pbs_one(b, J->g, J->in + c * (size_t)(b->n + 1), J->out + c * out_len, J->luts + li * gl, acc, tmp,
+                         kb, rot, &s, J->glwe_out);
+    }
+    free(acc);
+    free(tmp);
+    free(kb);
+    free(rot);
+    free(s.state);
+    free(s.digits);
+    free(s.t);
+    return NULL;
+}
+
+void orc_exact_mb_pbs_batch(const uint64_t *bsk, int n, int k, int N, int base_log, int level, int g,
+                            const uint64_t *in, uint64_t *out, const uint64_t *luts, const uint32_t *lut_idx,
+                            size_t count, int threads, int glwe_out) {
+    exact_bsk b = {bsk, n, k, N, base_log, level};
+    exact_mb_job J = {&b, g, in, luts, lut_idx, out, count, 0};
+    J.glwe_out = glwe_out;
+    pthread_mutex_init(&J.mu, NULL);
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, exact_mb_worker, &J);
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    pthread_mutex_destroy(&J.mu);
+}

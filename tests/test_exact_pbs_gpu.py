@@ -141,3 +141,35 @@ def test_pbs_noise_full_2_2_vs_exact(orc, keys_2_2):
     B = 1024, which the factor-2 band holds."""
     k = keys_2_2
     _compare_noise(orc, k.params, k.lwe_sk, k.glwe_sk, k.bsk, 1024, 54, 0.1, 2.0)
+
+
+def test_single_group_multibit_within_reference_fft_tolerance(orc):
+    """Multi-bit g = 3 (BASELINE config 5 parameters) with ONE group: the GPU's fused keybundle +
+    external product against the exact standard-domain keybundle and exact external product
+    (orc.exact_mb_pbs).  Same accumulator and digits on both sides, so each accumulator
+    coefficient must be within the reference FFT tolerance times the 2^g GGSWs a keybundle sums."""
+    from tfhe_mi355 import Engine
+    from tfhe_mi355.parameters import PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS as MB
+
+    g, N = MB.grouping_factor, MB.polynomial_size
+    p = MB.with_(lwe_dimension=g)
+    lwe_sk = orc.binary_key(71, 1, g)
+    glwe_sk = orc.binary_key(71, 2, N)
+    bsk = orc.gen_mb_bsk(71, lwe_sk, glwe_sk, 1, N, p.pbs_base_log, p.pbs_level, g, p.glwe_modular_std_dev,
+                         threads=THREADS)
+    rng = np.random.default_rng(72)
+    acc = rng.integers(0, 2 ** 64, 2 * N, dtype=np.uint64)
+    cts = rng.integers(0, 2 ** 64, (16, g + 1), dtype=np.uint64)
+    cts[0, :g] = 0  # every selector's monomial is X^0
+    eng = Engine(p, 0)
+    eng.upload_bootstrap_key(bsk)
+    got = eng.blind_rotate(cts, acc)
+    got_lwe = eng.programmable_bootstrap(cts, acc)
+    eng.close()
+    exact = orc.exact_mb_pbs(bsk, g, 1, N, p.pbs_base_log, p.pbs_level, g, cts, acc, threads=THREADS, glwe_out=True)
+    exact_lwe = orc.exact_mb_pbs(bsk, g, 1, N, p.pbs_base_log, p.pbs_level, g, cts, acc, threads=THREADS)
+    tol = (1 << g) * external_product_tolerance(p)
+    for a, b in ((got, exact), (got_lwe, exact_lwe)):
+        worst = int(modular_distance(a, b).max())
+        print(f"multi-bit g={g}: max |GPU - exact| = 2^{np.log2(max(worst, 1)):.1f}, tolerance 2^{tol.bit_length() - 1}")
+        assert 0 < worst <= tol

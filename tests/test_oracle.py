@@ -209,3 +209,32 @@ def test_single_level_digit_shortcut_matches_decomposer(orc, beta):
         ref = orc.decompose(x, beta, 1)[0]
         ref = ref - (1 << 64) if ref >= (1 << 63) else ref
         assert d == ref, (hex(x), d, ref)
+
+
+def test_exact_multi_bit_pbs_vs_fft_oracle(orc):
+    """The FFT-free multi-bit PBS (exact standard-domain keybundles, exact external products)
+    against the FFT oracle's multi-bit PBS: with ONE group (n = g) both start from the same
+    accumulator and digits, so every output coefficient must agree within the reference FFT
+    product tolerance (fft/tests.rs:166-172) times the 2^g GGSWs a keybundle sums; with several
+    groups the two decrypt identically."""
+    from noise_tools import external_product_tolerance, modular_distance
+    from tfhe_mi355.parameters import PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS as MB
+
+    g, N = MB.grouping_factor, MB.polynomial_size
+    for n, seed in ((g, 61), (4 * g, 62)):
+        p = MB.with_(lwe_dimension=n)
+        lwe_sk = orc.binary_key(seed, 1, n)
+        glwe_sk = orc.binary_key(seed, 2, N)
+        bsk = orc.gen_mb_bsk(seed, lwe_sk, glwe_sk, 1, N, p.pbs_base_log, p.pbs_level, g, p.glwe_modular_std_dev,
+                             threads=8)
+        fb = orc.MultiBitFourierBsk(bsk, n, 1, N, p.pbs_base_log, p.pbs_level, g)
+        acc = orc.fill_accumulator(N, 1, 4, 4, lambda x: (x + 1) % 16)
+        msgs = np.arange(16) % 16
+        cts = orc.lwe_encrypt(seed + 1, lwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta), p.lwe_modular_std_dev)
+        fft = fb.pbs(cts, acc, threads=8)
+        exact = orc.exact_mb_pbs(bsk, n, 1, N, p.pbs_base_log, p.pbs_level, g, cts, acc, threads=8)
+        for out in (fft, exact):
+            assert np.array_equal(decode(orc.lwe_decrypt(glwe_sk, out), p.delta) % 16, (msgs + 1) % 16)
+        if n == g:
+            worst = int(modular_distance(fft, exact).max())
+            assert 0 < worst <= (1 << g) * external_product_tolerance(p)
