@@ -262,9 +262,9 @@ def host_info() -> dict:
 def cpu_baseline(params, bsk, cts, acc, threads: int, ksk=None):
     """The oracle's PBS (C restatement of the reference fft64 PBS) on the host cores, as the
     reference's pbs_throughput bench (benches/core_crypto/pbs_bench.rs:430-549: independent
-    ciphertexts over all threads).  Classic PBS runs oracle/pbs_simd.c: W ciphertexts per SIMD
-    register (AVX-512: 8, AVX2: 4), every lane the oracle's exact operation sequence
-    (bit-identical, tests/test_oracle_simd.py); multi-bit runs the scalar oracle.  With `ksk`
+    ciphertexts over all threads), through oracle/pbs_simd.c: W ciphertexts per SIMD register
+    (AVX-512: 8, AVX2: 4), every lane the oracle's exact operation sequence (classic and
+    multi-bit, bit-identical: tests/test_oracle_simd.py).  With `ksk`
     each ciphertext is keyswitched first (scalar oracle keyswitch, threads split the batch)."""
     sys.path.insert(0, ROOT)
     from concurrent.futures import ThreadPoolExecutor
@@ -278,22 +278,21 @@ def cpu_baseline(params, bsk, cts, acc, threads: int, ksk=None):
             return batch
         parts = np.array_split(batch, min(threads, batch.shape[0]))
         with ThreadPoolExecutor(len(parts)) as ex:
-            outs = list(ex.map(lambda c: O.keyswitch(ksk, p.big_lwe_dimension, p.lwe_dimension, p.ks_base_log,
-                                                     p.ks_level, c), parts))
+            outs = list(ex.map(lambda c: O.keyswitch_simd(ksk, p.big_lwe_dimension, p.lwe_dimension, p.ks_base_log,
+                                                          p.ks_level, c), parts))
         return np.concatenate(outs)
 
     O.build()
     if params.grouping_factor:
         fb = O.MultiBitFourierBsk(bsk, params.lwe_dimension, params.glwe_dimension, params.polynomial_size,
                                   params.pbs_base_log, params.pbs_level, params.grouping_factor)
-        run, lanes, how = fb.pbs, 1, "scalar oracle FFT, 1 PBS per thread"
     else:
         fb = O.FourierBsk(bsk, params.lwe_dimension, params.glwe_dimension, params.polynomial_size,
                           params.pbs_base_log, params.pbs_level)
-        lanes = O.simd_lib().simd_width()
-        run = fb.pbs_simd
-        how = (f"oracle/pbs_simd.c: {lanes} ciphertexts per {'AVX-512' if lanes == 8 else 'AVX2'} register, each lane "
-               f"the oracle's exact op sequence (bit-identical), {lanes} PBS per thread step")
+    lanes = O.simd_lib().simd_width()
+    run = fb.pbs_simd
+    how = (f"oracle/pbs_simd.c: {lanes} ciphertexts per {'AVX-512' if lanes == 8 else 'AVX2'} register, each lane "
+           f"the oracle's exact op sequence (bit-identical), {lanes} PBS per thread step")
     run(ks(cts[:lanes]), acc, threads=1)  # warm (page-in, tables)
     t = time.perf_counter()
     run(ks(cts[:lanes]), acc, threads=1)

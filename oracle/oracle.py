@@ -289,8 +289,22 @@ def simd_lib():
         L.simd_pbs_batch.restype = ctypes.c_int
         L.simd_pbs_batch.argtypes = [f64p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      u64p, u64p, u64p, u32p, ctypes.c_size_t, ctypes.c_int]
+        L.simd_keyswitch_batch.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, u64p, u64p,
+                                           ctypes.c_size_t]
+        L.simd_mb_pbs_batch.restype = ctypes.c_int
+        L.simd_mb_pbs_batch.argtypes = [f64p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, u64p, u64p, u64p, u32p, ctypes.c_size_t, ctypes.c_int]
         _simd = L
     return _simd
+
+
+def keyswitch_simd(ksk, in_dim, out_dim, base_log, level, cts) -> np.ndarray:
+    """orc keyswitch through the SIMD build (vectorised AXPY, bit-identical): the CPU baseline's KS."""
+    ksk = _u64(ksk)
+    x = _u64(cts).reshape(-1, in_dim + 1)
+    out = np.zeros((x.shape[0], out_dim + 1), dtype=np.uint64)
+    simd_lib().simd_keyswitch_batch(_p(ksk), in_dim, out_dim, base_log, level, _p(x), _p(out), x.shape[0])
+    return out
 
 
 class FourierBsk:
@@ -415,6 +429,23 @@ class MultiBitFourierBsk:
             idx = np.ascontiguousarray(lut_idx, dtype=np.uint32)
         lib().orc_mb_pbs_batch(self.h, _p(lwe_in), _p(out), _p(luts),
                                idx.ctypes.data_as(u32p) if idx is not None else None, cnt, threads)
+        return out
+
+    def pbs_simd(self, lwe_in, luts, lut_idx=None, threads=8) -> np.ndarray:
+        """Same multi-bit PBS through pbs_simd.c (W ciphertexts per SIMD register, bit-identical)."""
+        lwe_in = _u64(lwe_in).reshape(-1, self.n + 1)
+        luts = _u64(luts)
+        if getattr(self, "_fourier", None) is None:
+            self._fourier = self.fourier()
+        cnt = lwe_in.shape[0]
+        out = np.zeros((cnt, self.k * self.N + 1), dtype=np.uint64)
+        idx = None
+        if lut_idx is not None:
+            idx = np.ascontiguousarray(lut_idx, dtype=np.uint32)
+        rc = simd_lib().simd_mb_pbs_batch(self._fourier.ctypes.data_as(f64p), self.n, self.k, self.N, self.base_log,
+                                          self.level, self.g, _p(lwe_in), _p(out), _p(luts),
+                                          idx.ctypes.data_as(u32p) if idx is not None else None, cnt, threads)
+        assert rc == 0, "pbs_simd: unsupported shape"
         return out
 
 

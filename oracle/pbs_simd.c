@@ -550,3 +550,232 @@ int simd_pbs_batch(const double *fourier, int n, int k, int N, int base_log, int
     sfft_free(&b.fft);
     return 0;
 }
+
+/* The oracle's keyswitch (pbs_oracle.c orc_keyswitch_batch, lwe_keyswitch.rs:96-170), compiled
+ * here with the SIMD build's flags: the per-level AXPY over the output row vectorises (u64
+ * multiply-subtract, exact), so it is bit-identical by construction. */
+void simd_keyswitch_batch(const uint64_t *ksk, int in_dim, int out_dim, int base_log, int level, const uint64_t *in,
+                          uint64_t *out, size_t count) {
+    const uint64_t mask = (1ULL << base_log) - 1;
+    for (size_t c = 0; c < count; c++) {
+        const uint64_t *x = in + c * (size_t)(in_dim + 1);
+        uint64_t *o = out + c * (size_t)(out_dim + 1);
+        memset(o, 0, sizeof(uint64_t) * (out_dim + 1));
+        o[out_dim] = x[in_dim];
+        for (int i = 0; i < in_dim; i++) {
+            uint64_t state = closest_representable(x[i], base_log, level) >> (64 - base_log * level);
+            for (int l = 0; l < level; l++) {
+                const uint64_t d = decompose_one_level(base_log, &state, mask);
+                const uint64_t *row = ksk + ((size_t)i * level + l) * (size_t)(out_dim + 1);
+                for (int j = 0; j <= out_dim; j++) o[j] -= d * row[j];
+            }
+        }
+    }
+}
+
+/* ---- multi-bit PBS, W ciphertexts per register (pbs_oracle.c mb_pbs_one / mb_keybundle) ---- */
+/* frequency of FFT output position P (pbs_oracle.c pos_freq) */
+static int pos_freq(const sfft *f, int P) {
+    int fr = 0, mult = 1, L = f->M;
+    for (int st = 0; st < f->nrad; st++) {
+        const int m = L / f->rad[st];
+        fr += mult * (P / m);
+        P %= m;
+        mult *= f->rad[st];
+        L = m;
+    }
+    return fr;
+}
+/* spectrum of X^d at frequency fr (pbs_oracle.c mono_spectrum): exact i^q twist[r] */
+static inline void mono_spectrum(const sfft *f, uint32_t d, int fr, double *re, double *im) {
+    const uint32_t t = (d - 4u * d * (uint32_t)fr) & (uint32_t)(2 * f->N - 1);
+    const uint32_t q = t / (uint32_t)f->M, r = t % (uint32_t)f->M;
+    const double wr = f->twre[r], wi = f->twim[r];
+    switch (q) {
+    case 0: *re = wr; *im = wi; break;
+    case 1: *re = -wi; *im = wr; break;
+    case 2: *re = -wr; *im = -wi; break;
+    default: *re = wi; *im = -wr; break;
+    }
+}
+
+typedef struct {
+    simd_bsk b;  /* b.fourier: [n/g][2^g][L][k+1][k+1][M] complex, position order */
+    int g;
+    int *freq;
+} simd_mb_bsk;
+
+typedef struct {
+    lanes_scratch s;
+    uint64_t *tmp;
+    vcx *kb, *mono;
+} mb_scratch;
+
+/* external_product_add with a per-lane GGSW (the keybundles): out[(k+1)N][W] += KB (x) glwe[...] */
+static void external_product_add_v(const simd_bsk *b, const vcx *kb, const uint64_t *glwe, uint64_t *out,
+                                   lanes_scratch *s) {
+    const int k = b->k, N = b->N, M = N / 2, L = b->level, beta = b->base_log;
+    const size_t gl = (size_t)(k + 1) * N * W;
+    const uint64_t mask = (1ULL << beta) - 1;
+    for (size_t e = 0; e < gl; e++) s->state[e] = closest_representable(glwe[e], beta, L) >> (64 - beta * L);
+    int first = 1;
+    for (int lvl = L; lvl >= 1; lvl--) {
+        const vcx *lm = kb + (size_t)(lvl - 1) * (k + 1) * (k + 1) * M;
+        for (int row = 0; row <= k; row++) {
+            uint64_t *st = s->state + (size_t)row * N * W;
+            for (size_t e = 0; e < (size_t)N * W; e++) s->dig[e] = (int64_t)decompose_one_level(beta, &st[e], mask);
+            forward_integer(&b->fft, s->dig, s->fd);
+            for (int col = 0; col <= k; col++) {
+                const vcx *g = lm + ((size_t)row * (k + 1) + col) * M;
+                vcx *acc = s->facc + (size_t)col * M;
+                for (int f = 0; f < M; f++) {
+                    const vd gr = g[f].re, gi = g[f].im, dr = s->fd[f].re, di = s->fd[f].im;
+                    if (first) {
+                        acc[f].re = vfma(gr, dr, vneg(vmul(gi, di)));
+                        acc[f].im = vfma(gr, di, vmul(gi, dr));
+                    } else {
+                        acc[f].re = vfma(gr, dr, vfma(vneg(gi), di, acc[f].re));
+                        acc[f].im = vfma(gr, di, vfma(gi, dr, acc[f].im));
+                    }
+                }
+            }
+            first = 0;
+        }
+    }
+    for (int col = 0; col <= k; col++) backward_torus_add(&b->fft, s->facc + (size_t)col * M, out + (size_t)col * N * W);
+}
+
+static void mb_pbs_lanes(const simd_mb_bsk *mb, const uint64_t *const *in, const uint64_t *const *lut, mb_scratch *ms) {
+    const simd_bsk *b = &mb->b;
+    lanes_scratch *s = &ms->s;
+    const int n = b->n, k = b->k, N = b->N, M = N / 2, g = mb->g;
+    const size_t npoly = (size_t)b->level * (k + 1) * (k + 1);
+    const size_t ggsw_len = npoly * M * 2;  /* doubles */
+    const size_t gl = (size_t)(k + 1) * N * W;
+    for (int l = 0; l < W; l++) {  /* acc = LUT / X^{b~} */
+        const uint64_t d = modulus_switch(in[l][n], b->log2N);
+        const uint64_t full = d / N, rem = d % N;
+        for (int p = 0; p <= k; p++)
+            for (int j = 0; j < N; j++) {
+                const uint64_t src = j + rem;
+                uint64_t v = src < (uint64_t)N ? lut[l][(size_t)p * N + src] : 0 - lut[l][(size_t)p * N + src - N];
+                s->acc[((size_t)p * N + j) * W + l] = (full & 1) ? 0 - v : v;
+            }
+    }
+    double __attribute__((aligned(ALIGN))) mr[W], mi[W];
+    for (int j = 0; j < n / g; j++) {
+        const double *grp = b->fourier + (size_t)j * ((size_t)1 << g) * ggsw_len;
+        /* keybundle, per lane, in the oracle's order: GGSW_0, then sel = 1 .. 2^g - 1 */
+        for (size_t e = 0; e < npoly * M; e++) ms->kb[e] = (vcx){vset1(grp[2 * e]), vset1(grp[2 * e + 1])};
+        for (int sel = 1; sel < (1 << g); sel++) {
+            uint32_t d[W];
+            for (int l = 0; l < W; l++) {
+                uint64_t deg = 0;
+                for (int i = 0; i < g; i++)
+                    if ((sel >> (g - 1 - i)) & 1) deg += in[l][(size_t)j * g + i];
+                d[l] = (uint32_t)modulus_switch(deg, b->log2N);
+            }
+            for (int P = 0; P < M; P++) {
+                for (int l = 0; l < W; l++) mono_spectrum(&b->fft, d[l], mb->freq[P], &mr[l], &mi[l]);
+                ms->mono[P] = (vcx){vload(mr), vload(mi)};
+            }
+            const double *G = grp + (size_t)sel * ggsw_len;
+            for (size_t q = 0; q < npoly; q++)
+                for (int P = 0; P < M; P++) {
+                    const vd gr = vset1(G[2 * (q * M + P)]), gi = vset1(G[2 * (q * M + P) + 1]);
+                    const vcx m = ms->mono[P];
+                    vcx *o = &ms->kb[q * M + P];
+                    o->re = vfma(gr, m.re, vfma(vneg(gi), m.im, o->re));
+                    o->im = vfma(gr, m.im, vfma(gi, m.re, o->im));
+                }
+        }
+        /* acc <- ExtProd(KB, acc) into a zeroed GLWE (ping-pong) */
+        memset(ms->tmp, 0, sizeof(uint64_t) * gl);
+        external_product_add_v(b, ms->kb, s->acc, ms->tmp, s);
+        memcpy(s->acc, ms->tmp, sizeof(uint64_t) * gl);
+    }
+}
+
+typedef struct {
+    const simd_mb_bsk *mb;
+    const uint64_t *in, *luts;
+    const uint32_t *lut_idx;
+    uint64_t *out;
+    size_t count, next;
+    pthread_mutex_t mu;
+} simd_mb_job;
+
+static void *simd_mb_worker(void *arg) {
+    simd_mb_job *J = arg;
+    const simd_bsk *b = &J->mb->b;
+    const int k = b->k, N = b->N, M = N / 2;
+    const size_t gl = (size_t)(k + 1) * N * W;
+    mb_scratch ms;
+    lanes_scratch *s = &ms.s;
+    s->acc = aligned_alloc(ALIGN, sizeof(uint64_t) * gl);
+    s->ct1 = NULL;
+    s->state = aligned_alloc(ALIGN, sizeof(uint64_t) * gl);
+    s->dig = aligned_alloc(ALIGN, sizeof(int64_t) * (size_t)N * W);
+    s->fd = aligned_alloc(ALIGN, sizeof(vcx) * M);
+    s->facc = aligned_alloc(ALIGN, sizeof(vcx) * (size_t)(k + 1) * M);
+    ms.tmp = aligned_alloc(ALIGN, sizeof(uint64_t) * gl);
+    ms.kb = aligned_alloc(ALIGN, sizeof(vcx) * (size_t)b->level * (k + 1) * (k + 1) * M);
+    ms.mono = aligned_alloc(ALIGN, sizeof(vcx) * M);
+    const size_t out_len = (size_t)k * N + 1;
+    for (;;) {
+        pthread_mutex_lock(&J->mu);
+        const size_t c0 = J->next;
+        J->next += W;
+        pthread_mutex_unlock(&J->mu);
+        if (c0 >= J->count) break;
+        const uint64_t *in[W], *lut[W];
+        for (int l = 0; l < W; l++) {
+            const size_t c = c0 + l < J->count ? c0 + l : J->count - 1;
+            in[l] = J->in + c * (size_t)(b->n + 1);
+            lut[l] = J->luts + (J->lut_idx ? J->lut_idx[c] : 0) * (size_t)(k + 1) * N;
+        }
+        mb_pbs_lanes(J->mb, in, lut, &ms);
+        for (int l = 0; l < W && c0 + l < J->count; l++) {  /* sample extract at degree 0 */
+            uint64_t *o = J->out + (c0 + l) * out_len;
+            for (int p = 0; p < k; p++) {
+                const uint64_t *a = s->acc + (size_t)p * N * W + l;
+                o[(size_t)p * N] = a[0];
+                for (int j = 1; j < N; j++) o[(size_t)p * N + j] = 0 - a[(size_t)(N - j) * W];
+            }
+            o[(size_t)k * N] = s->acc[(size_t)k * N * W + l];
+        }
+    }
+    free(s->acc);
+    free(s->state);
+    free(s->dig);
+    free(s->fd);
+    free(s->facc);
+    free(ms.tmp);
+    free(ms.kb);
+    free(ms.mono);
+    return NULL;
+}
+
+/* Multi-bit PBS (deterministic group order) of `count` ciphertexts, W per thread step;
+ * fourier = the oracle's multi-bit Fourier BSK (orc_mb_fbsk_copy). */
+int simd_mb_pbs_batch(const double *fourier, int n, int k, int N, int base_log, int level, int g, const uint64_t *in,
+                      uint64_t *out, const uint64_t *luts, const uint32_t *lut_idx, size_t count, int threads) {
+    if (g < 1 || n % g) return -1;
+    simd_mb_bsk mb = {{n, k, N, base_log, level, 0}, g, NULL};
+    while ((1 << mb.b.log2N) < N) mb.b.log2N++;
+    if (sfft_init(&mb.b.fft, N)) return -1;
+    mb.b.fourier = fourier;
+    mb.freq = malloc(sizeof(int) * (N / 2));
+    for (int P = 0; P < N / 2; P++) mb.freq[P] = pos_freq(&mb.b.fft, P);
+    simd_mb_job J = {&mb, in, luts, lut_idx, out, count, 0};
+    pthread_mutex_init(&J.mu, NULL);
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, simd_mb_worker, &J);
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    pthread_mutex_destroy(&J.mu);
+    free(mb.freq);
+    sfft_free(&mb.b.fft);
+    return 0;
+}

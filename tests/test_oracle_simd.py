@@ -42,3 +42,29 @@ def test_simd_pbs_bit_identical_to_oracle(orc, variant):
     assert np.array_equal(out, exp), f"{np.count_nonzero(out != exp)} words differ"
     if variant == orc.simd_variant():
         assert np.array_equal(fb.pbs_simd(cts, luts, lut_idx=idx, threads=2), exp)
+
+
+def test_simd_keyswitch_bit_identical_to_oracle(orc, keys_2_2):
+    p = keys_2_2.params
+    rng = np.random.default_rng(4)
+    cts = rng.integers(0, 2 ** 64, (5, p.big_lwe_dimension + 1), dtype=np.uint64)
+    exp = orc.keyswitch(keys_2_2.ksk, p.big_lwe_dimension, p.lwe_dimension, p.ks_base_log, p.ks_level, cts)
+    got = orc.keyswitch_simd(keys_2_2.ksk, p.big_lwe_dimension, p.lwe_dimension, p.ks_base_log, p.ks_level, cts)
+    assert np.array_equal(got, exp)
+
+
+def test_simd_multibit_pbs_bit_identical_to_oracle(orc):
+    from tfhe_mi355.parameters import PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS as MB
+
+    g, N, n = MB.grouping_factor, MB.polynomial_size, 9
+    p = MB.with_(lwe_dimension=n)
+    lwe_sk = orc.binary_key(9, 1, n)
+    glwe_sk = orc.binary_key(9, 2, N)
+    bsk = orc.gen_mb_bsk(9, lwe_sk, glwe_sk, 1, N, p.pbs_base_log, p.pbs_level, g, p.glwe_modular_std_dev, threads=8)
+    fb = orc.MultiBitFourierBsk(bsk, n, 1, N, p.pbs_base_log, p.pbs_level, g)
+    acc = orc.fill_accumulator(N, 1, 4, 4, lambda x: (5 * x) % 16)
+    rng = np.random.default_rng(10)
+    cts = rng.integers(0, 2 ** 64, (11, n + 1), dtype=np.uint64)  # ragged lane tail
+    cts[0, :n] = 0
+    exp = fb.pbs(cts, acc, threads=4)
+    assert np.array_equal(fb.pbs_simd(cts, acc, threads=3), exp)
