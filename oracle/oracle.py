@@ -550,13 +550,18 @@ class OracleEngine:
     """The oracle (CPU restatement) behind the Engine's host API, so host-side orchestration
     (shortint / integer layers) can run its exact DAG on the CPU as the parity reference."""
 
-    def __init__(self, params, threads=8):
+    def __init__(self, params, threads=8, simd=False):
+        """simd: run the PBS and keyswitch through pbs_simd.c (bit-identical; the CPU baseline)."""
         import sys
 
         O = sys.modules[__name__]
         build()
-        self.O, self.p, self.threads = O, params, threads
+        self.O, self.p, self.threads, self.simd = O, params, threads, simd
         self.fb = self.ksk = None
+
+    def _pbs(self, x, luts, lut_indexes):
+        f = self.fb.pbs_simd if self.simd else self.fb.pbs
+        return f(x, luts, lut_indexes, threads=self.threads)
 
     def upload_bootstrap_key(self, bsk):
         p = self.p
@@ -572,18 +577,19 @@ class OracleEngine:
         p = self.p
         parts = [c for c in np.array_split(np.asarray(x), min(self.threads, len(x))) if len(c)]
         with ThreadPoolExecutor(len(parts)) as ex:
-            outs = list(ex.map(lambda c: self.O.keyswitch(self.ksk, p.big_lwe_dimension, p.lwe_dimension,
-                                                          p.ks_base_log, p.ks_level, c), parts))
+            ks = self.O.keyswitch_simd if self.simd else self.O.keyswitch
+            outs = list(ex.map(lambda c: ks(self.ksk, p.big_lwe_dimension, p.lwe_dimension, p.ks_base_log,
+                                            p.ks_level, c), parts))
         return np.concatenate(outs)
 
     def keyswitch_programmable_bootstrap(self, x, luts, lut_indexes=None):
-        return self.fb.pbs(self.keyswitch(x), luts, lut_indexes, threads=self.threads)
+        return self._pbs(self.keyswitch(x), luts, lut_indexes)
 
     def programmable_bootstrap(self, x, luts, lut_indexes=None):
-        return self.fb.pbs(x, luts, lut_indexes, threads=self.threads)
+        return self._pbs(x, luts, lut_indexes)
 
     def programmable_bootstrap_keyswitch(self, x, luts, lut_indexes=None):
-        return self.keyswitch(self.fb.pbs(x, luts, lut_indexes, threads=self.threads))
+        return self.keyswitch(self._pbs(x, luts, lut_indexes))
 
     def blind_rotate(self, x, luts, lut_indexes=None):
         return self.fb.blind_rotate(x, luts, lut_indexes, threads=self.threads)

@@ -68,3 +68,18 @@ def test_simd_multibit_pbs_bit_identical_to_oracle(orc):
     cts[0, :n] = 0
     exp = fb.pbs(cts, acc, threads=4)
     assert np.array_equal(fb.pbs_simd(cts, acc, threads=3), exp)
+
+
+def test_oracle_engine_simd_mode_matches_scalar(orc, keys_2_2):
+    """bench.py's FheUint32-multiply CPU leg runs OracleEngine(simd=True): same words as the scalar engine."""
+    p = keys_2_2.params
+    acc = orc.fill_accumulator(p.polynomial_size, 1, 4, 4, lambda x: (x * x) % 16)
+    rng = np.random.default_rng(11)
+    cts = rng.integers(0, 2 ** 64, (9, p.big_lwe_dimension + 1), dtype=np.uint64)
+    outs = []
+    for simd in (False, True):
+        eng = orc.OracleEngine(p, threads=4, simd=simd)
+        eng.upload_bootstrap_key(keys_2_2.bsk)
+        eng.upload_keyswitch_key(keys_2_2.ksk)
+        outs.append(eng.keyswitch_programmable_bootstrap(cts, acc))
+    assert np.array_equal(outs[0], outs[1])
