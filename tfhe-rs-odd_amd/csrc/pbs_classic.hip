@@ -111,9 +111,7 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
     const int n = a.n;
     const int beta = a.base_log;
     const uint32_t dmask = (1u << beta) - 1;
-    const int dk1 = 31 - beta;                        // L = 1 digit constants (digit_l1)
-    const uint32_t dc1 = dmask;
-    const int32_t dh1 = (int32_t)(1u << (beta - 1)) - 1;
+    const DigitL1 digit_l1(beta);                      // L = 1 digits
     BlockSync sync;       // cross-wave: spectrum exchange
 #if PBS_WAVE_LOCAL
     WaveLocalSync wsync;  // wave-private buffer reuse
@@ -243,11 +241,18 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
         wsync();
         // (X^d p)[j] = -p[N-d+j] for j < d, p[j-d] otherwise (sign flipped again when the
         // rotation passes a full N); only the top 32 bits of ct1 feed the decomposition.
-        const int rbase = lane - rem;
+        // Source index jj = lane - rem + 64 h wraps (jj < 0) exactly for h < hcut, so the gather
+        // address is a select between two lane bases with 8*64*h in the ds_read offset field (no
+        // per-coefficient index arithmetic); xpos may sit up to 8(N-1) bytes below xb64, which is
+        // still inside LDS since the twist table (8N bytes) precedes every exchange buffer.
+        const int rbase = lane - rem;  // in (-N, 64)
+        const int hcut = (63 - rbase) >> 6;
+        const uint64_t *xpos = xb64 + rbase;
+        const uint64_t *xneg = xpos + N;
         auto ct1_hi = [&](int h) -> uint32_t {
-            const int jj = rbase + 64 * h;
-            const bool neg = (jj < 0) != full_odd;
-            const uint64_t x = xb64[(unsigned)jj & (unsigned)(N - 1)];
+            const bool wrap = h < hcut;
+            const bool neg = wrap != full_odd;
+            const uint64_t x = (wrap ? xneg : xpos)[64 * h];
             const uint64_t r = neg ? 0 - x : x;
             return (uint32_t)((r - c0[h]) >> 32);
         };
@@ -267,8 +272,8 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
             for (int b = 0; b < V; b++) {
                 int32_t d0, d1;
                 if constexpr (L == 1) {
-                    d0 = digit_l1(ct1_hi(b), dk1, dc1, beta, dh1);
-                    d1 = digit_l1(ct1_hi(V + b), dk1, dc1, beta, dh1);
+                    d0 = digit_l1(ct1_hi(b));
+                    d1 = digit_l1(ct1_hi(V + b));
                 } else {
                     d0 = decomp_digit32(st[b], beta, dmask);
                     d1 = decomp_digit32(st[V + b], beta, dmask);

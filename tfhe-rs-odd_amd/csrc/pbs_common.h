@@ -133,10 +133,20 @@ __device__ __forceinline__ uint32_t decomp_state32_hi(uint32_t x_hi, int beta) {
 // L = 1: s = ((x >> (63 - beta)) + 1) >> 1, digit = s mod 2^beta balanced into
 // (-2^(beta-1), 2^(beta-1)] -- the SignedDecomposer's carry rule for one level, since the
 // state left after the level is 0 or 1 and only 1 when the digit is 0.
-// With c = 2^beta - 1 and h = 2^(beta-1) - 1:  digit = bfe(a + c, 1, beta) - h, a = x_hi >> (31 - beta).
-__device__ __forceinline__ int32_t digit_l1(uint32_t x_hi, int k, uint32_t c, int beta, int32_t h) {
-    return (int32_t)__builtin_amdgcn_ubfe((x_hi >> k) + c, 1, beta) - h;
-}
+// With c = 2^beta - 1, k = 31 - beta and h = 2^(beta-1) - 1 the digit is
+// bfe((x_hi >> k) + c, 1, beta) - h; adding c << k before the shift (the low k bits of x_hi
+// cannot carry into bit k) turns the bfe into the plain shift by 32 - beta:
+// digit = ((x_hi + (c << k)) >> (32 - beta)) - h  -- three VALU ops instead of four.
+struct DigitL1 {
+    uint32_t ck;  // (2^beta - 1) << (31 - beta)
+    int sh;       // 32 - beta
+    int32_t h;    // 2^(beta-1) - 1
+    __device__ __forceinline__ explicit DigitL1(int beta)
+        : ck(((1u << beta) - 1) << (31 - beta)), sh(32 - beta), h((int32_t)(1u << (beta - 1)) - 1) {}
+    __device__ __forceinline__ int32_t operator()(uint32_t x_hi) const {
+        return (int32_t)((x_hi + ck) >> sh) - h;
+    }
+};
 __device__ __forceinline__ int32_t decomp_digit32(uint32_t &state, int beta, uint32_t mask) {
     uint32_t res = state & mask;
     state >>= beta;

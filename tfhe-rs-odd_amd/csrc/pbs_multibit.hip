@@ -70,9 +70,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
     const int n = a.n;
     const int beta = a.base_log;
     const uint32_t dmask = (1u << beta) - 1;
-    const int dk1 = 31 - beta;
-    const uint32_t dc1 = dmask;
-    const int32_t dh1 = (int32_t)(1u << (beta - 1)) - 1;
+    const DigitL1 digit_l1(beta);
     BlockSync sync;
     WaveLocalSync wsync;
 
@@ -164,8 +162,8 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
             for (int b = 0; b < V; b++) {
                 int32_t d0, d1;
                 if constexpr (L == 1) {
-                    d0 = digit_l1((uint32_t)(c0[b] >> 32), dk1, dc1, beta, dh1);
-                    d1 = digit_l1((uint32_t)(c0[V + b] >> 32), dk1, dc1, beta, dh1);
+                    d0 = digit_l1((uint32_t)(c0[b] >> 32));
+                    d1 = digit_l1((uint32_t)(c0[V + b] >> 32));
                 } else {
                     d0 = decomp_digit32(st[b], beta, dmask);
                     d1 = decomp_digit32(st[V + b], beta, dmask);
@@ -332,9 +330,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
     const int lane0 = threadIdx.x & 63;
     const int n = a.n;
     const int beta = a.base_log;
-    const int dk1 = 31 - beta;
-    const uint32_t dc1 = (1u << beta) - 1;
-    const int32_t dh1 = (int32_t)(1u << (beta - 1)) - 1;
+    const DigitL1 digit_l1(beta);
     WaveLocalSync wsync;
 
     for (int e = threadIdx.x; e < M; e += blockDim.x) lds[Lay::twist_off + e] = a.twist[e];
@@ -380,8 +376,8 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
             cx v[V];
 #pragma unroll
             for (int b = 0; b < V; b++) {
-                const int32_t d0 = digit_l1((uint32_t)(c0[b] >> 32), dk1, dc1, beta, dh1);
-                const int32_t d1 = digit_l1((uint32_t)(c0[V + b] >> 32), dk1, dc1, beta, dh1);
+                const int32_t d0 = digit_l1((uint32_t)(c0[b] >> 32));
+                const int32_t d1 = digit_l1((uint32_t)(c0[V + b] >> 32));
                 const double2 w = s_twist[lane + 64 * b];
                 v[b] = cmulw(cx{(double)d0, (double)d1}, w.x, w.y);
             }
