@@ -17,8 +17,9 @@
 // polynomial); the (k+1) row spectra of a ciphertext are published to LDS and wave c computes
 // output column c = sum_r F_r * GGSW[r][c] (GGSW streamed from L2/MALL, 16 B per lane, coalesced;
 // MAC operands read back from LDS at N = 2048 and 1024), inverse-FFTs it and adds it back.  FFT
-// twiddles and the twist live in LDS.  At 2_2: 2 waves per SIMD (<= 256 VGPRs, 242 used), LDS
+// twiddles and the twist live in LDS.  At 2_2: 2 waves per SIMD (<= 256 VGPRs, 244 used), LDS
 // 31 KiB of tables + 8 x 16 KiB exchange buffers + sync flags = 159 KiB -> 4 ciphertexts per CU.
+// The grid is persistent with a global ciphertext ticket queue at 2_2 (PbsConfig::PERSIST).
 // Synchronisation: wave-private LDS reuse is ordered with wave-local fences; the spectrum exchange
 // among the (k+1) waves of ONE ciphertext uses LDS flag words (GroupSync, pbs_common.h), so the
 // ciphertexts of a workgroup drift apart instead of running in lockstep behind s_barrier.
