@@ -191,9 +191,10 @@ def test_oracle_keyswitch_round_trip(orc, keys_2_2):
 
 @pytest.mark.parametrize("beta", [23, 21, 15, 10])
 def test_single_level_digit_shortcut_matches_decomposer(orc, beta):
-    """The HIP kernel's L=1 digit shortcut (pbs_classic.hip digit_l1):
-    bfe((x_hi >> (31 - beta)) + 2^beta - 1, 1, beta) - (2^(beta-1) - 1)
-    must equal the SignedDecomposer digit (decomposer.rs:99-153, iter.rs:134-141)."""
+    """The HIP kernels' L=1 digit shortcut (pbs_common.h DigitL1):
+    ((x_hi + ((2^beta - 1) << (31 - beta))) >> (32 - beta)) - (2^(beta-1) - 1), and the bfe form
+    bfe((x_hi >> (31 - beta)) + 2^beta - 1, 1, beta) - (2^(beta-1) - 1) it replaced, must equal the
+    SignedDecomposer digit (decomposer.rs:99-153, iter.rs:134-141)."""
     rng = np.random.default_rng(beta)
     xs = [int(x) for x in rng.integers(0, 2 ** 64, 3000, dtype=np.uint64)]
     # rounding ties and overflow edges: values around multiples of 2^(63-beta)
@@ -206,9 +207,11 @@ def test_single_level_digit_shortcut_matches_decomposer(orc, beta):
         hi = x >> 32
         t = ((hi >> (31 - beta)) + mask) & 0xFFFFFFFF
         d = ((t >> 1) & mask) - h
+        d_shift = (((hi + (mask << (31 - beta))) & 0xFFFFFFFF) >> (32 - beta)) - h
         ref = orc.decompose(x, beta, 1)[0]
         ref = ref - (1 << 64) if ref >= (1 << 63) else ref
         assert d == ref, (hex(x), d, ref)
+        assert d_shift == ref, (hex(x), d_shift, ref)
 
 
 def test_exact_multi_bit_pbs_vs_fft_oracle(orc):
