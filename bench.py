@@ -216,10 +216,11 @@ def roofline(tag, p, units_per_launch: int, kernel_ms: float, kname: str, with_k
             r["valu_issue"] = {
                 "per_wave_cycle": pmc["sq_active_inst_valu_per_wave_cycle"],
                 "simd_busy_grbm": pmc.get("valu_busy"),
-                "note": ("PMC of the main kernel: SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES per resident wave (x 2 "
+                "avg_waves_per_simd": pmc.get("avg_waves_per_simd"),
+                "note": ("PMC of the main kernel: SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES per resident wave (x the "
                          "resident waves per SIMD = the fraction of SIMD issue cycles with a VALU instruction); "
-                         "simd_busy_grbm normalises by GRBM_GUI_ACTIVE instead and reads ~0.8x lower (the SQ "
-                         "wave-cycle count implies 1.6 resident waves/SIMD where the launch holds 2)"),
+                         "simd_busy_grbm is the same count normalised by GRBM_GUI_ACTIVE x SIMDs, and "
+                         "avg_waves_per_simd = SQ_WAVE_CYCLES / (GRBM_GUI_ACTIVE x SIMDs)"),
                 "source": pmc["_file"]}
     r["kernel"] = kname
     r["kernel_ms"] = kernel_ms
