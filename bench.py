@@ -219,8 +219,8 @@ def roofline(tag, p, units_per_launch: int, kernel_ms: float, kname: str, with_k
                 "avg_waves_per_simd": pmc.get("avg_waves_per_simd"),
                 "note": ("PMC of the main kernel: SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES per resident wave (x the "
                          "resident waves per SIMD = the fraction of SIMD issue cycles with a VALU instruction); "
-                         "simd_busy_grbm is the same count normalised by GRBM_GUI_ACTIVE x SIMDs, and "
-                         "avg_waves_per_simd = SQ_WAVE_CYCLES / (GRBM_GUI_ACTIVE x SIMDs)"),
+                         "simd_busy_grbm is the same count normalised by the kernel's GPU-active cycles x 1024 "
+                         "SIMDs, avg_waves_per_simd = SQ_WAVE_CYCLES over the same (scripts/pmc_workload.py)"),
                 "source": pmc["_file"]}
     r["kernel"] = kname
     r["kernel_ms"] = kernel_ms
