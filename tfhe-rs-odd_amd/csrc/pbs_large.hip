@@ -106,6 +106,27 @@ __device__ __forceinline__ size_t spec_off(int wave, int h, int s, int lane) {
 
 }  // namespace
 
+// Accumulator row layout: position p at u64 index 2 (p mod M) + (p div M), so the pair (j, j + M)
+// that one folded complex coefficient is made of sits in one 16-byte word (one load / store in
+// top_inv, one self and one rotated load per row in the digits).
+__device__ __forceinline__ int accx(int p) { return 2 * (p & (LM - 1)) + (p >> 14); }
+static_assert(LM == 1 << 14, "accx assumes M = 2^14");
+typedef unsigned long long acc_pair __attribute__((ext_vector_type(2)));
+// ct1 = X^{a~} acc - acc at positions j and j + M of one row (rem = a~ mod N, full_odd = a~ >= N):
+// the rotated sources j - rem and j + M - rem lie in ONE pair word, q = (j - rem) mod M, with its
+// halves swapped when only the first one wraps
+__device__ __forceinline__ void ct1_pair(const uint64_t *acc, int j, int rem, bool full_odd, uint64_t &d0,
+                                         uint64_t &d1) {
+    const acc_pair self = *reinterpret_cast<const acc_pair *>(acc + 2 * j);
+    const int jj0 = j - rem;  // in (-N, M)
+    const acc_pair rot = *reinterpret_cast<const acc_pair *>(acc + 2 * (jj0 & (LM - 1)));
+    const bool swap = jj0 < 0 && jj0 >= -LM;
+    const uint64_t x0 = swap ? rot.y : rot.x, x1 = swap ? rot.x : rot.y;
+    const bool neg0 = (jj0 < 0) != full_odd, neg1 = (jj0 + LM < 0) != full_odd;
+    d0 = (neg0 ? 0 - x0 : x0) - self.x;
+    d1 = (neg1 ? 0 - x1 : x1) - self.y;
+}
+
 // acc[ct] = LUT[idx] / X^{b~}  (bootstrap.rs:255-275)
 template <int K>
 __global__ void __launch_bounds__(256) large_init_kernel(LargePbsLaunch a, int ct0, int cnt) {
@@ -123,7 +144,7 @@ __global__ void __launch_bounds__(256) large_init_kernel(LargePbsLaunch a, int c
     const int src = j + rem;
     const bool wrap = src >= LN;
     const uint64_t v = lut[wrap ? src - LN : src];
-    a.acc[e] = (wrap != (bool)(full & 1)) ? 0 - v : v;
+    a.acc[(e / LN) * LN + accx(j)] = (wrap != (bool)(full & 1)) ? 0 - v : v;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -175,13 +196,11 @@ __device__ __forceinline__ void top_fwd_body(const LargePbsLaunch &a, int ct0, i
     for (int b = 0; b < 16; b++) {
         const int j = t + 1024 * b;
         int32_t dg[2], dl[2];
+        uint64_t dd[2];  // ct1 = X^{a~} acc - acc  (polynomial_wrapping_monic_monomial_mul_and_subtract)
+        ct1_pair(acc, j, rem, full_odd, dd[0], dd[1]);
 #pragma unroll
         for (int half = 0; half < 2; half++) {
-            // ct1 = X^{a~} acc - acc  (polynomial_wrapping_monic_monomial_mul_and_subtract)
-            const int jj = j + half * LM - rem;
-            const bool neg = (jj < 0) != full_odd;
-            const uint64_t x = acc[(unsigned)jj & (unsigned)(LN - 1)];
-            const uint64_t d = (neg ? 0 - x : x) - acc[j + half * LM];
+            const uint64_t d = dd[half];
             uint32_t st = decomp_state32_hi<L>((uint32_t)(d >> 32), beta);
             dg[half] = decomp_digit32(st, beta, dmask);               // level L
             dl[half] = L == 2 ? decomp_digit32(st, beta, dmask) : 0;  // level L-1
@@ -620,14 +639,11 @@ __device__ __forceinline__ uint64_t group_digit_word(const LargePbsLaunch &a, in
     const int beta = a.base_log;
     const uint32_t dmask = (1u << beta) - 1;
     const uint64_t *acc = a.acc + ((size_t)cl * 2 + r) * LN;
-    uint64_t w = 0;
+    uint64_t w = 0, dd[2];
+    ct1_pair(acc, j, rem, full_odd, dd[0], dd[1]);  // ct1 = X^{a~} acc - acc
 #pragma unroll
     for (int half = 0; half < 2; half++) {
-        // ct1 = X^{a~} acc - acc  (polynomial_wrapping_monic_monomial_mul_and_subtract)
-        const int jj = j + half * LM - rem;
-        const bool neg = (jj < 0) != full_odd;
-        const uint64_t xv = acc[(unsigned)jj & (unsigned)(LN - 1)];
-        const uint64_t d = (neg ? 0 - xv : xv) - acc[j + half * LM];
+        const uint64_t d = dd[half];
         uint32_t st = decomp_state32_hi<L>((uint32_t)(d >> 32), beta);
         const int32_t dg = decomp_digit32(st, beta, dmask);  // level L
         const int32_t dl = decomp_digit32(st, beta, dmask);  // level L-1
@@ -691,10 +707,12 @@ __device__ __forceinline__ void top_inv_body(const LargePbsLaunch &a, int cl, in
     for (int b = 0; b < 16; b++) {
         const int j = t + 1024 * b;
         const cx w = gld(a.twist + j);
-        uint64_t lo = acc[j], hi = acc[j + LM];
+        acc_pair pr = *reinterpret_cast<const acc_pair *>(acc + 2 * j);
+        uint64_t lo = pr.x, hi = pr.y;
         backward_add(u[b], w, lo, hi, k32);  // the resident key carries the 1/M
-        acc[j] = lo;
-        acc[j + LM] = hi;
+        pr.x = lo;
+        pr.y = hi;
+        *reinterpret_cast<acc_pair *>(acc + 2 * j) = pr;
     }
 }
 
@@ -735,10 +753,10 @@ __global__ void __launch_bounds__(256) large_extract_kernel(LargePbsLaunch a, in
     const uint64_t *acc = a.acc + (size_t)cl * (K + 1) * LN;
     uint64_t v;
     if (q == (size_t)K * LN) {
-        v = acc[(size_t)K * LN];
+        v = acc[(size_t)K * LN];  // accx(0) = 0
     } else {
         const int p = (int)(q / LN), j = (int)(q % LN);
-        v = j == 0 ? acc[(size_t)p * LN] : 0 - acc[(size_t)p * LN + LN - j];
+        v = j == 0 ? acc[(size_t)p * LN] : 0 - acc[(size_t)p * LN + accx(LN - j)];
     }
     a.lwe_out[(size_t)(ct0 + cl) * per + q] = v;
 }
