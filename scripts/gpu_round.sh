@@ -14,7 +14,7 @@ step() {  # step NAME TIMEOUT CMD...
 STAGES=${STAGES:-"tests smoke bench prof"}
 for s in $STAGES; do
   case $s in
-    tests) step gpu_tests 600 python -m pytest tests -m gpu -x -q ;;
+    tests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 5 --warmup 1 ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
