@@ -10,7 +10,7 @@ i=0
 P3="SQ_LDS_CMD_FIFO_FULL SQ_INST_LEVEL_LDS SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_ACTIVE_INST_MISC SQ_INSTS_SALU"
 for P in "$P1" "$P2" "$P3"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $P -d gpurun_out/pmc_sq$i -o run --output-format csv -- python3 bench.py ${BENCH_ARGS:---steps 2 --warmup 1} --no-cpu-baseline > gpurun_out/pmc_sq$i.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $P -d gpurun_out/pmc_sq$i -o run --output-format csv -- python3 bench.py ${BENCH_ARGS:---params 2_2 --steps 2 --warmup 1} --no-cpu-baseline > gpurun_out/pmc_sq$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"; tail -3 gpurun_out/pmc_sq$i.log
   [ $rc -eq 0 ] || exit $rc
 done

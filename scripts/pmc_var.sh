@@ -9,7 +9,7 @@ i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp -d gpurun_out/pmc_$v/g$i -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_${v}_g$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $grp -d gpurun_out/pmc_$v/g$i -o run --output-format csv -- python3 bench.py --params 2_2 --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_${v}_g$i.log 2>&1
   rc=$?; echo "group $i ($grp) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc_${v}_g$i.log; exit $rc; fi
 done <<GROUPS

@@ -50,3 +50,20 @@ def test_gpus_mismatch_with_world_is_an_error():
     p, _ = _run(["--gpus", "2", "--launch-selftest"], extra_env={"WORLD_SIZE": "1"})
     assert p.returncode != 0
     assert "WORLD_SIZE" in (p.stderr + p.stdout)
+
+
+@pytest.mark.timeout(180)
+def test_other_workloads_failed_child_is_reported_not_fatal(monkeypatch):
+    """The default run's side measurements (other_workloads): a child that cannot run (no GPU
+    here) is reported as an error entry with its wall time; the caller keeps going."""
+    import argparse
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    monkeypatch.setattr(bench, "OTHER_WORKLOADS", (("2_2ks", 1),))
+    monkeypatch.setenv("CUDA_VISIBLE_DEVICES", "")  # the child must fail fast on this CPU box
+    res = bench.other_workloads(argparse.Namespace(seed=1))
+    assert set(res) == {"2_2ks"}
+    assert "error" in res["2_2ks"] and res["2_2ks"]["wall_s"] > 0
