@@ -653,8 +653,11 @@ __device__ __forceinline__ uint64_t group_digit_word(const LargePbsLaunch &a, in
 }
 
 // digits of CMUX i: one thread per (ciphertext, j < M), both rows in one 16-byte store
-__global__ void __launch_bounds__(256) large_digits_kernel(LargePbsLaunch a, int ct0, int i) {
-    constexpr int PER = LM / 256;  // workgroups per ciphertext
+#ifndef LARGE_DIGT
+#define LARGE_DIGT 256  // digits-kernel workgroup size
+#endif
+__global__ void __launch_bounds__(LARGE_DIGT) large_digits_kernel(LargePbsLaunch a, int ct0, int i) {
+    constexpr int PER = LM / LARGE_DIGT;  // workgroups per ciphertext
     // XCD-aware: ciphertext cl on XCD group cl % 8, as its grouped-CMUX workgroups
     const int x = blockIdx.x & 7, m = blockIdx.x >> 3;
     const int cl = x + 8 * (m / PER), sub = m % PER;
@@ -663,7 +666,7 @@ __global__ void __launch_bounds__(256) large_digits_kernel(LargePbsLaunch a, int
     const uint32_t at = pbs_modulus_switch<15>(in[i]);
     const bool full_odd = (at / LN) & 1;
     const int rem = at % LN;
-    const int j = sub * 256 + threadIdx.x;
+    const int j = sub * LARGE_DIGT + threadIdx.x;
     typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
     const u64x2 w = {group_digit_word(a, cl, 0, j, full_odd, rem), group_digit_word(a, cl, 1, j, full_odd, rem)};
     reinterpret_cast<u64x2 *>(group_digits(a, cl))[j] = w;
@@ -818,9 +821,9 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
         if constexpr (K == 1 && L == 2) {
             if (LARGE_GROUP_SUB) {
                 const unsigned grp_blocks = (unsigned)((cnt + 7) / 8) * 8 * 4 * GroupCfg::PARTS;
-                const unsigned dig_blocks = (unsigned)((cnt + 7) / 8) * 8 * (LM / 256);
+                const unsigned dig_blocks = (unsigned)((cnt + 7) / 8) * 8 * (LM / LARGE_DIGT);
                 for (int i = 0; i < a.n; i++) {
-                    hipLaunchKernelGGL(large_digits_kernel, dim3(dig_blocks), dim3(256), 0, s, a, ct0, i);
+                    hipLaunchKernelGGL(large_digits_kernel, dim3(dig_blocks), dim3(LARGE_DIGT), 0, s, a, ct0, i);
                     hipLaunchKernelGGL(large_group_cmux_kernel, dim3(grp_blocks), dim3(GroupCfg::THREADS), GroupCfg::LDS,
                                        s, a, ct0, i);
                     hipLaunchKernelGGL((large_top_inv_kernel<K>), dim3(top_blocks), dim3(TOPT), 0, s, a, ct0, i);
