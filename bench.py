@@ -59,7 +59,7 @@ PARAMS = {  # --params choice -> (parameter set name, workload text, kernel name
             "pbs_multibit_shared_kernel<2048,1,1,3>"),
     "4_4": ("PARAM_MESSAGE_4_CARRY_4_KS_PBS",
             "BASELINE config 3: shortint apply_lookup_table (keyswitch -> PBS) at N=32768 per GPU batch",
-            "large_digits_kernel + large_group_cmux_kernel + large_top_inv_kernel<1> (+ ks_mfma_kernel)"),
+            "large_group_cmux_kernel (+ large_digits_kernel + large_top_inv_kernel<1> per CMUX, ks_mfma_kernel)"),
     "mul32": ("PARAM_MESSAGE_2_CARRY_2_KS_PBS",
               "BASELINE config 4: FheUint32 multiply (16-block radix DAG, radix_parallel/mul.rs), "
               "K independent pairs per GPU, every DAG layer one batched KS+PBS launch, the whole DAG "
@@ -67,7 +67,7 @@ PARAMS = {  # --params choice -> (parameter set name, workload text, kernel name
               "pbs_classic_kernel<2048,1,1> + ks_mfma_kernel"),
     "mb2": ("PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS",
             "batch of 4096 independent multi-bit (grouping 2) PBS per GPU, identity LUT",
-            "pbs_multibit_kernel<2048,1,1,2>"),
+            "pbs_multibit_shared_kernel<2048,1,1,2>"),
     # the fork's gadget parameter sets (gadget/parameters/mod.rs), same PBS workload
     "manticore": ("MANTICORE_PARAMETERS",
                   "batch of 4096 independent classic PBS per GPU at the fork's MANTICORE_PARAMETERS",
@@ -138,94 +138,141 @@ def pbs_flops(p) -> float:
     return per * p.lwe_dimension
 
 
-def large_model_bytes(p, chunk: int, with_ks: bool, units: int) -> float:
-    """Algorithmic bytes per PBS of the N = 32768 grouped CMUX: per CMUX and
-    ciphertext the accumulator is read by large_digits and read+written by large_top_inv
-    (3 (k+1) N 8 B), the packed digits ((k+1) M 8 B) are written and read once, the sub-block
-    outputs U ((k+1) M 16 B) likewise (the 4 group workgroups of a ciphertext re-read its digits
-    from L2, not counted); GGSW_i (L (k+1)^2 M 16 B) is read once per chunk.  Plus the LWE in/out
-    and LUT, and with the keyswitch the KSK once per launch."""
-    M = p.polynomial_size // 2
-    k1 = p.glwe_dimension + 1
-    per_cmux = 3 * k1 * p.polynomial_size * 8 + 2 * k1 * M * 8 + 2 * k1 * M * 16
-    per_cmux += p.pbs_level * k1 * k1 * M * 16 / chunk
-    b = p.lwe_dimension * per_cmux + io_bytes(p, with_ks) + 8 * k1 * p.polynomial_size
-    if with_ks:
-        b += 8 * p.glwe_dimension * p.polynomial_size * p.ks_level * (p.lwe_dimension + 1) / units
-    return b
-
-
 PMC_ALIAS = {"mul32": "2_2ks"}  # the multiply DAG runs the 2_2 KS+PBS kernels: per-PBS traffic of that workload
+PMC_ROUND = "r03"
+
+# dominant kernel of each workload: (kernel-timer family, rocprofv3 name normalised as
+# scripts/pmc_workload.py does).  Its average duration comes from the engine's HIP-event timer
+# on the launch stream (tfhe_mi355_kernel_timing_*), its counters from the PMC file.
+DOMINANT = {
+    "2_2": ("pbs_classic_kernel", "pbs_classic_kernel<2048,1,1>"),
+    "2_2ks": ("pbs_classic_kernel", "pbs_classic_kernel<2048,1,1>"),
+    "mul32": ("pbs_classic_kernel", "pbs_classic_kernel<2048,1,1>"),
+    "mb3": ("pbs_multibit", "pbs_multibit_shared_kernel<2048,1,1,3>"),
+    "mb2": ("pbs_multibit", "pbs_multibit_shared_kernel<2048,1,1,2>"),
+    "4_4": ("large_group_cmux_kernel", "large_group_cmux_kernel"),
+    "manticore": ("pbs_classic_kernel", "pbs_classic_kernel<1024,1,2>"),
+    "ascon": ("pbs_classic_kernel", "pbs_classic_kernel<1024,2,3>"),
+    "simon": ("pbs_classic_kernel", "pbs_classic_kernel<512,3,2>"),
+    "tfhelib": ("pbs_classic_kernel", "pbs_classic_kernel<1024,2,1>"),
+    "aes40": ("pbs_classic_kernel", "pbs_classic_kernel<512,3,4>"),
+    "sha3": ("pbs_classic_kernel", "pbs_classic_kernel<256,5,1>"),
+}
 
 
-def load_pmc(tag: str):
-    """Committed rocprofv3 PMC summary of this workload (scripts/pmc_workload.sh ->
-    profiles/r02_pmc_<tag>.json): HBM bytes per unit (2*FETCH_SIZE + WRITE_SIZE, gfx950
-    correction of MI355X_MICROARCH.md 'HBM') and the SQ VALU-busy fraction."""
-    for name in (f"r02_pmc_{PMC_ALIAS.get(tag, tag)}.json",):
-        path = os.path.join(ROOT, "profiles", name)
-        if os.path.exists(path):
-            d = json.load(open(path))
-            d["_file"] = f"profiles/{name}"
-            return d
-    return None
+def load_pmc(tag: str, kernel: str):
+    """The committed rocprofv3 PMC summary of this workload (scripts/pmc_workload.sh ->
+    profiles/r03_pmc_<tag>.json) and its entry for `kernel`.  A file without an entry for the
+    kernel the bench times is refused (returns the reason instead): counters of another kernel
+    are not evidence for this one."""
+    name = f"{PMC_ROUND}_pmc_{PMC_ALIAS.get(tag, tag)}.json"
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None, f"no PMC summary profiles/{name}"
+    d = json.load(open(path))
+    e = (d.get("by_kernel") or {}).get(kernel)
+    if e is None:
+        return None, (f"refused: profiles/{name} holds counters for {sorted(d.get('by_kernel') or {})}, "
+                      f"not for the timed kernel {kernel}")
+    e = dict(e)
+    e.pop("sq_counters_sum", None)
+    e["_file"] = f"profiles/{name}"
+    e["_all"] = d.get("by_kernel")
+    return e, None
 
 
-def roofline(tag, p, units_per_launch: int, kernel_ms: float, kname: str, with_ks: bool):
-    """Roofline object of the dominant kernel.  N <= 2048: bound by FP64 VALU issue (DESIGN.md 5.1
-    -- the Fourier BSK is L2/MALL-resident, measured HBM traffic is ~1% of peak); N = 32768: the
-    BSK (2.09 GB) and the spectra stream through HBM/MALL, so the HBM model bounds it."""
-    secs = kernel_ms * 1e-3
-    flop = pbs_flops(p) * units_per_launch
-    fp64 = flop / secs / 1e12
-    pmc = load_pmc(tag)
-    traffic = None
-    if pmc and "hbm_bytes_per_unit" in pmc:
-        traffic = pmc["hbm_bytes_per_unit"] * units_per_launch
-    stream_b = pbs_streaming_bytes(p) + (io_bytes(p, True) - io_bytes(p, False) if with_ks else 0)
-    hbm = {
-        "streaming_model_bytes_per_pbs": stream_b,
-        "streaming_model_GBps": stream_b * units_per_launch / secs / 1e9,
-        "min_unique_bytes_per_pbs": pbs_min_unique_bytes(p, units_per_launch, with_ks),
-        "measured_traffic_GBps": traffic / secs / 1e9 if traffic else None,
-        "measured_frac_of_peak": traffic / secs / 1e9 / HBM_PEAK_GBS if traffic else None,
-        "measured_bytes_per_pbs": traffic / units_per_launch if traffic else None,
-        "traffic_source": pmc["_file"] if pmc else None,
-    }
-    if p.polynomial_size > 2048:
-        chunk = min(units_per_launch, 128)
-        model_b = large_model_bytes(p, chunk, with_ks, units_per_launch)
-        achieved = model_b * units_per_launch / secs / 1e9
-        r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-             "model": (f"N = 32768 grouped-CMUX bytes (DESIGN.md 5.3): {model_b:,.0f} B per PBS (accumulator, "
-                       f"packed digits and sub-block outputs through HBM/MALL every CMUX, GGSW once per chunk "
-                       f"of {chunk}, KSK once per launch) x PBS per launch / kernel time; the PMC traffic "
-                       "(L2<->fabric, Infinity-Cache hits included) is the measured counterpart"),
-             "model_bytes_per_pbs": model_b,
-             "fp64": {"achieved": fp64, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                      "frac": fp64 / FP64_PEAK_TFLOPS, "flop_per_pbs": pbs_flops(p)}}
+def large_group_flops(p) -> float:
+    """FP64 flop of large_group_cmux_kernel per ciphertext and CMUX (k = 1, L = 2):
+    twist of the (k+1)L digit polynomials (6 flop per point), their whole forward FFTs (the top
+    radix-16 share and the 1024-point sub-FFTs: 5 M log2 M each), the MAC ((k+1)^2 L M 8) and the
+    (k+1) inverse sub-FFTs (5 M log2(1024) each; the top DIT stage runs in large_top_inv)."""
+    M = p.polynomial_size // 2
+    k1, L = p.glwe_dimension + 1, p.pbs_level
+    return (k1 * L * (6 * M + 5 * M * math.log2(M)) + k1 * k1 * L * M * 8 + k1 * 5 * M * 10)
+
+
+def large_memory_model(p):
+    """Bytes per ciphertext and CMUX of the two memory kernels of the N = 32768 grouped CMUX
+    (DESIGN.md 5.3): large_digits reads the accumulator rows (twice: self and rotated) and writes
+    the packed digits; large_top_inv reads U and the accumulator and writes the accumulator."""
+    M, N = p.polynomial_size // 2, p.polynomial_size
+    k1 = p.glwe_dimension + 1
+    return {"large_digits_kernel": 2 * k1 * N * 8 + k1 * M * 8,
+            "large_top_inv_kernel": k1 * M * 16 + 2 * k1 * N * 8}
+
+
+def roofline(tag, p, units_per_launch: int, step_ms: float, kname: str, with_ks: bool, ktimes: dict | None):
+    """Roofline object of the DOMINANT kernel (FP64-VALU bound for every PBS kernel here: DESIGN.md
+    5): achieved = its algorithmic flop per launch / its average launch duration from the engine's
+    HIP-event timer on the launch stream; traffic and VALU issue from the PMC entry of that same
+    kernel.  The whole step's FP64 rate and the HBM/fabric byte models sit beside it."""
+    fam, pmc_name = DOMINANT.get(tag, ("pbs_classic_kernel", kname))
+    steps_flop = pbs_flops(p) * units_per_launch
+    fp64_step = steps_flop / (step_ms * 1e-3) / 1e12
+    large = p.polynomial_size > 2048
+    chunk = min(units_per_launch, 128) if large else units_per_launch
+    kt = (ktimes or {}).get(fam)
+    if kt:
+        kernel_ms, timed = kt
+        kernel_src = f"engine HIP-event timer on the launch stream, {timed} timed launches"
+    else:  # one launch per step (or a replayed graph): the step's own events
+        kernel_ms, timed = step_ms, None
+        kernel_src = "HIP events around the whole step on the launch stream (no per-kernel timer)"
+    flop_launch = large_group_flops(p) * chunk if large else steps_flop
+    fp64 = flop_launch / (kernel_ms * 1e-3) / 1e12
+    if tag == "mul32":
+        pmc, why = None, ("the multiply DAG replays the 2_2 KS+PBS kernels in one hipGraph: their per-kernel "
+                          "counters are those of the 2_2ks line")
     else:
-        r = {"bound": "fp64-valu", "achieved": fp64, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-             "frac": fp64 / FP64_PEAK_TFLOPS, "traffic": traffic,
-             "model": (f"FP64 flop model (SURVEY.md 8d): {pbs_flops(p):,.0f} flop per PBS x PBS per launch / "
-                       "kernel time (HIP events on the launch stream"
-                       + (", keyswitch included in the time, its int8 MFMA work not counted)" if with_ks else ")")),
-             "flop_per_pbs": pbs_flops(p)}
-        if pmc and "sq_active_inst_valu_per_wave_cycle" in pmc:
-            r["valu_issue"] = {
-                "per_wave_cycle": pmc["sq_active_inst_valu_per_wave_cycle"],
-                "simd_busy_grbm": pmc.get("valu_busy"),
-                "avg_waves_per_simd": pmc.get("avg_waves_per_simd"),
-                "note": ("PMC of the main kernel: SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES per resident wave (x the "
-                         "resident waves per SIMD = the fraction of SIMD issue cycles with a VALU instruction); "
-                         "simd_busy_grbm is the same count normalised by the kernel's GPU-active cycles x 1024 "
-                         "SIMDs, avg_waves_per_simd = SQ_WAVE_CYCLES over the same (scripts/pmc_workload.py)"),
-                "source": pmc["_file"]}
-    r["kernel"] = kname
-    r["kernel_ms"] = kernel_ms
-    r["units_per_launch"] = units_per_launch
-    r["hbm"] = hbm
+        pmc, why = load_pmc(tag, pmc_name)
+    traffic = pmc.get("hbm_bytes_per_dispatch") if pmc else None
+    r = {"bound": "fp64-valu", "achieved": fp64, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+         "frac": fp64 / FP64_PEAK_TFLOPS, "traffic": traffic,
+         "kernel": pmc_name, "kernel_ms": kernel_ms, "kernel_ms_source": kernel_src,
+         "flop_per_launch": flop_launch,
+         "units_per_launch": chunk,
+         "model": ((f"large_group_cmux_kernel FP64 flop per ciphertext and CMUX {large_group_flops(p):,.0f} "
+                    f"(twist, forward FFTs incl. the top radix-16 share, MAC, inverse sub-FFTs) x {chunk} ciphertexts "
+                    f"per launch / its average launch duration") if large else
+                   (f"FP64 flop model (SURVEY.md 8d): {pbs_flops(p):,.0f} flop per PBS x {units_per_launch} PBS per "
+                    f"launch / the kernel's average launch duration")),
+         "traffic_note": ("L2<->fabric bytes per launch of this kernel (2 FETCH_SIZE + WRITE_SIZE, gfx950 correction; "
+                          "Infinity-Cache hits included)" if pmc else why),
+         "whole_step": {"fp64_tflops": fp64_step, "frac": fp64_step / FP64_PEAK_TFLOPS, "step_ms": step_ms,
+                        "flop_per_pbs": pbs_flops(p),
+                        "note": "PBS flop model x PBS per step / step time" + (
+                            " (keyswitch included in the time, its int8 MFMA work not counted)" if with_ks else "")}}
+    if pmc:
+        r["valu_issue"] = {k: pmc.get(k) for k in ("sq_active_inst_valu_per_wave_cycle", "avg_waves_per_simd",
+                                                   "valu_busy", "sq_wait_inst_any_per_wave_cycle",
+                                                   "sq_wait_any_per_wave_cycle", "lds_bank_conflict_frac",
+                                                   "l2_hit_rate") if pmc.get(k) is not None}
+        r["valu_issue"]["source"] = pmc["_file"]
+        r["valu_issue"]["note"] = ("per-wave-cycle fractions x avg_waves_per_simd = share of SIMD issue cycles; "
+                                   "valu_busy = the same over GRBM_GUI_ACTIVE x 1024 SIMDs (scripts/pmc_workload.py)")
+    stream_b = pbs_streaming_bytes(p) + (io_bytes(p, True) - io_bytes(p, False) if with_ks else 0)
+    secs = step_ms * 1e-3
+    r["hbm"] = {"streaming_model_bytes_per_pbs": stream_b,
+                "streaming_model_GBps": stream_b * units_per_launch / secs / 1e9,
+                "min_unique_bytes_per_pbs": pbs_min_unique_bytes(p, units_per_launch, with_ks),
+                "note": "BSK-streaming model (SURVEY.md 8d) over the whole step; >8 TB/s means on-chip reuse"}
+    if large and ktimes:
+        mem = {}
+        for kn, b in large_memory_model(p).items():
+            t = ktimes.get(kn)
+            if not t:
+                continue
+            e = (pmc or {}).get("_all", {}).get(kn) or {}
+            ach = b * chunk / (t[0] * 1e-3) / 1e9
+            mem[kn] = {"bound": "fabric (L2 <-> Infinity Cache / HBM)", "model_bytes_per_launch": b * chunk,
+                       "kernel_ms": t[0], "achieved_GBps": ach, "frac_of_hbm_peak": ach / HBM_PEAK_GBS,
+                       "pmc_bytes_per_launch": e.get("hbm_bytes_per_dispatch")}
+        r["memory_kernels"] = mem
+        r["memory_kernels_note"] = (f"per-CMUX memory kernels on a chunk of {chunk}: the chunk's accumulators, digits "
+                                    "and sub-block outputs (~1.5 MiB per ciphertext) stay in the 256 MB Infinity Cache, "
+                                    "so these byte rates are fabric rates, not DRAM rates (MI355X_MICROARCH.md 'HBM')")
+    if ktimes:
+        r["kernel_times_ms"] = {k: v[0] for k, v in ktimes.items()}
     return r
 
 
@@ -346,35 +393,91 @@ def launch_ranks(args) -> int:
     return subprocess.call(cmd, env=env)
 
 
-OTHER_WORKLOADS = (("2_2ks", 3), ("mb3", 3), ("mb2", 3), ("4_4", 3), ("mul32", 2))
+# The other BASELINE configurations measured beside the headline by the default run:
+# (entry name, --params, extra options).  `4_4_full` is config 3 at its stated size (65,536
+# ciphertexts in one call, a GLOBAL batch: split over the ranks at N > 1, i.e. strong scaling for
+# that entry), warmed up on its first 1024 ciphertexts.
+OTHER_WORKLOADS = (
+    ("2_2ks", "2_2ks", {"steps": 3}),
+    ("mb3", "mb3", {"steps": 3}),
+    ("mb2", "mb2", {"steps": 3}),
+    ("4_4", "4_4", {"steps": 3}),
+    ("mul32", "mul32", {"steps": 2}),
+    ("4_4_full", "4_4", {"steps": 1, "global_batch": 65536, "warmup_batch": 1024}),
+)
+
+
+def summarize(line: dict) -> dict:
+    rl = line.get("roofline") or {}
+    return {"value": line["value"], "unit": line["unit"], "ms_per_step": line["ms_per_step"],
+            "steps": line["steps"], "n_gpus": line["n_gpus"], "world_size": line.get("world_size"),
+            "scaling": line.get("scaling"), "workload": line["config"]["workload"],
+            "batch": line["config"].get("global_batch", line["config"].get("global_pairs")),
+            "kernel": rl.get("kernel"), "bound": rl.get("bound"), "frac": rl.get("frac"),
+            "check": line.get("check")}
+
+
+def _child_args(args, params, opts) -> list:
+    a = ["--params", params, "--steps", str(opts["steps"]), "--warmup", str(opts.get("warmup", 1)),
+         "--no-cpu-baseline", "--no-host-abi", "--seed", str(args.seed)]
+    if opts.get("global_batch"):
+        a += ["--global-batch", str(opts["global_batch"])]
+    if opts.get("warmup_batch"):
+        a += ["--warmup-batch", str(opts["warmup_batch"])]
+    return a
 
 
 def other_workloads(args) -> dict:
-    """The other BASELINE configurations (KS+PBS, multi-bit, N = 32768, FheUint32 multiply), each
-    run once as a child `bench.py --params X` BEFORE this process touches the GPU, so the default
-    run also measures them under the caller's clock; summarised into the headline line (the
-    headline value stays the 2_2 PBS rate).  A failed child is reported, not fatal."""
+    """N = 1: the other configurations, each run once as a child `bench.py --params X` BEFORE this
+    process touches the GPU, so the default run also measures them under the caller's clock;
+    summarised into the headline line (the headline value stays the 2_2 PBS rate).  A failed
+    child is reported, not fatal."""
     res = {}
-    for tag, steps in OTHER_WORKLOADS:
-        cmd = [sys.executable, os.path.abspath(__file__), "--params", tag, "--steps", str(steps), "--warmup", "1",
-               "--no-cpu-baseline", "--no-host-abi", "--seed", str(args.seed)]
+    for name, params, opts in OTHER_WORKLOADS:
+        cmd = [sys.executable, os.path.abspath(__file__)] + _child_args(args, params, opts)
         t = time.perf_counter()
         try:
-            cp = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+            cp = subprocess.run(cmd, capture_output=True, text=True, timeout=420)
             lines = [l for l in cp.stdout.splitlines() if l.startswith("{")]
             if cp.returncode != 0 or not lines:
-                res[tag] = {"error": f"rc={cp.returncode}: {cp.stderr.strip()[-300:]}"}
+                res[name] = {"error": f"rc={cp.returncode}: {cp.stderr.strip()[-300:]}"}
             else:
-                d = json.loads(lines[-1])
-                rl = d.get("roofline") or {}
-                res[tag] = {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"],
-                            "steps": d["steps"], "workload": d["config"]["workload"],
-                            "kernel": rl.get("kernel"), "bound": rl.get("bound"), "frac": rl.get("frac"),
-                            "check": d.get("check")}
+                res[name] = summarize(json.loads(lines[-1]))
         except subprocess.TimeoutExpired:
-            res[tag] = {"error": "timeout after 300 s"}
-        res[tag]["wall_s"] = time.perf_counter() - t
-        print(f"bench.py: {tag} done in {res[tag]['wall_s']:.1f} s", file=sys.stderr, flush=True)
+            res[name] = {"error": "timeout after 420 s"}
+        res[name]["wall_s"] = time.perf_counter() - t
+        print(f"bench.py: {name} done in {res[name]['wall_s']:.1f} s", file=sys.stderr, flush=True)
+    return res
+
+
+def other_workloads_ranks(args, R, runner) -> dict:
+    """N > 1 (every rank of the driver's torch.distributed.run runs this): the same configurations
+    in-process, one after the other on the job's process group, each a full multi-rank run
+    (keys broadcast once, contiguous shards, barrier-bracketed timing, max wall over ranks), before
+    the headline.  `runner(args) -> line` (rank 0) runs one workload; the CPU self-test passes a
+    stub.  Device memory of one workload is released before the next."""
+    import copy
+    import gc
+
+    res = {}
+    for name, params, opts in OTHER_WORKLOADS:
+        a = copy.copy(args)
+        a.params, a.steps, a.warmup = params, opts["steps"], opts.get("warmup", 1)
+        a.no_cpu_baseline = a.no_host_abi = True
+        a.global_batch = opts.get("global_batch", 0)
+        a.warmup_batch = opts.get("warmup_batch", 0)
+        a.batch = args.batch if args.launch_selftest else 0
+        a.other = None
+        t = time.perf_counter()
+        line = runner(a)
+        if R.rank == 0:
+            res[name] = summarize(line)
+            res[name]["wall_s"] = time.perf_counter() - t
+            print(f"bench.py: {name} done in {res[name]['wall_s']:.1f} s", file=sys.stderr, flush=True)
+        gc.collect()
+        if R.device.type == "cuda":
+            R.torch.cuda.synchronize(R.device)
+            R.torch.cuda.empty_cache()
     return res
 
 
@@ -458,11 +561,25 @@ def aggregate(R: Ranks, units: int, wall: float, ok: int, of: int, lo: int, hi: 
 def run_selftest(args) -> int:
     import torch
 
+    R = Ranks(torch.device("cpu"), os.environ.get("BENCH_DIST_BACKEND", "gloo"))
+    other = None
+    if args.params is None and not args.no_other_workloads and R.world > 1:
+        other = other_workloads_ranks(args, R, lambda a: selftest_line(a, R))
+    line = selftest_line(args, R)
+    if R.rank == 0:
+        if other is not None:
+            line["other_workloads"] = other
+        print(json.dumps(line), flush=True)
+    R.finish()
+    return 0
+
+
+def selftest_line(args, R) -> dict | None:
+    """One stub workload through the rank/shard/aggregation code (rank 0 gets the line)."""
     from tfhe_mi355.distributed import shard_range
 
-    R = Ranks(torch.device("cpu"), os.environ.get("BENCH_DIST_BACKEND", "gloo"))
     B = args.batch or 64
-    G = R.world * B
+    G = args.global_batch or R.world * B
     lo, hi = shard_range(G, R.rank, R.world)
     msgs = np.random.default_rng(args.seed).integers(0, 16, G).astype(np.uint64)[lo:hi]
     per_step = 0.02 * (R.rank + 1)   # ranks run at different speeds: the max must win
@@ -482,17 +599,16 @@ def run_selftest(args) -> int:
     wall = time.perf_counter() - t0
     ok = int(np.count_nonzero(out == msgs))
     agg = aggregate(R, (hi - lo) * args.steps, wall, ok, hi - lo, lo, hi)
-    if R.rank == 0:
-        line = {"metric": "launch self-test (stub step, no GPU)", "selftest": True,
-                "value": agg["value"], "unit": "stub units/s", "n_gpus": R.world, "steps": args.steps,
-                "warmup": args.warmup, "ms_per_step": agg["wall_max"] / args.steps * 1e3,
-                "check": {"decrypted_ok": agg["ok"], "of": agg["of"]},
-                "config": {"global_batch": G, "batch_per_rank": B, "shards": agg["shards"],
-                           "stub_seconds_per_step": [0.02 * (r + 1) for r in range(R.world)]},
-                "units_total": agg["units"], "wall_max_s": agg["wall_max"], **R.info()}
-        print(json.dumps(line), flush=True)
-    R.finish()
-    return 0
+    if R.rank != 0:
+        return None
+    return {"metric": "launch self-test (stub step, no GPU)", "selftest": True,
+            "value": agg["value"], "unit": "stub units/s", "n_gpus": R.world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": agg["wall_max"] / args.steps * 1e3,
+            "scaling": "strong" if args.global_batch else "weak",
+            "check": {"decrypted_ok": agg["ok"], "of": agg["of"]},
+            "config": {"workload": f"stub {args.params or 'headline'}", "global_batch": G, "batch_per_rank": B,
+                       "shards": agg["shards"], "stub_seconds_per_step": [0.02 * (r + 1) for r in range(R.world)]},
+            "units_total": agg["units"], "wall_max_s": agg["wall_max"], **R.info()}
 
 
 # ---------------------------------------------------------------------------------------------
@@ -514,6 +630,10 @@ def main():
                     help="2_2 = the BASELINE metric; 2_2ks = KS+PBS; mb3/mb2 = multi-bit PBS (config 5)")
     ap.add_argument("--launch-selftest", action="store_true",
                     help="exercise the rank launch / shard / aggregation path on the CPU (gloo, stub step)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="total ciphertexts over all ranks (split into contiguous shards: strong scaling)")
+    ap.add_argument("--warmup-batch", type=int, default=0,
+                    help="warm-up launches use only the first N ciphertexts of the rank's batch")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -523,18 +643,16 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}; n_gpus is taken from the world that runs")
     if args.launch_selftest:
         sys.exit(run_selftest(args))
-    # the default invocation (no --params) on one GPU also measures the other configurations
+    # the default invocation (no --params) also measures the other configurations: on one GPU as
+    # child processes before this one touches the GPU, on N GPUs in-process on every rank
+    default_run = args.params is None and not args.no_other_workloads
     args.other = None
-    if args.params is None and ws == 1 and not args.no_other_workloads:
+    if default_run and ws == 1:
         args.other = other_workloads(args)
     args.params = args.params or "2_2"
 
     import torch
 
-    from tfhe_mi355.parameters import ALL
-
-    pname, workload, kname = PARAMS[args.params]
-    P = ALL[pname]
     _, world, local = env_world()
     # one process per GPU; on a box with fewer GPUs than ranks (a rehearsal of the multi-rank
     # path, BENCH_DIST_BACKEND=gloo) ranks share devices round-robin
@@ -542,6 +660,20 @@ def main():
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     R = Ranks(device, os.environ.get("BENCH_DIST_BACKEND", "nccl"))  # nccl = RCCL over xGMI
+    if default_run and ws > 1:
+        args.other = other_workloads_ranks(args, R, lambda a: run_workload(a, R))
+    line = run_workload(args, R)
+    if R.rank == 0:
+        print(json.dumps(line), flush=True)
+    R.finish()
+
+
+def run_workload(args, R) -> dict | None:
+    """One configuration on every rank; rank 0 returns its JSON line (others None)."""
+    from tfhe_mi355.parameters import ALL
+
+    pname, workload, kname = PARAMS[args.params]
+    P = ALL[pname]
     if args.params == "mul32":
         return run_mul32(args, P, workload, kname, R)
     return run_pbs(args, P, pname, workload, kname, R)
@@ -633,8 +765,9 @@ def run_pbs(args, P, pname, workload, kname, R):
     msg_space = P.message_modulus * P.carry_modulus
     eng, lwe_sk, glwe_sk, bsk, ksk, setup = make_keys(args, P, R, with_ks)
 
-    G = R.world * B
+    G = args.global_batch or R.world * B   # --global-batch: fixed total (strong scaling)
     lo, hi = shard_range(G, R.rank, R.world)
+    B = hi - lo if args.global_batch else B
     msgs = np.random.default_rng(args.seed).integers(0, msg_space, G).astype(np.uint64)[lo:hi]
     key, std = (glwe_sk, P.glwe_modular_std_dev) if with_ks else (lwe_sk, P.lwe_modular_std_dev)
     cts = client.lwe_encrypt(args.seed * 1000 + R.rank, key, msgs * np.uint64(P.delta), std)
@@ -647,14 +780,17 @@ def run_pbs(args, P, pname, workload, kname, R):
     need = eng.ks_pbs_scratch_bytes(nb) if with_ks else eng.pbs_scratch_bytes(nb)
     d_scratch = torch.empty(max(need, 1), dtype=torch.uint8, device=R.device)
 
-    def step():
+    def step(cnt=nb):
         if with_ks:
-            eng.keyswitch_programmable_bootstrap_async(d_in, d_out, d_lut, 1, nb, d_scratch, stream=stream)
+            eng.keyswitch_programmable_bootstrap_async(d_in, d_out, d_lut, 1, cnt, d_scratch, stream=stream)
         else:
-            eng.programmable_bootstrap_async(d_in, d_out, d_lut, 1, nb, stream=stream, d_scratch=d_scratch)
+            eng.programmable_bootstrap_async(d_in, d_out, d_lut, 1, cnt, stream=stream, d_scratch=d_scratch)
 
     for _ in range(args.warmup):
-        step()
+        step(min(nb, args.warmup_batch) if args.warmup_batch else nb)
+    # per-kernel durations of the timed steps (HIP events on the launch stream around every launch
+    # of a classic / multi-bit PBS, every 16th CMUX launch of the N = 32768 kernels)
+    eng.kernel_timing(16 if P.polynomial_size > 2048 else 1)
     R.barrier()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
@@ -664,7 +800,9 @@ def run_pbs(args, P, pname, workload, kname, R):
         e.record(stream)
     R.barrier()
     wall = time.perf_counter() - t0
-    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
+    step_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
+    ktimes = eng.kernel_times()
+    eng.kernel_timing(0)
 
     out = d_out.cpu().numpy().view(np.uint64)
     dec = client.decode(client.lwe_decrypt(glwe_sk, out), P.delta) % np.uint64(msg_space)
@@ -692,7 +830,7 @@ def run_pbs(args, P, pname, workload, kname, R):
             "warmup": args.warmup,
             "ms_per_step": agg["wall_max"] / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.global_batch else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded LWE encryptions of uniform messages; keys from the engine's client-side keygen)",
@@ -708,7 +846,7 @@ def run_pbs(args, P, pname, workload, kname, R):
                 "parallelism": f"dp{R.world} (contiguous batch shards, BSK replicated by one RCCL broadcast)",
             },
             **R.info(),
-            "roofline": roofline(args.params, P, nb, kernel_ms, kname, with_ks),
+            "roofline": roofline(args.params, P, nb, step_ms, kname, with_ks, ktimes),
             "check": {"decrypted_ok": agg["ok"], "of": agg["of"]},
             "setup": setup,
         }
@@ -719,8 +857,8 @@ def run_pbs(args, P, pname, workload, kname, R):
         if R.world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or cpu_share()
             line["cpu_baseline"] = cpu_baseline(P, bsk, cts, acc, threads, ksk)
-        print(json.dumps(line), flush=True)
-    R.finish()
+        return line
+    return None
 
 
 def run_mul32(args, P, workload, kname, R):
@@ -788,7 +926,7 @@ def run_mul32(args, P, workload, kname, R):
     if R.rank == 0:
         pbs_rate = agg["value"] * pbs_per_mul
         units = int(round(pbs_per_mul * (hi - lo)))
-        rl = roofline("mul32", P, units, step_ms, kname, True)
+        rl = roofline("mul32", P, units, step_ms, kname, True, None)
         rl["model"] += "; the step is the whole multiply DAG (11 KS+PBS layers and the LWE additions)"
         line = {
             "metric": "FheUint32 multiplies/sec (PARAM_MESSAGE_2_CARRY_2 radix, 16 blocks) at 1/2/4/8 MI355X",
@@ -830,8 +968,8 @@ def run_mul32(args, P, workload, kname, R):
                            f"bit-identical) behind the engine API, {threads} threads ({cw:.1f} s); reference published 333 ms/mul "
                            f"on a 128-vCPU m6i.metal (benchmarks.md:17)"),
             }
-        print(json.dumps(line), flush=True)
-    R.finish()
+        return line
+    return None
 
 
 def RadixSlice(rb, n):

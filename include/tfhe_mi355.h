@@ -70,6 +70,17 @@ const char *tfhe_mi355_last_error(void);
 /* Number of visible GPUs. */
 int tfhe_mi355_device_count(int *out_count);
 
+/* Per-kernel timing (profiling aid; the counterpart of the reference's `__profiling` feature,
+ * tfhe/Cargo.toml:131, which un-inlines the FFT and external-product pieces for perf): with
+ * `every` > 0 the device launchers of this context bracket every `every`-th launch of each kernel
+ * family with HIP events on the launch stream (never while the stream is being captured);
+ * `every` = 0 turns it off.  Enabling clears earlier totals.  Entries are read one by one:
+ * index -> (kernel family name, total ms, timed launches); the call waits for the recorded
+ * events and fails past the last entry. */
+int tfhe_mi355_kernel_timing_enable(TfheMi355Context *ctx, int every);
+int tfhe_mi355_kernel_timing_entry(TfheMi355Context *ctx, size_t index, char *name, size_t name_len,
+                                   double *total_ms, uint64_t *launches);
+
 /* Page-locked (pinned) host memory for batch buffers.  The synchronous host-pointer entry points
  * detect pinned input/output buffers and DMA them directly, chunk by chunk, overlapped with the
  * kernels (no host staging copies); pageable buffers go through the engine's pinned staging.
@@ -204,6 +215,9 @@ int tfhe_mi355_packing_keyswitch_key_upload(TfheMi355Context *ctx, const uint64_
 int tfhe_mi355_packing_keyswitch(TfheMi355Context *ctx, const uint64_t *lwe_in, uint64_t *glwe_out, size_t count);
 int tfhe_mi355_packing_keyswitch_async(TfheMi355Context *ctx, const uint64_t *d_lwe_in, uint64_t *d_glwe_out,
                                        size_t count, void *d_scratch, size_t scratch_bytes, void *stream);
+/* Device scratch (bytes) of the async packing keyswitch.  The packing key's decomposition (base,
+ * level) belongs to the key, not to the parameter set: this query fails until the packing key is
+ * uploaded, and its answer then depends only on that decomposition and `count`. */
 int tfhe_mi355_packing_keyswitch_scratch(TfheMi355Context *ctx, size_t count, size_t *bytes);
 
 /* GLWE x plaintext-polynomial products over (Z/2^64)[X]/(X^N+1):

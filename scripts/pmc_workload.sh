@@ -1,6 +1,7 @@
 #!/bin/bash
 # rocprofv3 PMC passes (one counter group per run, each under its own time limit) of one bench
-# workload, summarised into profiles/r02_pmc_<tag>.json.   usage: pmc_workload.sh <tag>
+# workload, summarised per kernel into gpurun_out/r03_pmc_<tag>.json (copied to profiles/).
+#   usage: pmc_workload.sh <tag>
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 tag=$1
@@ -10,18 +11,20 @@ case $tag in
   2_2ks) K='pbs_classic_kernel|ks_digits|ks_mfma'; U='pbs_classic_kernel'; UPD=4096; M='pbs_classic_kernel'; ARGS="--params 2_2ks" ;;
   mb3)   K='pbs_multibit'; U='pbs_multibit'; UPD=4096; M='pbs_multibit'; ARGS="--params mb3" ;;
   mb2)   K='pbs_multibit'; U='pbs_multibit'; UPD=4096; M='pbs_multibit'; ARGS="--params mb2" ;;
-  4_4)   K='large_(init|top|sub|extract|group|digits)|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=128; M='large_group_cmux_kernel'; ARGS="--params 4_4 --batch 128" ;;
+  4_4)   K='large_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=128; M='large_group_cmux_kernel'; ARGS="--params 4_4 --batch 128" ;;
+  3_3)   K='large_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=1024; M='large_sub_kernel|large_group'; ARGS="--params 3_3 --batch 1024" ;;
   *) echo "unknown tag $tag"; exit 2 ;;
 esac
 B="$ARGS --steps 2 --warmup 1 --no-cpu-baseline --no-host-abi"
 run() {  # run NAME COUNTERS...
   local n=$1; shift
-  timeout -k 10 240 rocprofv3 --pmc "$@" -d gpurun_out/pmc_$tag/$n -o run --output-format csv -- python3 bench.py $B \
+  timeout -s KILL 240 rocprofv3 --pmc "$@" -d gpurun_out/pmc_$tag/$n -o run --output-format csv -- python3 bench.py $B \
     > gpurun_out/pmc_$tag/$n.log 2>&1
   local rc=$?; echo "pmc $tag $n rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/pmc_$tag/$n.log; exit $rc; }
 }
 run fetch FETCH_SIZE && run write WRITE_SIZE && \
 run sq SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE && \
+run lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS TCC_HIT_sum TCC_MISS_sum && \
 python3 scripts/pmc_workload.py --fetch gpurun_out/pmc_$tag/fetch --write gpurun_out/pmc_$tag/write \
-  --sq gpurun_out/pmc_$tag/sq --tag $tag --kernels "$K" --unit-kernel "$U" --units-per-dispatch $UPD \
-  --main-kernel "$M" --out gpurun_out/r02_pmc_$tag.json
+  --sq gpurun_out/pmc_$tag/sq --extra gpurun_out/pmc_$tag/lds --tag $tag --kernels "$K" --unit-kernel "$U" \
+  --units-per-dispatch $UPD --main-kernel "$M" --out gpurun_out/r03_pmc_$tag.json

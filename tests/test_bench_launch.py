@@ -62,8 +62,39 @@ def test_other_workloads_failed_child_is_reported_not_fatal(monkeypatch):
     spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
-    monkeypatch.setattr(bench, "OTHER_WORKLOADS", (("2_2ks", 1),))
+    monkeypatch.setattr(bench, "OTHER_WORKLOADS", (("2_2ks", "2_2ks", {"steps": 1}),))
     monkeypatch.setenv("CUDA_VISIBLE_DEVICES", "")  # the child must fail fast on this CPU box
     res = bench.other_workloads(argparse.Namespace(seed=1))
     assert set(res) == {"2_2ks"}
     assert "error" in res["2_2ks"] and res["2_2ks"]["wall_s"] > 0
+
+
+@pytest.mark.timeout(240)
+def test_multi_rank_default_run_merges_every_configuration():
+    """The driver's N > 1 default run: every rank runs each other configuration in-process on the
+    job's process group (keys broadcast, shards, barrier-bracketed timing, max wall over ranks)
+    before the headline, and rank 0 prints ONE line whose other_workloads entries carry the world
+    size they ran at (stub steps on gloo here; on the GPU box these are the PBS workloads)."""
+    p, lines = _run(["--gpus", "2", "--launch-selftest", "--steps", "2", "--warmup", "1", "--batch", "8"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    names = [w[0] for w in bench.OTHER_WORKLOADS]
+    assert {"mb3", "mul32", "4_4", "4_4_full"} <= set(names)
+    ow = d["other_workloads"]
+    assert list(ow) == names
+    for name, params, opts in bench.OTHER_WORKLOADS:
+        e = ow[name]
+        assert e["world_size"] == 2 and e["n_gpus"] == 2, (name, e)
+        assert e["steps"] == opts["steps"]
+        if opts.get("global_batch"):   # config 3 at its stated size: a fixed total split over the ranks
+            assert e["batch"] == opts["global_batch"] and e["scaling"] == "strong"
+        else:
+            assert e["batch"] == 16 and e["scaling"] == "weak"
+        assert e["check"]["decrypted_ok"] == e["check"]["of"] == e["batch"]
+    assert d["world_size"] == 2 and d["check"]["decrypted_ok"] == 16

@@ -63,3 +63,25 @@ def test_fheuint32_mul_dag_with_oracle_engine():
     assert sks.pbs_count % 2 == 0
     per_mul = sks.pbs_count // 2
     assert 256 < per_mul < 700, per_mul
+
+
+def test_device_table_cache_is_bounded_and_pins_captured_entries():
+    """the layer-table cache is an LRU of bounded size; entries used while a hipGraph
+    is captured are never evicted (the graph reads their device memory on every replay)."""
+    from tfhe_mi355.integer import _BoundedCache
+
+    capturing = [False]
+    c = _BoundedCache(3, lambda: capturing[0])
+    for k in range(5):
+        c.put(k, k * 10)
+    assert len(c) == 3 and c.get(0) is None and c.get(1) is None and c.get(4) == 40
+    c.get(2)                      # 2 becomes most recent: 3 is evicted next
+    c.put(5, 50)
+    assert c.get(3) is None and c.get(2) == 20
+    capturing[0] = True
+    assert c.get(4) == 40         # touched during capture: pinned
+    c.put(6, 60)                  # created during capture: pinned
+    capturing[0] = False
+    for k in range(100, 110):
+        c.put(k, k)
+    assert c.get(4) == 40 and c.get(6) == 60 and c.get(5) is None

@@ -121,6 +121,31 @@ def test_inconsistent_or_unsupported_keys_are_rejected():
         S.inspect_compressed_server_key(bytes(bad))
 
 
+def test_oversized_header_fields_fail_with_a_message():
+    """Header fields that would wrap the word-count products (glwe_size = N = 2^32, L = 1 makes
+    L (k+1) N = 0 mod 2^64 and the next `% per` a division by zero) are range-checked before any
+    arithmetic: the call returns an error, it does not crash the process."""
+    ksk, bsk = np.zeros(8, dtype=np.uint64), np.zeros(16, dtype=np.uint64)
+    good = _tiny_compressed_by_hand(ksk, 1, bsk, 2)
+    glwe_off = 8 + 64 + 8 * 3 + 16 + 24 + 4 + 8 + 16 * 8   # SeededGgswCiphertextList.glwe_size
+    assert struct.unpack_from("<QQ", good, glwe_off) == (2, 4)
+    for gs, n, lvl in [(2 ** 32, 2 ** 32, 1), (2, 2 ** 63, 1), (2, 4, 2 ** 63), (2 ** 63, 4, 1), (2, 6, 1)]:
+        bad = bytearray(good)
+        struct.pack_into("<QQ", bad, glwe_off, gs, n)
+        struct.pack_into("<Q", bad, glwe_off + 24, lvl)
+        with pytest.raises(Exception, match="out of range|power of two"):
+            S.inspect_compressed_server_key(bytes(bad))
+    # ServerKey: a FourierPolynomialList claiming N = 2^62 (M * 16 would wrap the bounds check)
+    p = PARAM_MESSAGE_2_CARRY_2_KS_PBS.with_(lwe_dimension=3)
+    ksk = np.zeros(p.big_lwe_dimension * p.ks_level * (p.lwe_dimension + 1), dtype=np.uint64)
+    fb = np.zeros((3 * 4, p.polynomial_size // 2), dtype=np.complex128)
+    data = bytearray(S.serialize_server_key(p, ksk, fb))
+    off = 8 + ksk.size * 8 + 8 * 3 + 24 + 4
+    struct.pack_into("<Q", data, off + 8, 2 ** 62)
+    with pytest.raises(Exception, match="polynomial size"):
+        S.inspect_server_key(bytes(data))
+
+
 def test_server_key_round_trip_and_layout():
     p = PARAM_MESSAGE_2_CARRY_2_KS_PBS.with_(lwe_dimension=3)
     M = p.polynomial_size // 2

@@ -137,6 +137,8 @@ struct TfheMi355Context {
     DeviceBuffer pksk, pksk_planes;
     uint32_t pks_base_log = 0, pks_level = 0;
     bool pksk_ready = false, pksk_planes_ready = false;
+    KernelTimer timer;  // per-kernel durations (tfhe_mi355_kernel_timing_*), off by default
+    KernelTimer *timer_or_null() { return timer.every > 0 ? &timer : nullptr; }
 
     size_t n() const { return p.lwe_dimension; }
     size_t k() const { return p.glwe_dimension; }
@@ -245,8 +247,16 @@ size_t ks_scratch_bytes(const TfheMi355Context *c, size_t count) {
     return count ? ks_mfma_scratch_bytes((int)c->big_dim(), (int)c->p.ks_level, (int)count) : 0;
 }
 
+// The packing key's decomposition (base, level) is part of the key, not of the parameter set, so
+// this size is defined from the key's upload on (the scratch query fails before it); it follows
+// from the decomposition and the MFMA eligibility alone, not from the repack having run.
+bool pks_use_mfma(const TfheMi355Context *c) {
+    static const bool disabled = env_flag("TFHE_MI355_KS_NO_MFMA");
+    return !disabled && c->pks_level &&
+           ks_mfma_supported((int)c->big_dim(), (int)c->pks_level, (int)c->pks_base_log);
+}
 size_t pks_scratch_bytes(const TfheMi355Context *c, size_t count) {
-    if (!c->pksk_planes_ready || count == 0) return 0;
+    if (!pks_use_mfma(c) || count == 0) return 0;
     return ks_mfma_scratch_bytes((int)c->big_dim(), (int)c->pks_level, (int)count);
 }
 
@@ -288,6 +298,7 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
         a.base_log = (int)c->p.pbs_base_log;
         a.count = (int)count;
         a.glwe_out = glwe_out;
+        TimedLaunch tl(c->timer_or_null(), "pbs_multibit", s);
         check(launch_multibit_pbs((int)c->N(), (int)c->k(), (int)c->p.pbs_level, (int)c->p.grouping_factor, a, s),
               "launch multi-bit pbs");
         return;
@@ -313,6 +324,7 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
         a.count = (int)count;
         a.scratch = scratch;
         a.scratch_bytes = std::min(scratch_bytes, per_ct * large_chunk());
+        a.timer = c->timer_or_null();
         check(launch_large_pbs((int)c->N(), (int)c->k(), (int)c->p.pbs_level, a, s), "launch large pbs");
         return;
     }
@@ -334,6 +346,7 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
         a.ticket = reinterpret_cast<uint32_t *>(scratch);
         check(hipMemsetAsync(a.ticket, 0, sizeof(uint32_t), s), "zero pbs ticket");
     }
+    TimedLaunch tl(c->timer_or_null(), "pbs_classic_kernel", s);
     check(launch_classic_pbs((int)c->N(), (int)c->k(), (int)c->p.pbs_level, a, s), "launch pbs");
 }
 
@@ -363,6 +376,7 @@ void launch_ks_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, s
     a.base_log = (int)c->p.ks_base_log;
     a.level = (int)c->p.ks_level;
     a.count = (int)count;
+    TimedLaunch tl(c->timer_or_null(), "keyswitch", s);
     if (c->ksk_planes_ready) {
         require_scratch(scratch ? scratch_bytes : 0, ks_scratch_bytes(c, count));
         check(launch_keyswitch_mfma(a, (const int8_t *)c->ksk_planes.ptr, scratch, s), "launch mfma keyswitch");
@@ -615,6 +629,36 @@ int tfhe_mi355_device_count(int *out_count) {
         int n = 0;
         check(hipGetDeviceCount(&n), "hipGetDeviceCount");
         *out_count = n;
+    });
+}
+
+int tfhe_mi355_kernel_timing_enable(TfheMi355Context *ctx, int every) {
+    return guarded([&] {
+        if (!ctx) fail("null argument");
+        if (every < 0) fail("sampling interval must be >= 0");
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        ctx->timer.reset();
+        ctx->timer.every = every;
+    });
+}
+
+int tfhe_mi355_kernel_timing_entry(TfheMi355Context *ctx, size_t index, char *name, size_t name_len,
+                                   double *total_ms, uint64_t *launches) {
+    return guarded([&] {
+        if (!ctx || !name || !name_len || !total_ms || !launches) fail("null argument");
+        name[0] = 0;
+        *total_ms = 0;
+        *launches = 0;
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        ctx->timer.collect();
+        std::lock_guard<std::mutex> g(ctx->timer.mu);
+        if (index >= ctx->timer.totals.size()) fail("kernel timing index %zu out of range (%zu entries)", index,
+                                                    ctx->timer.totals.size());
+        auto it = ctx->timer.totals.begin();
+        std::advance(it, index);
+        std::snprintf(name, name_len, "%s", it->first.c_str());
+        *total_ms = it->second.first;
+        *launches = it->second.second;
     });
 }
 
@@ -978,7 +1022,7 @@ int tfhe_mi355_packing_keyswitch_key_upload(TfheMi355Context *ctx, const uint64_
         ctx->pks_base_log = base_log;
         ctx->pks_level = level;
         const int in_dim = (int)ctx->big_dim(), out_dim = (int)ctx->glwe_len() - 1;
-        if (!env_flag("TFHE_MI355_KS_NO_MFMA") && ks_mfma_supported(in_dim, (int)level, (int)base_log)) {
+        if (pks_use_mfma(ctx)) {
             ctx->pksk_planes.reserve(8 * ks_mfma_rows(in_dim, (int)level) * ks_mfma_cols(out_dim));
             check(launch_ksk_repack((const uint64_t *)ctx->pksk.ptr, (int8_t *)ctx->pksk_planes.ptr, in_dim,
                                     (int)level, out_dim, ctx->stream),
@@ -1005,6 +1049,7 @@ int tfhe_mi355_packing_keyswitch_scratch(TfheMi355Context *ctx, size_t count, si
     return guarded([&] {
         if (!ctx || !bytes) fail("null argument");
         std::lock_guard<std::mutex> g(ctx->mu);
+        if (!ctx->pksk_ready) fail("packing keyswitching key not uploaded: its decomposition sizes the scratch");
         *bytes = pks_scratch_bytes(ctx, count);
     });
 }

@@ -4,7 +4,102 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
 namespace tfhe_mi355 {
+
+// Per-kernel durations measured on the launch stream (a profiling aid, off unless enabled through
+// tfhe_mi355_kernel_timing_enable): the launchers bracket every `every`-th launch of a kernel
+// family with HIP events; collect() waits for them and accumulates per-name totals.  bench.py
+// reads the dominant kernel's average from here for its roofline.  Nothing is recorded while the
+// stream is being captured into a graph.
+struct KernelTimer {
+    int every = 0;  // 0: off
+    std::mutex mu;
+    struct Rec {
+        std::string name;
+        hipEvent_t a, b;
+    };
+    std::vector<Rec> pending;
+    std::vector<hipEvent_t> pool;
+    std::map<std::string, std::pair<double, uint64_t>> totals;  // name -> (ms, launches)
+    std::map<std::string, uint64_t> calls;                      // launches seen per name (sampling)
+
+    // true when this launch of `name` is to be timed
+    bool want(const char *name, hipStream_t s) {
+        if (every <= 0) return false;
+        hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return false;
+        std::lock_guard<std::mutex> g(mu);
+        return calls[name]++ % (uint64_t)every == 0;
+    }
+    hipEvent_t record(hipStream_t s) {
+        hipEvent_t e = nullptr;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (!pool.empty()) {
+                e = pool.back();
+                pool.pop_back();
+            }
+        }
+        if (!e && hipEventCreate(&e) != hipSuccess) return nullptr;
+        (void)hipEventRecord(e, s);
+        return e;
+    }
+    void done(const char *name, hipEvent_t a, hipStream_t s) {
+        hipEvent_t b = record(s);
+        if (!a || !b) return;
+        std::lock_guard<std::mutex> g(mu);
+        pending.push_back({name, a, b});
+    }
+    void collect() {
+        std::vector<Rec> recs;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            recs.swap(pending);
+        }
+        for (auto &r : recs) {
+            float ms = 0.f;
+            if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+                std::lock_guard<std::mutex> g(mu);
+                auto &t = totals[r.name];
+                t.first += ms;
+                t.second += 1;
+            }
+            std::lock_guard<std::mutex> g(mu);
+            pool.push_back(r.a);
+            pool.push_back(r.b);
+        }
+    }
+    void reset() {
+        collect();
+        std::lock_guard<std::mutex> g(mu);
+        totals.clear();
+        calls.clear();
+    }
+    ~KernelTimer() {
+        collect();
+        for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+    }
+};
+
+// RAII bracket of one kernel launch (no-op without a timer or when this launch is not sampled)
+struct TimedLaunch {
+    KernelTimer *t;
+    const char *name;
+    hipStream_t s;
+    hipEvent_t a = nullptr;
+    TimedLaunch(KernelTimer *t_, const char *name_, hipStream_t s_) : t(t_), name(name_), s(s_) {
+        if (t && t->want(name, s)) a = t->record(s);
+        else t = nullptr;
+    }
+    ~TimedLaunch() {
+        if (t) t->done(name, a, s);
+    }
+};
 
 struct FftTables {
     // device tables, M entries each (M = N/2)
@@ -70,6 +165,7 @@ struct LargePbsLaunch {
     double2 *spectra;            // set by the launcher
     int levels;                  // set by the launcher (= pbs_level)
     int chunk_count;             // set by the launcher: ciphertexts in the current chunk
+    KernelTimer *timer = nullptr;  // optional per-kernel timing
 };
 bool large_pbs_supported(int N, int k, int L);
 size_t large_pbs_scratch_per_ct(int N, int k, int L);

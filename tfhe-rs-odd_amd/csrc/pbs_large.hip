@@ -823,9 +823,16 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
                 const unsigned grp_blocks = (unsigned)((cnt + 7) / 8) * 8 * 4 * GroupCfg::PARTS;
                 const unsigned dig_blocks = (unsigned)((cnt + 7) / 8) * 8 * (LM / LARGE_DIGT);
                 for (int i = 0; i < a.n; i++) {
-                    hipLaunchKernelGGL(large_digits_kernel, dim3(dig_blocks), dim3(LARGE_DIGT), 0, s, a, ct0, i);
-                    hipLaunchKernelGGL(large_group_cmux_kernel, dim3(grp_blocks), dim3(GroupCfg::THREADS), GroupCfg::LDS,
-                                       s, a, ct0, i);
+                    {
+                        TimedLaunch tl(a.timer, "large_digits_kernel", s);
+                        hipLaunchKernelGGL(large_digits_kernel, dim3(dig_blocks), dim3(LARGE_DIGT), 0, s, a, ct0, i);
+                    }
+                    {
+                        TimedLaunch tl(a.timer, "large_group_cmux_kernel", s);
+                        hipLaunchKernelGGL(large_group_cmux_kernel, dim3(grp_blocks), dim3(GroupCfg::THREADS),
+                                           GroupCfg::LDS, s, a, ct0, i);
+                    }
+                    TimedLaunch tl(a.timer, "large_top_inv_kernel", s);
                     hipLaunchKernelGGL((large_top_inv_kernel<K>), dim3(top_blocks), dim3(TOPT), 0, s, a, ct0, i);
                 }
                 const size_t out_elems = (size_t)cnt * (K * LN + 1);

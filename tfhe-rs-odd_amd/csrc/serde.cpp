@@ -155,6 +155,20 @@ SeededGgswList seeded_ggsw_list(Reader &r) {
     return g;
 }
 
+// Upper bounds on the header fields, checked before they enter any product (a crafted key with
+// e.g. glwe_size = N = 2^32 would otherwise wrap a word count to 0 and divide by it).  Generous
+// against every reference parameter set (N <= 2^15, k + 1 <= 6, levels <= 7, n <= 2^11).
+constexpr uint64_t kMaxPolySize = 1ull << 17;
+constexpr uint64_t kMaxGlweSize = 64;
+constexpr uint64_t kMaxLevels = 64;
+constexpr uint64_t kMaxLweSize = 1ull << 20;
+
+void check_range(uint64_t v, uint64_t lo, uint64_t hi, const char *what) {
+    if (v < lo || v > hi)
+        fail("%s = %llu out of range [%llu, %llu]", what, (unsigned long long)v, (unsigned long long)lo,
+             (unsigned long long)hi);
+}
+
 struct FourierList {
     uint64_t N = 0, polys = 0;
     size_t first = 0;  // byte offset of the first polynomial's length word
@@ -166,7 +180,9 @@ FourierList fourier_list(Reader &r) {
     f.polys = r.u64("Fourier polynomial count");
     if (seq != 2 + f.polys) fail("Fourier polynomial list: sequence of %llu elements for %llu polynomials",
                                  (unsigned long long)seq, (unsigned long long)f.polys);
-    if (f.N < 2 || (f.N & (f.N - 1))) fail("Fourier polynomial list: polynomial size %llu", (unsigned long long)f.N);
+    // bounded before any size arithmetic (M * 16 below must not wrap)
+    if (f.N < 2 || f.N > kMaxPolySize || (f.N & (f.N - 1)))
+        fail("Fourier polynomial list: polynomial size %llu", (unsigned long long)f.N);
     f.first = r.off;
     const uint64_t M = f.N / 2;
     for (uint64_t q = 0; q < f.polys; q++) {
@@ -216,8 +232,14 @@ void finish(Key &k, Reader &r) {
     const uint64_t glwe_size = k.compressed ? k.sbsk.glwe_size : k.glwe_size;
     const uint64_t N = k.compressed ? k.sbsk.N : k.fbsk.N;
     const uint64_t L = k.compressed ? k.sbsk.level : k.pbs_level;
-    if (glwe_size < 2 || N == 0 || L == 0) fail("bootstrapping key with glwe_size %llu, N %llu, level %llu",
-                                                (unsigned long long)glwe_size, (unsigned long long)N, (unsigned long long)L);
+    // every field that enters a product below is range-checked first (no wrap-around)
+    check_range(glwe_size, 2, kMaxGlweSize, "bootstrapping key glwe_size");
+    check_range(N, 2, kMaxPolySize, "bootstrapping key polynomial_size");
+    if (N & (N - 1)) fail("bootstrapping key polynomial_size %llu is not a power of two", (unsigned long long)N);
+    check_range(L, 1, kMaxLevels, "bootstrapping key decomp_level_count");
+    check_range(k.ks_level, 1, kMaxLevels, "keyswitching key decomp_level_count");
+    check_range(k.ks_out_size, 2, kMaxLweSize, "keyswitching key output_lwe_size");
+    if (!k.compressed) check_range(k.n, 1, kMaxLweSize, "input_lwe_dimension");
     const uint64_t k1 = glwe_size;
     uint64_t ggsw = 0;
     if (k.compressed) {
@@ -239,7 +261,7 @@ void finish(Key &k, Reader &r) {
     if (!k.compressed && k.n != n) fail("Fourier bootstrapping key: input_lwe_dimension %llu but %llu GGSWs",
                                         (unsigned long long)k.n, (unsigned long long)ggsw);
     const uint64_t big = (k1 - 1) * N;
-    if (k.ks_level == 0 || k.ks_out_size != n + 1)
+    if (k.ks_out_size != n + 1)
         fail("keyswitching key output size %llu does not match the bootstrapping key's n = %llu",
              (unsigned long long)k.ks_out_size, (unsigned long long)n);
     const uint64_t per_in = k.compressed ? k.ks_level : k.ks_level * k.ks_out_size;

@@ -128,6 +128,9 @@ SIGNATURES = [
     ("tfhe_mi355_server_key_inspect", ctypes.c_int, [u8p, sz, ctypes.POINTER(TfheMi355ServerKeyInfo)]),
     ("tfhe_mi355_server_key_upload", ctypes.c_int, [vp, u8p, sz]),
     ("tfhe_mi355_fourier_engine_frequency", ctypes.c_int, [ctypes.c_uint32, u32p]),
+    ("tfhe_mi355_kernel_timing_enable", ctypes.c_int, [vp, ctypes.c_int]),
+    ("tfhe_mi355_kernel_timing_entry", ctypes.c_int,
+     [vp, sz, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]),
 ]
 
 _lib = None

@@ -143,6 +143,24 @@ class Engine:
     def keyswitch_key_set_ready(self):
         _lib.call("tfhe_mi355_keyswitch_key_set_ready", self._h)
 
+    # -- profiling -----------------------------------------------------------------------
+    def kernel_timing(self, every: int) -> None:
+        """Time every `every`-th launch of each kernel family with HIP events on its stream
+        (0 = off); clears the totals."""
+        _lib.call("tfhe_mi355_kernel_timing_enable", self._h, int(every))
+
+    def kernel_times(self) -> dict:
+        """{kernel family: (average ms per timed launch, timed launches)}; waits for the events."""
+        out = {}
+        name = ctypes.create_string_buffer(128)
+        tot, cnt = ctypes.c_double(), ctypes.c_uint64()
+        lib = _lib.load()
+        i = 0
+        while lib.tfhe_mi355_kernel_timing_entry(self._h, i, name, 128, ctypes.byref(tot), ctypes.byref(cnt)) == 0:
+            out[name.value.decode()] = (tot.value / max(cnt.value, 1), cnt.value)
+            i += 1
+        return out
+
     # -- host (numpy) batched ops ---------------------------------------------------------
     def _luts(self, luts):
         luts = _u64(luts)
@@ -305,7 +323,12 @@ class Engine:
         import torch
 
         t = torch.empty(need, dtype=torch.uint8, device=torch.device("cuda", self.device))
-        if stream is not None and not isinstance(stream, int) and stream != torch.cuda.current_stream():
+        # The tensor is freed when the wrapper returns, while the kernel may still run: tell the
+        # caching allocator which stream uses the block so it is not handed out before that
+        # stream reaches this point (raw int handles are wrapped as an ExternalStream).
+        if isinstance(stream, int):
+            stream = torch.cuda.ExternalStream(stream, device=t.device)
+        if stream is not None and stream != torch.cuda.current_stream(t.device):
             t.record_stream(stream)
         return t.data_ptr(), need, t
 

@@ -166,9 +166,47 @@ class _HostOps:
         return x.shape[0]
 
 
+class _BoundedCache:
+    """LRU map of device tables (LUT stacks, index arrays) with at most `cap` entries.  Entries
+    touched while a hipGraph is being captured are pinned and never evicted: a captured graph
+    keeps reading their device memory on every replay, so freeing them would let the caching
+    allocator hand that memory to someone else under the graph."""
+
+    def __init__(self, cap: int, capturing):
+        from collections import OrderedDict
+
+        self.cap, self._capturing = cap, capturing
+        self._d = OrderedDict()
+        self._pinned = {}
+
+    def get(self, key):
+        if key in self._pinned:
+            return self._pinned[key]
+        v = self._d.get(key)
+        if v is not None:
+            self._d.move_to_end(key)
+            if self._capturing():
+                self._pinned[key] = self._d.pop(key)
+        return v
+
+    def put(self, key, value):
+        if self._capturing():
+            self._pinned[key] = value
+            return
+        self._d[key] = value
+        self._d.move_to_end(key)
+        while len(self._d) > self.cap:
+            self._d.popitem(last=False)
+
+    def __len__(self):
+        return len(self._d) + len(self._pinned)
+
+
 class _DeviceOps:
     """torch int64 tensors resident on the engine's GPU between layers; the LWE arithmetic runs in
     the engine's own kernels (lwe_ops.hip), torch only allocates, slices and copies."""
+
+    CACHE_ENTRIES = 256  # distinct layer tables kept on the device (a FheUint32 multiply uses 11)
 
     def __init__(self, sk: "ServerKey"):
         import torch
@@ -177,8 +215,10 @@ class _DeviceOps:
         self.sk = sk
         self.eng = sk.shortint.engine
         self.device = torch.device("cuda", self.eng.device)
-        self._lut_dev = {}
-        self._stacks = {}   # LUT stacks and per-row LUT index arrays of the layers seen so far
+        capturing = torch.cuda.is_current_stream_capturing
+        self._lut_dev = _BoundedCache(self.CACHE_ENTRIES, capturing)
+        # LUT stacks and per-row LUT index arrays of the layers seen so far (bounded LRU)
+        self._stacks = _BoundedCache(self.CACHE_ENTRIES, capturing)
         self._scratch = None
 
     def zeros(self, k, b, s):
@@ -213,7 +253,7 @@ class _DeviceOps:
         t = self._lut_dev.get(id(lut))
         if t is None or t[0] is not lut:
             t = (lut, self.from_host(lut.acc))
-            self._lut_dev[id(lut)] = t
+            self._lut_dev.put(id(lut), t)
         return t[1]
 
     def trivial_pbs(self, rb, j, lut):
@@ -235,7 +275,7 @@ class _DeviceOps:
                 li = np.repeat(np.asarray([li for _, _, li in todo], dtype=np.int32), K)
                 idx = self.torch.from_numpy(li).to(self.device)
             hit = (list(luts), d_luts, idx)
-            self._stacks[key] = hit
+            self._stacks.put(key, hit)
         return hit[1], hit[2]
 
     def pbs_rows(self, todo, luts):
