@@ -754,6 +754,51 @@ def host_abi_rate(eng, P, cts, acc, with_ks: bool, reps: int = 3) -> dict:
                      "directly, same outputs); PCIe-inclusive, rank 0's GPU, not the headline value")}
 
 
+def single_ct_rates(eng, cts, acc, with_ks: bool, batched_rate: float, secs: float = 2.0) -> dict:
+    """The reference's own calling pattern through the synchronous host-pointer ABI: ONE ciphertext
+    per call (keyswitch_programmable_bootstrap_assign, shortint/server_key/mod.rs:783-857), from T
+    concurrent caller threads (rayon workers, radix_parallel/mul.rs:347-407).  The engine coalesces
+    concurrent small calls into batches (capi.cpp "request coalescing").  Reports the single-call
+    latency with one caller and the ciphertexts per second reached by 16 and 64 closed-loop callers
+    (each issues its next call when the previous returns), against the batched device rate."""
+    import threading
+
+    f = eng.keyswitch_programmable_bootstrap if with_ks else eng.programmable_bootstrap
+    f(cts[:1], acc)
+    lat = []
+    for i in range(10):
+        t = time.perf_counter()
+        f(cts[i:i + 1], acc)
+        lat.append(time.perf_counter() - t)
+    res = {"entry_point": ("tfhe_mi355_keyswitch_programmable_bootstrap" if with_ks
+                           else "tfhe_mi355_programmable_bootstrap"),
+           "single_call_latency_ms": 1e3 * float(np.median(lat)), "callers": {}}
+    for T in (16, 64):
+        done = [0] * T
+        stop = time.perf_counter() + secs
+
+        def worker(t):
+            i = t
+            while time.perf_counter() < stop:
+                f(cts[i % cts.shape[0]:i % cts.shape[0] + 1], acc)
+                done[t] += 1
+                i += T
+
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        wall = time.perf_counter() - t0
+        rate = sum(done) / wall
+        res["callers"][str(T)] = {"value": rate, "frac_of_batched_device_rate": rate / batched_rate,
+                                  "little_bound": T / (res["single_call_latency_ms"] * 1e-3)}
+    res["note"] = ("closed-loop callers, count = 1 per call; by Little's law T callers cannot exceed T / latency "
+                   "(little_bound); the batched device rate is the headline step's")
+    return res
+
+
 def run_pbs(args, P, pname, workload, kname, R):
     import torch
 
@@ -812,6 +857,7 @@ def run_pbs(args, P, pname, workload, kname, R):
     host_abi = None
     if not args.no_host_abi and R.rank == 0 and P.polynomial_size <= 2048:
         host_abi = host_abi_rate(eng, P, cts, acc, with_ks)
+        host_abi["single_ct"] = single_ct_rates(eng, cts, acc, with_ks, nb * args.steps / wall)
 
     if R.rank == 0:
         unit = "KS+PBS/s" if with_ks else "PBS/s"

@@ -1,0 +1,116 @@
+"""The drop-in under the reference's own calling pattern: one ciphertext per call, from many
+threads at once (shortint keyswitch_programmable_bootstrap_assign, shortint/server_key/mod.rs:
+783-857, called from rayon workers per block, integer/server_key/radix_parallel/mul.rs:347-407).
+
+Small host-pointer calls on one context are coalesced into batches (capi.cpp "request
+coalescing"): every caller must still get exactly its own rows -- bit-exact against the oracle's
+keyswitch + PBS of the same ciphertext with the same LUT -- whatever the batch it landed in, with
+different LUTs per caller (deduplicated by buffer), per-row LUT indexes and different ops
+interleaved.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import decode
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng(keys_2_2):
+    from tfhe_mi355 import Engine
+
+    e = Engine(keys_2_2.params, 0)
+    e.upload_bootstrap_key(keys_2_2.bsk)
+    e.upload_keyswitch_key(keys_2_2.ksk)
+    return e
+
+
+def _run_threads(n, fn):
+    errors = []
+
+    def wrap(i):
+        try:
+            fn(i)
+        except Exception as ex:  # pragma: no cover - reported below
+            errors.append(repr(ex))
+
+    ts = [threading.Thread(target=wrap, args=(i,)) for i in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in ts), "a caller never returned"
+    assert not errors, errors[:3]
+
+
+def test_16_threads_x_64_single_ciphertext_ks_pbs_bit_exact(orc, keys_2_2, eng):
+    p = keys_2_2.params
+    T, C = 16, 64
+    fs = [lambda x, a=a: (a * x + 1) % 16 for a in (1, 3, 5, 7)]
+    accs = [orc.fill_accumulator(2048, 1, 4, 4, f) for f in fs]   # 4 LUT buffers shared by 16 threads
+    msgs = (np.arange(T * C) * 7) % 16
+    cts = orc.lwe_encrypt(901, keys_2_2.glwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta),
+                          p.glwe_modular_std_dev)
+    out = np.zeros((T * C, p.big_lwe_dimension + 1), dtype=np.uint64)
+
+    def worker(t):
+        for c in range(C):
+            i = t * C + c
+            out[i:i + 1] = eng.keyswitch_programmable_bootstrap(cts[i:i + 1], accs[t % 4])
+
+    _run_threads(T, worker)
+    small = orc.keyswitch(keys_2_2.ksk, p.big_lwe_dimension, p.lwe_dimension, p.ks_base_log, p.ks_level, cts)
+    for a in range(4):
+        rows = np.nonzero((np.arange(T * C) // C) % 4 == a)[0]
+        exp = keys_2_2.fbsk.pbs(small[rows], accs[a], threads=16)
+        bad = np.nonzero(np.any(out[rows] != exp, axis=1))[0]
+        assert bad.size == 0, f"LUT {a}: {bad.size} of {rows.size} single-ciphertext calls differ from the oracle"
+        dec = decode(orc.lwe_decrypt(keys_2_2.glwe_sk, out[rows]), p.delta) % 16
+        assert np.array_equal(dec, [fs[a](m) for m in msgs[rows]])
+
+
+def test_mixed_ops_counts_and_lut_indexes_coalesce_exactly(orc, keys_2_2, eng):
+    """Concurrent PBS, KS+PBS and KS calls of 1-5 ciphertexts, some with two LUTs and per-row
+    indexes: each result equals the oracle's result of the same call made alone."""
+    p = keys_2_2.params
+    accs = np.stack([orc.fill_accumulator(2048, 1, 4, 4, lambda x: x),
+                     orc.fill_accumulator(2048, 1, 4, 4, lambda x: 15 - x)])
+    rng = np.random.default_rng(5)
+    jobs = []
+    for j in range(96):
+        cnt = int(rng.integers(1, 6))
+        msgs = rng.integers(0, 16, cnt).astype(np.uint64)
+        big = orc.lwe_encrypt(1000 + j, keys_2_2.glwe_sk, msgs * np.uint64(p.delta), p.glwe_modular_std_dev)
+        op = ("pbs", "ks_pbs", "ks")[j % 3]
+        idx = rng.integers(0, 2, cnt).astype(np.uint32) if j % 2 else None
+        jobs.append((op, big, idx))
+    small_all = [orc.keyswitch(keys_2_2.ksk, p.big_lwe_dimension, p.lwe_dimension, p.ks_base_log, p.ks_level, b)
+                 for _, b, _ in jobs]
+
+    def call(op, big, small, idx):
+        luts = accs if idx is not None else accs[0]
+        if op == "pbs":
+            return eng.programmable_bootstrap(small, luts, idx)
+        if op == "ks_pbs":
+            return eng.keyswitch_programmable_bootstrap(big, luts, idx)
+        return eng.keyswitch(big)
+
+    got = [None] * len(jobs)
+
+    def worker(t):
+        for j in range(t, len(jobs), 12):
+            op, big, idx = jobs[j]
+            got[j] = call(op, big, small_all[j], idx)
+
+    _run_threads(12, worker)
+    # the oracle's result of each call on its own
+    for j, (op, big, idx) in enumerate(jobs):
+        if op == "ks":
+            exp = small_all[j]
+        else:
+            luts = accs if idx is not None else accs[0]
+            exp = keys_2_2.fbsk.pbs(small_all[j], luts, lut_idx=idx, threads=8)
+        assert np.array_equal(got[j], exp), f"job {j} ({op}, {big.shape[0]} cts, idx={idx is not None}) differs"

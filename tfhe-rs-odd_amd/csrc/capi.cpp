@@ -4,7 +4,9 @@
 // key.  Error convention: 0/1 return + thread-local message (tfhe/src/c_api/utils.rs:3-73).
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
@@ -108,6 +110,19 @@ size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 bool is_pow2(uint32_t x) { return x && !(x & (x - 1)); }
 }  // namespace
 
+// one small host-pointer call waiting to be coalesced into a batch (see "request coalescing")
+enum CoalescedOp { CO_PBS = 0, CO_KS_PBS, CO_PBS_KS, CO_KS, CO_OPS };
+struct CoalescedReq {
+    const uint64_t *in;
+    uint64_t *out;
+    const uint64_t *luts;
+    size_t lut_count;
+    const uint32_t *idx;
+    size_t count;
+    bool done = false;
+    std::string err;
+};
+
 struct TfheMi355Context {
     TfheMi355Parameters p{};
     int device = 0;
@@ -138,6 +153,25 @@ struct TfheMi355Context {
     uint32_t pks_base_log = 0, pks_level = 0;
     bool pksk_ready = false, pksk_planes_ready = false;
     KernelTimer timer;  // per-kernel durations (tfhe_mi355_kernel_timing_*), off by default
+    // Request coalescing of small host-pointer calls (the reference calls the PBS one ciphertext
+    // at a time from rayon workers: shortint/server_key/mod.rs:783-857, radix_parallel/mul.rs:
+    // 347-407).  Concurrent calls of one op are queued; one caller collects the queue into a
+    // batch (after a short window or when the batch is full) and runs it on one of the batch
+    // slots, each with its own stream, staging and scratch, so several batches can be in flight;
+    // every caller gets its rows back bit-identical to a call of its own.
+    struct Coalescer {
+        std::mutex m;
+        std::condition_variable cv;
+        std::vector<CoalescedReq *> queue[CO_OPS];
+        size_t queued[CO_OPS] = {};
+        bool collecting[CO_OPS] = {};
+        struct Slot {
+            hipStream_t stream = nullptr;
+            PinnedBuffer h_in, h_out, h_luts, h_idx;
+            DeviceBuffer d_in, d_out, d_luts, d_idx, d_scratch;
+            bool busy = false;
+        } slots[4];
+    } co;
     KernelTimer *timer_or_null() { return timer.every > 0 ? &timer : nullptr; }
 
     size_t n() const { return p.lwe_dimension; }
@@ -616,6 +650,177 @@ void chunk_pks(TfheMi355Context *c, const uint64_t *i, uint64_t *o, const uint64
                size_t n, void *sc, size_t sb, hipStream_t s) {
     launch_packing_ks_dev(c, i, o, n, sc, sb, s);
 }
+
+// ---- request coalescing ---------------------------------------------------------------------------
+// Calls of at most coalesce_max_count() ciphertexts (default 64; TFHE_MI355_COALESCE_MAX_COUNT,
+// 0 = off) are coalesced: up to coalesce_batch() ciphertexts (default 1024, one ciphertext per PBS
+// slot of the chip at 2_2) gathered for at most coalesce_window() (default 200 us) from the first
+// queued call.  The window is small next to a PBS (milliseconds), and a full batch leaves at once.
+size_t env_size(const char *name, size_t dflt) {
+    const char *e = std::getenv(name);
+    if (!e || !*e) return dflt;
+    const long x = std::atol(e);
+    return x >= 0 ? (size_t)x : dflt;
+}
+size_t coalesce_max_count() {
+    static const size_t v = env_size("TFHE_MI355_COALESCE_MAX_COUNT", 64);
+    return v;
+}
+size_t coalesce_batch() {
+    static const size_t v = std::max<size_t>(env_size("TFHE_MI355_COALESCE_BATCH", 1024), 1);
+    return v;
+}
+std::chrono::microseconds coalesce_window() {
+    static const size_t v = env_size("TFHE_MI355_COALESCE_WINDOW_US", 200);
+    return std::chrono::microseconds(v);
+}
+
+struct CoalescedOpDesc {
+    size_t in_words, out_words;
+    bool lut;
+    ChunkLaunch launch;
+    ScratchSize scratch;
+};
+CoalescedOpDesc coalesced_op(const TfheMi355Context *c, CoalescedOp op) {
+    const size_t small = c->n() + 1, big = c->big_dim() + 1;
+    switch (op) {
+        case CO_PBS: return {small, big, true, chunk_pbs, pbs_scratch_bytes};
+        case CO_KS_PBS: return {big, big, true, launch_ks_pbs_dev, ks_pbs_scratch_bytes};
+        case CO_PBS_KS: return {small, small, true, launch_pbs_ks_dev, pbs_ks_scratch_bytes};
+        default: return {big, small, false, chunk_ks, ks_scratch_bytes};
+    }
+}
+
+// one batch on one slot: concatenated inputs, LUT sets deduplicated by pointer with per-row LUT
+// indexes shifted to the set's offset, one launch of the _async path on the slot's stream
+void run_coalesced_batch(TfheMi355Context *c, TfheMi355Context::Coalescer::Slot &sl, CoalescedOp op,
+                         const std::vector<CoalescedReq *> &batch) {
+    check(hipSetDevice(c->device), "hipSetDevice");
+    const CoalescedOpDesc d = coalesced_op(c, op);
+    const size_t cap = coalesce_batch(), glwe = c->glwe_len();
+    if (!sl.stream) check(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking), "hipStreamCreate(slot)");
+    size_t total = 0;
+    for (auto *r : batch) total += r->count;
+    // sized for a full batch once (no hipFree between batches: it would wait for the device)
+    sl.h_in.reserve(cap * d.in_words * 8);
+    sl.h_out.reserve(cap * d.out_words * 8);
+    sl.d_in.reserve(cap * d.in_words * 8);
+    sl.d_out.reserve(cap * d.out_words * 8);
+    const size_t scratch = d.scratch(c, cap);
+    if (scratch) sl.d_scratch.reserve(scratch);
+    size_t rows = 0, sets = 0;
+    std::vector<std::pair<const uint64_t *, size_t>> seen;  // LUT pointer -> first set index
+    std::vector<size_t> seen_count;                           // its lut_count
+    uint32_t *hidx = nullptr;
+    if (d.lut) {
+        sl.h_idx.reserve(cap * 4);
+        sl.d_idx.reserve(cap * 4);
+        hidx = static_cast<uint32_t *>(sl.h_idx.ptr);
+    }
+    std::vector<size_t> base(batch.size(), 0);
+    if (d.lut) {  // distinct LUT sets (by pointer) and their offsets, then one staging buffer for all
+        for (size_t b = 0; b < batch.size(); b++) {
+            const CoalescedReq *r = batch[b];
+            base[b] = (size_t)-1;
+            for (size_t q = 0; q < seen.size(); q++)  // same buffer, same number of tables
+                if (seen[q].first == r->luts && seen_count[q] == r->lut_count) base[b] = seen[q].second;
+            if (base[b] == (size_t)-1) {
+                base[b] = sets;
+                seen.push_back({r->luts, sets});
+                seen_count.push_back(r->lut_count);
+                sets += r->lut_count;
+            }
+        }
+        sl.h_luts.reserve(sets * glwe * 8);
+        for (size_t q = 0; q < seen.size(); q++)
+            std::memcpy(static_cast<uint64_t *>(sl.h_luts.ptr) + seen[q].second * glwe, seen[q].first,
+                        seen_count[q] * glwe * 8);
+    }
+    for (size_t b = 0; b < batch.size(); b++) {
+        const CoalescedReq *r = batch[b];
+        std::memcpy(static_cast<uint64_t *>(sl.h_in.ptr) + rows * d.in_words, r->in, r->count * d.in_words * 8);
+        if (d.lut)
+            for (size_t i = 0; i < r->count; i++) hidx[rows + i] = (uint32_t)(base[b] + (r->idx ? r->idx[i] : 0));
+        rows += r->count;
+    }
+    const hipStream_t s = sl.stream;
+    check(hipMemcpyAsync(sl.d_in.ptr, sl.h_in.ptr, total * d.in_words * 8, hipMemcpyHostToDevice, s), "H2D batch");
+    if (d.lut) {
+        sl.d_luts.reserve(sets * glwe * 8);
+        check(hipMemcpyAsync(sl.d_luts.ptr, sl.h_luts.ptr, sets * glwe * 8, hipMemcpyHostToDevice, s), "H2D luts");
+        check(hipMemcpyAsync(sl.d_idx.ptr, hidx, total * 4, hipMemcpyHostToDevice, s), "H2D idx");
+    }
+    d.launch(c, (const uint64_t *)sl.d_in.ptr, (uint64_t *)sl.d_out.ptr, (const uint64_t *)sl.d_luts.ptr,
+             d.lut ? sets : 0, d.lut && sets > 1 ? (const uint32_t *)sl.d_idx.ptr : nullptr, total,
+             scratch ? sl.d_scratch.ptr : nullptr, scratch ? sl.d_scratch.bytes : 0, s);
+    check(hipMemcpyAsync(sl.h_out.ptr, sl.d_out.ptr, total * d.out_words * 8, hipMemcpyDeviceToHost, s), "D2H batch");
+    check(hipStreamSynchronize(s), "batch sync");
+    rows = 0;
+    for (auto *r : batch) {
+        std::memcpy(r->out, static_cast<uint64_t *>(sl.h_out.ptr) + rows * d.out_words, r->count * d.out_words * 8);
+        rows += r->count;
+    }
+}
+
+// the calling thread's request joins the op's queue; whichever caller finds no collector becomes
+// it, waits up to the window for a full batch, takes the queue and runs it on a free slot
+void coalesced_call(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
+    auto &co = c->co;
+    std::unique_lock<std::mutex> lk(co.m);
+    co.queue[op].push_back(&r);
+    co.queued[op] += r.count;
+    co.cv.notify_all();
+    const size_t cap = coalesce_batch();
+    while (!r.done) {
+        if (co.collecting[op] || co.queue[op].empty()) {
+            co.cv.wait(lk);
+            continue;
+        }
+        co.collecting[op] = true;
+        co.cv.wait_until(lk, std::chrono::steady_clock::now() + coalesce_window(),
+                         [&] { return co.queued[op] >= cap; });
+        std::vector<CoalescedReq *> batch;
+        size_t cts = 0;
+        auto &q = co.queue[op];
+        size_t take = 0;
+        while (take < q.size() && (batch.empty() || cts + q[take]->count <= cap)) {
+            cts += q[take]->count;
+            batch.push_back(q[take++]);
+        }
+        q.erase(q.begin(), q.begin() + take);
+        co.queued[op] -= cts;
+        co.collecting[op] = false;  // the next batch can gather while this one runs
+        co.cv.notify_all();
+        TfheMi355Context::Coalescer::Slot *sl = nullptr;
+        co.cv.wait(lk, [&] {
+            for (auto &x : co.slots)
+                if (!x.busy) {
+                    sl = &x;
+                    return true;
+                }
+            return false;
+        });
+        sl->busy = true;
+        lk.unlock();
+        std::string err;
+        try {
+            run_coalesced_batch(c, *sl, op, batch);
+        } catch (const std::exception &ex) {
+            err = ex.what();
+        }
+        lk.lock();
+        sl->busy = false;
+        for (auto *x : batch) {
+            x->err = err;
+            x->done = true;
+        }
+        co.cv.notify_all();
+    }
+    lk.unlock();
+    if (!r.err.empty()) fail("%s", r.err.c_str());
+}
+
+bool coalescible(size_t count) { return count > 0 && count <= coalesce_max_count(); }
 }  // namespace
 
 extern "C" {
@@ -737,6 +942,11 @@ int tfhe_mi355_context_destroy(TfheMi355Context *ctx) {
             if (L.stream) (void)hipStreamDestroy(L.stream);
         }
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+        for (auto &sl : ctx->co.slots)
+            if (sl.stream) {
+                (void)hipStreamSynchronize(sl.stream);
+                (void)hipStreamDestroy(sl.stream);
+            }
         delete ctx;  // device and pinned buffers free themselves
     });
 }
@@ -953,11 +1163,15 @@ int tfhe_mi355_programmable_bootstrap(TfheMi355Context *ctx, const uint64_t *lwe
                                       size_t count) {
     return guarded([&] {
         if (!ctx || (!lwe_in && count) || (!lwe_out && count) || !luts) fail("null argument");
-        std::lock_guard<std::mutex> g(ctx->mu);
         check(hipSetDevice(ctx->device), "hipSetDevice");
         require_fbsk(ctx);
         if (lut_count == 0) fail("lut_count must be >= 1");
         validate_lut_indexes(lut_indexes, count, lut_count);
+        if (coalescible(count)) {
+            CoalescedReq r{lwe_in, lwe_out, luts, lut_count, lut_indexes, count};
+            return coalesced_call(ctx, CO_PBS, r);
+        }
+        std::lock_guard<std::mutex> g(ctx->mu);
         run_host_pipeline(ctx, lwe_in, ctx->n() + 1, lwe_out, ctx->big_dim() + 1, luts, ctx->glwe_len(), lut_count,
                           lut_indexes, count, chunk_pbs, pbs_scratch_bytes);
     });
@@ -1103,9 +1317,13 @@ int tfhe_mi355_glwe_poly_mul_async(TfheMi355Context *ctx, const uint64_t *d_glwe
 int tfhe_mi355_keyswitch(TfheMi355Context *ctx, const uint64_t *lwe_in, uint64_t *lwe_out, size_t count) {
     return guarded([&] {
         if (!ctx || (!lwe_in && count) || (!lwe_out && count)) fail("null argument");
-        std::lock_guard<std::mutex> g(ctx->mu);
         check(hipSetDevice(ctx->device), "hipSetDevice");
         require_ksk(ctx);
+        if (coalescible(count)) {
+            CoalescedReq r{lwe_in, lwe_out, nullptr, 0, nullptr, count};
+            return coalesced_call(ctx, CO_KS, r);
+        }
+        std::lock_guard<std::mutex> g(ctx->mu);
         run_host_pipeline(ctx, lwe_in, ctx->big_dim() + 1, lwe_out, ctx->n() + 1, nullptr, 0, 0, nullptr, count,
                           chunk_ks, ks_scratch_bytes);
     });
@@ -1154,12 +1372,16 @@ int tfhe_mi355_keyswitch_programmable_bootstrap(TfheMi355Context *ctx, const uin
                                                 const uint32_t *lut_indexes, size_t count) {
     return guarded([&] {
         if (!ctx || (!lwe_in && count) || (!lwe_out && count) || !luts) fail("null argument");
-        std::lock_guard<std::mutex> g(ctx->mu);
         check(hipSetDevice(ctx->device), "hipSetDevice");
         require_fbsk(ctx);
         require_ksk(ctx);
         if (lut_count == 0) fail("lut_count must be >= 1");
         validate_lut_indexes(lut_indexes, count, lut_count);
+        if (coalescible(count)) {
+            CoalescedReq r{lwe_in, lwe_out, luts, lut_count, lut_indexes, count};
+            return coalesced_call(ctx, CO_KS_PBS, r);
+        }
+        std::lock_guard<std::mutex> g(ctx->mu);
         run_host_pipeline(ctx, lwe_in, ctx->big_dim() + 1, lwe_out, ctx->big_dim() + 1, luts, ctx->glwe_len(),
                           lut_count, lut_indexes, count, launch_ks_pbs_dev, ks_pbs_scratch_bytes);
     });
@@ -1191,12 +1413,16 @@ int tfhe_mi355_programmable_bootstrap_keyswitch(TfheMi355Context *ctx, const uin
                                                 const uint32_t *lut_indexes, size_t count) {
     return guarded([&] {
         if (!ctx || (!lwe_in && count) || (!lwe_out && count) || !luts) fail("null argument");
-        std::lock_guard<std::mutex> g(ctx->mu);
         check(hipSetDevice(ctx->device), "hipSetDevice");
         require_fbsk(ctx);
         require_ksk(ctx);
         if (lut_count == 0) fail("lut_count must be >= 1");
         validate_lut_indexes(lut_indexes, count, lut_count);
+        if (coalescible(count)) {
+            CoalescedReq r{lwe_in, lwe_out, luts, lut_count, lut_indexes, count};
+            return coalesced_call(ctx, CO_PBS_KS, r);
+        }
+        std::lock_guard<std::mutex> g(ctx->mu);
         run_host_pipeline(ctx, lwe_in, ctx->n() + 1, lwe_out, ctx->n() + 1, luts, ctx->glwe_len(), lut_count,
                           lut_indexes, count, launch_pbs_ks_dev, pbs_ks_scratch_bytes);
     });
