@@ -90,6 +90,33 @@ PARAMS = {  # --params choice -> (parameter set name, workload text, kernel name
 }
 
 
+
+def _split_params():
+    """`--params m_c`: every shortint KS_PBS set at N = 4096 ... 32768 (the split CMUX, pbs_large.hip)
+    as a shortint apply_lookup_table (KS -> PBS) batch; 4_4 keeps its grouped-CMUX entry above."""
+    sys.path.insert(0, os.path.join(ROOT, "tfhe-rs-odd_amd"))
+    from tfhe_mi355.parameters import SHORTINT_ALL, SHORTINT_SOURCE_LINE
+
+    out = {}
+    for name, p in SHORTINT_ALL.items():
+        if p.polynomial_size < 4096 or not name.endswith("_KS_PBS"):
+            continue
+        tag = f"{p.message_modulus.bit_length() - 1}_{p.carry_modulus.bit_length() - 1}"
+        if tag == "4_4":
+            continue
+        out[tag] = (name, f"shortint apply_lookup_table (keyswitch -> PBS) at {name} (shortint/parameters/mod.rs:"
+                          f"{SHORTINT_SOURCE_LINE[name]}), N={p.polynomial_size}, batch per GPU; the reference publishes "
+                          + ("121 ms per KS+PBS at 3_3 (benchmarks.md:42)" if tag == "3_3" else "no number for this set"),
+                    f"large_sub_kernel<{p.polynomial_size},1,{p.pbs_level}> (+ large_top_fwd/top_inv per CMUX, "
+                    "ks_mfma_kernel)")
+    return out
+
+
+PARAMS.update(_split_params())
+SPLIT_TAGS = {t for t, v in PARAMS.items() if v[2].startswith("large_sub_kernel")}
+WITH_KS = {"4_4", "2_2ks"} | SPLIT_TAGS
+
+
 # ---------------------------------------------------------------------------------------------
 # models (SURVEY.md 8d)
 
@@ -158,6 +185,7 @@ DOMINANT = {
     "aes40": ("pbs_classic_kernel", "pbs_classic_kernel<512,3,4>"),
     "sha3": ("pbs_classic_kernel", "pbs_classic_kernel<256,5,1>"),
 }
+DOMINANT.update({t: ("large_sub_kernel", PARAMS[t][2].split(" ")[0]) for t in SPLIT_TAGS})
 
 
 def load_pmc(tag: str, kernel: str):
@@ -191,6 +219,25 @@ def large_group_flops(p) -> float:
     return (k1 * L * (6 * M + 5 * M * math.log2(M)) + k1 * k1 * L * M * 8 + k1 * 5 * M * 10)
 
 
+def split_sub_flops(p) -> float:
+    """FP64 flop of large_sub_kernel per ciphertext and CMUX (split CMUX, pbs_large.hip): the
+    1024-point forward sub-FFTs of the (k+1)L digit polynomials (5 M log2(1024) each, M = R 1024),
+    the MAC ((k+1)^2 L M 8) and the (k+1) inverse sub-FFTs; the top radix-R stages and the twist run
+    in large_top_fwd / large_top_inv."""
+    M = p.polynomial_size // 2
+    k1, L = p.glwe_dimension + 1, p.pbs_level
+    return k1 * L * 5 * M * 10 + k1 * k1 * L * M * 8 + k1 * 5 * M * 10
+
+
+def split_chunk(p, units: int) -> int:
+    """Ciphertexts per pass of the split CMUX (capi.cpp large_chunk)."""
+    if p.polynomial_size >= 32768:
+        return min(units, 128)
+    M, k1 = p.polynomial_size // 2, p.glwe_dimension + 1
+    per = k1 * p.polynomial_size * 8 + p.pbs_level * k1 * M * 16
+    return min(units, min(1024, max(64, (160 << 20) // per // 64 * 64)))
+
+
 def large_memory_model(p):
     """Bytes per ciphertext and CMUX of the two memory kernels of the N = 32768 grouped CMUX
     (DESIGN.md 5.3): large_digits reads the accumulator rows (twice: self and rotated) and writes
@@ -210,7 +257,8 @@ def roofline(tag, p, units_per_launch: int, step_ms: float, kname: str, with_ks:
     steps_flop = pbs_flops(p) * units_per_launch
     fp64_step = steps_flop / (step_ms * 1e-3) / 1e12
     large = p.polynomial_size > 2048
-    chunk = min(units_per_launch, 128) if large else units_per_launch
+    grouped = p.polynomial_size == 32768 and p.pbs_level == 2 and p.glwe_dimension == 1
+    chunk = split_chunk(p, units_per_launch) if large else units_per_launch
     kt = (ktimes or {}).get(fam)
     if kt:
         kernel_ms, timed = kt
@@ -218,7 +266,7 @@ def roofline(tag, p, units_per_launch: int, step_ms: float, kname: str, with_ks:
     else:  # one launch per step (or a replayed graph): the step's own events
         kernel_ms, timed = step_ms, None
         kernel_src = "HIP events around the whole step on the launch stream (no per-kernel timer)"
-    flop_launch = large_group_flops(p) * chunk if large else steps_flop
+    flop_launch = ((large_group_flops(p) if grouped else split_sub_flops(p)) * chunk) if large else steps_flop
     fp64 = flop_launch / (kernel_ms * 1e-3) / 1e12
     if tag == "mul32":
         pmc, why = None, ("the multiply DAG replays the 2_2 KS+PBS kernels in one hipGraph: their per-kernel "
@@ -233,7 +281,10 @@ def roofline(tag, p, units_per_launch: int, step_ms: float, kname: str, with_ks:
          "units_per_launch": chunk,
          "model": ((f"large_group_cmux_kernel FP64 flop per ciphertext and CMUX {large_group_flops(p):,.0f} "
                     f"(twist, forward FFTs incl. the top radix-16 share, MAC, inverse sub-FFTs) x {chunk} ciphertexts "
-                    f"per launch / its average launch duration") if large else
+                    f"per launch / its average launch duration") if grouped else
+                   (f"large_sub_kernel FP64 flop per ciphertext and CMUX {split_sub_flops(p):,.0f} (1024-point "
+                    f"forward and inverse sub-FFTs, MAC) x {chunk} ciphertexts per launch / its average launch "
+                    f"duration") if large else
                    (f"FP64 flop model (SURVEY.md 8d): {pbs_flops(p):,.0f} flop per PBS x {units_per_launch} PBS per "
                     f"launch / the kernel's average launch duration")),
          "traffic_note": ("L2<->fabric bytes per launch of this kernel (2 FETCH_SIZE + WRITE_SIZE, gfx950 correction; "
@@ -256,7 +307,7 @@ def roofline(tag, p, units_per_launch: int, step_ms: float, kname: str, with_ks:
                 "streaming_model_GBps": stream_b * units_per_launch / secs / 1e9,
                 "min_unique_bytes_per_pbs": pbs_min_unique_bytes(p, units_per_launch, with_ks),
                 "note": "BSK-streaming model (SURVEY.md 8d) over the whole step; >8 TB/s means on-chip reuse"}
-    if large and ktimes:
+    if grouped and ktimes:
         mem = {}
         for kn, b in large_memory_model(p).items():
             t = ktimes.get(kn)
@@ -805,7 +856,7 @@ def run_pbs(args, P, pname, workload, kname, R):
     from tfhe_mi355 import client, fill_accumulator
     from tfhe_mi355.distributed import shard_range
 
-    with_ks = args.params in ("4_4", "2_2ks")   # config 3 and the 2_2 KS+PBS line
+    with_ks = args.params in WITH_KS   # config 3, the other shortint sets at N >= 4096, the 2_2 KS+PBS line
     B = args.batch or (1024 if args.params == "4_4" else 4096)
     msg_space = P.message_modulus * P.carry_modulus
     eng, lwe_sk, glwe_sk, bsk, ksk, setup = make_keys(args, P, R, with_ks)

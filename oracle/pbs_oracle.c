@@ -328,9 +328,11 @@ static int radix_plan(int M, int *rad) {
     switch (M) {
     case 512: rad[0] = 8; rad[1] = 8; rad[2] = 8; return 3;
     case 1024: rad[0] = 16; rad[1] = 16; rad[2] = 4; return 3;
-    case 2048: rad[0] = 16; rad[1] = 16; rad[2] = 8; return 3;
-    case 4096: rad[0] = 16; rad[1] = 16; rad[2] = 16; return 3;
-    case 8192: rad[0] = 16; rad[1] = 16; rad[2] = 16; rad[3] = 2; return 4;
+    /* N = 4096 / 8192 / 16384: top radix R = M / 1024, then the 1024-point [16, 16, 4] plan of
+     * each sub-block -- the engine's split CMUX (pbs_large.hip) runs this DAG */
+    case 2048: rad[0] = 2; rad[1] = 16; rad[2] = 16; rad[3] = 4; return 4;
+    case 4096: rad[0] = 4; rad[1] = 16; rad[2] = 16; rad[3] = 4; return 4;
+    case 8192: rad[0] = 8; rad[1] = 16; rad[2] = 16; rad[3] = 4; return 4;
     case 16384: rad[0] = 16; rad[1] = 16; rad[2] = 16; rad[3] = 4; return 4;
     case 256: rad[0] = 16; rad[1] = 16; return 2;
     case 128: rad[0] = 16; rad[1] = 8; return 2;

@@ -73,7 +73,8 @@ def _digit_reversed_index(M, radices):
 
 
 @pytest.mark.parametrize("M,radices", [(1024, [16, 16, 4]), (512, [8, 8, 8]), (16384, [16, 16, 16, 4]),
-                                       (64, [16, 4]), (2048, [16, 16, 8])])
+                                       (64, [16, 4]), (2048, [2, 16, 16, 4]), (4096, [4, 16, 16, 4]),
+                                       (8192, [8, 16, 16, 4])])
 def test_complex_fft_matches_dft(orc, M, radices):
     rng = np.random.default_rng(M)
     z = rng.standard_normal(M) + 1j * rng.standard_normal(M)

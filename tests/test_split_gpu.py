@@ -1,0 +1,204 @@
+"""GPU parity tests of the split CMUX (N = 4096 ... 32768, pbs_large.hip) and of every shortint
+parameter set of the reference (shortint/parameters/mod.rs:598-1201).
+
+The split CMUX runs the oracle's [R | 16, 16, 4] FFT DAG (R = N / 2048) with the accumulator in
+device scratch: top radix-R stage, 1024-point sub-block FFTs + MAC, top inverse stage.  The bar is
+bit-exact u64 outputs against the oracle on the same inputs (and decryption round trips), at
+reduced LWE dimension n so that the oracle finishes in seconds; the full 3_3 shape (n = 864) is
+checked through KS -> PBS decryptions plus two bit-exact ciphertexts.
+
+Keys come from the engine's client-side keygen (exact FFT negacyclic products) and are fed to both
+sides as standard u64 keys.
+"""
+import numpy as np
+import pytest
+
+from conftest import decode
+
+pytestmark = pytest.mark.gpu
+
+
+def _keys(orc, p, seed):
+    from tfhe_mi355 import client
+
+    lwe_sk = client.gen_binary_key(seed, 1, p.lwe_dimension)
+    glwe_sk = client.gen_binary_key(seed, 2, p.big_lwe_dimension)
+    bsk = client.gen_bootstrap_key(seed + 1, lwe_sk, glwe_sk, p.glwe_dimension, p.polynomial_size, p.pbs_base_log,
+                                   p.pbs_level, p.glwe_modular_std_dev)
+    fbsk = orc.FourierBsk(bsk, p.lwe_dimension, p.glwe_dimension, p.polynomial_size, p.pbs_base_log, p.pbs_level)
+    return lwe_sk, glwe_sk, bsk, fbsk
+
+
+def _engine(p, bsk, ksk=None):
+    from tfhe_mi355 import Engine
+
+    e = Engine(p, 0)
+    e.upload_bootstrap_key(bsk)
+    if ksk is not None:
+        e.upload_keyswitch_key(ksk)
+    return e
+
+
+def _device_to_host(ptr, nbytes):
+    import ctypes
+
+    import torch  # noqa: F401  (loads libamdhip64)
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    out = np.empty(nbytes // 8, dtype=np.uint64)
+    assert hip.hipMemcpy(ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(ptr), ctypes.c_size_t(nbytes), 2) == 0
+    return out
+
+
+def engine_position(N):
+    """FFT position of each engine-layout spectrum element: sub-block q = e // 1024 holds
+    positions 1024 q + the WaveFft<1024> layout."""
+    e = np.arange(N // 2)
+    lane, s, blk = e % 64, (e // 64) % 16, e // 1024
+    return 1024 * blk + 64 * (lane & 15) + 16 * (lane >> 4) + s
+
+
+SPLIT = ["PARAM_MESSAGE_1_CARRY_4_KS_PBS",   # N = 4096,  L = 2, base 2^15
+         "PARAM_MESSAGE_2_CARRY_3_KS_PBS",   # N = 4096,  L = 1, base 2^22
+         "PARAM_MESSAGE_3_CARRY_3_KS_PBS",   # N = 8192,  L = 2
+         "PARAM_MESSAGE_6_CARRY_0_KS_PBS",   # N = 8192,  L = 1, base 2^22
+         "PARAM_MESSAGE_1_CARRY_6_KS_PBS",   # N = 16384, L = 3, base 2^11 (33 decomposed bits)
+         "PARAM_MESSAGE_2_CARRY_5_KS_PBS",   # N = 16384, L = 2
+         "PARAM_MESSAGE_1_CARRY_7_KS_PBS"]   # N = 32768, L = 3 (the generic path, not the grouped one)
+
+
+@pytest.mark.parametrize("N", [4096, 8192, 16384])
+def test_split_fourier_bsk_bit_exact_vs_oracle(orc, N):
+    from tfhe_mi355 import client
+    from tfhe_mi355.parameters import SHORTINT_ALL
+
+    p = next(q for q in SHORTINT_ALL.values() if q.polynomial_size == N).with_(lwe_dimension=2)
+    lwe_sk = client.gen_binary_key(3, 1, 2)
+    glwe_sk = client.gen_binary_key(3, 2, N)
+    bsk = client.gen_bootstrap_key(4, lwe_sk, glwe_sk, 1, N, p.pbs_base_log, p.pbs_level, p.glwe_modular_std_dev)
+    eng = _engine(p, bsk)
+    ptr, nbytes = eng.fourier_bootstrap_key()
+    got = _device_to_host(ptr, nbytes).view(np.complex128).reshape(-1, N // 2)
+    exp = orc.FourierBsk(bsk, 2, 1, N, p.pbs_base_log, p.pbs_level).fourier().reshape(-1, N // 2)
+    exp = np.ascontiguousarray(exp[:, engine_position(N)])
+    exp = np.ldexp(exp.view(np.float64), -int(np.log2(N // 2))).view(np.complex128)  # the resident 1/M
+    bad = np.count_nonzero(got.view(np.uint64) != exp.view(np.uint64))
+    assert bad == 0, f"{bad} of {got.size * 2} doubles differ; max |diff| {np.max(np.abs(got - exp))}"
+
+
+@pytest.mark.parametrize("name", SPLIT)
+def test_split_pbs_bit_exact_vs_oracle(orc, name):
+    """Per-ciphertext LUTs, 8-bit-wide message spaces, edge inputs (b~ = 2N, every a~ = 0, a~ = N,
+    alternating all-ones masks): bit-exact against the oracle's PBS at n = 6."""
+    from tfhe_mi355.parameters import SHORTINT_ALL
+
+    p = SHORTINT_ALL[name].with_(lwe_dimension=6)
+    N, space = p.polynomial_size, p.message_modulus * p.carry_modulus
+    lwe_sk, glwe_sk, bsk, fbsk = _keys(orc, p, 51)
+    eng = _engine(p, bsk)
+    fs = [lambda x: x, lambda x: (3 * x + 1) % space]
+    luts = np.stack([orc.fill_accumulator(N, 1, p.message_modulus, p.carry_modulus, f) for f in fs])
+    msgs = np.array([0, 1, space // 2, space - 1, 5 % space, 7 % space])
+    idx = np.array([0, 1, 1, 0, 1, 0])
+    cts = orc.lwe_encrypt(61, lwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta), p.lwe_modular_std_dev)
+    edge = np.random.default_rng(9).integers(0, 2 ** 64, (4, p.lwe_dimension + 1), dtype=np.uint64)
+    edge[0, -1] = np.uint64((1 << 64) - 1)
+    edge[1, :-1] = 0
+    edge[2, :-1] = np.uint64(1 << 63)
+    edge[3, ::2] = np.uint64((1 << 64) - 1)
+    allc = np.concatenate([cts, edge])
+    alli = np.concatenate([idx, [0, 1, 0, 1]]).astype(np.uint32)
+    got = eng.programmable_bootstrap(allc, luts, lut_indexes=alli)
+    exp = fbsk.pbs(allc, luts, lut_idx=alli, threads=8)
+    bad = np.nonzero(np.any(got != exp, axis=1))[0]
+    assert bad.size == 0, f"{name}: ciphertexts {bad} differ ({np.count_nonzero(got != exp)} words)"
+    dec = decode(orc.lwe_decrypt(glwe_sk, got[:6]), p.delta) % space
+    assert np.array_equal(dec, [fs[i](m) for i, m in zip(idx, msgs)])
+
+
+def test_split_pbs_chunks_ragged(orc):
+    """More ciphertexts than one pass of the split CMUX holds (TFHE_MI355_LARGE_CHUNK is not set:
+    the chunk follows from the scratch given): 3 passes of 64 + a ragged 17 through the async entry
+    with a deliberately small scratch; every output equals the one-pass host call."""
+    import torch
+
+    from tfhe_mi355.parameters import PARAM_MESSAGE_3_CARRY_3_KS_PBS
+
+    p = PARAM_MESSAGE_3_CARRY_3_KS_PBS.with_(lwe_dimension=4)
+    lwe_sk, glwe_sk, bsk, fbsk = _keys(orc, p, 71)
+    eng = _engine(p, bsk)
+    msgs = np.random.default_rng(3).integers(0, 64, 209)
+    cts = orc.lwe_encrypt(72, lwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta), p.lwe_modular_std_dev)
+    acc = orc.fill_accumulator(p.polynomial_size, 1, 8, 8, lambda x: (x * 5 + 3) % 64)
+    ref = eng.programmable_bootstrap(cts, acc)
+    dev = torch.device("cuda", 0)
+    per = eng.pbs_scratch_bytes(1)
+    d_in = torch.from_numpy(cts.view(np.int64)).to(dev)
+    d_out = torch.zeros((209, p.big_lwe_dimension + 1), dtype=torch.int64, device=dev)
+    d_lut = torch.from_numpy(acc.view(np.int64)).to(dev)
+    scratch = torch.empty(per * 64, dtype=torch.uint8, device=dev)
+    eng.programmable_bootstrap_async(d_in, d_out, d_lut, 1, 209, d_scratch=scratch)
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy().view(np.uint64)
+    assert np.array_equal(got, ref)
+    assert np.array_equal(decode(orc.lwe_decrypt(glwe_sk, got), p.delta) % 64, (msgs * 5 + 3) % 64)
+    sample = np.array([0, 63, 64, 200, 208])
+    assert np.array_equal(got[sample], fbsk.pbs(cts[sample], acc, threads=5))
+
+
+@pytest.mark.timeout(900)
+def test_full_3_3_keyswitch_pbs(orc):
+    """Full PARAM_MESSAGE_3_CARRY_3_KS_PBS (n = 864, N = 8192, L = 2; the reference's 121 ms
+    KS+PBS set, benchmarks.md:42): KS -> PBS decrypts to f(m); two ciphertexts bit-exact."""
+    from tfhe_mi355 import client
+    from tfhe_mi355.parameters import PARAM_MESSAGE_3_CARRY_3_KS_PBS as P
+
+    lwe_sk, glwe_sk, bsk, fbsk = _keys(orc, P, 81)
+    ksk = client.gen_keyswitch_key(83, glwe_sk, lwe_sk, P.ks_base_log, P.ks_level, P.lwe_modular_std_dev)
+    eng = _engine(P, bsk, ksk)
+    msgs = np.array([0, 5, 17, 33, 63, 40, 9, 50])
+    big = orc.lwe_encrypt(84, glwe_sk, msgs.astype(np.uint64) * np.uint64(P.delta), P.glwe_modular_std_dev)
+    acc = orc.fill_accumulator(P.polynomial_size, 1, 8, 8, lambda x: (x + 11) % 64)
+    out = eng.keyswitch_programmable_bootstrap(big, acc)
+    assert np.array_equal(decode(orc.lwe_decrypt(glwe_sk, out), P.delta) % 64, (msgs + 11) % 64)
+    small = orc.keyswitch(ksk, P.big_lwe_dimension, P.lwe_dimension, P.ks_base_log, P.ks_level, big[:2])
+    assert np.array_equal(out[:2], fbsk.pbs(small, acc, threads=2))
+
+
+def _all_sets():
+    from tfhe_mi355.parameters import SHORTINT_ALL
+
+    return sorted(SHORTINT_ALL)
+
+
+@pytest.mark.parametrize("name", _all_sets())
+def test_every_shortint_parameter_set_bit_exact(orc, name):
+    """Every shortint ClassicPBSParameters set of the reference creates a context, and its keyswitch
+    and PBS (KS -> PBS for the Big-key sets, PBS -> KS for the Small-key ones) are bit-exact
+    against the oracle at n = 4, outputs decrypting to f(m)."""
+    from tfhe_mi355 import client
+    from tfhe_mi355.parameters import SHORTINT_ALL
+
+    p = SHORTINT_ALL[name].with_(lwe_dimension=4)
+    N, k, space = p.polynomial_size, p.glwe_dimension, p.message_modulus * p.carry_modulus
+    lwe_sk, glwe_sk, bsk, fbsk = _keys(orc, p, 91)
+    ksk = client.gen_keyswitch_key(92, glwe_sk, lwe_sk, p.ks_base_log, p.ks_level, p.lwe_modular_std_dev)
+    eng = _engine(p, bsk, ksk)
+    f = lambda x: (x * 3 + 1) % space  # noqa: E731
+    acc = orc.fill_accumulator(N, k, p.message_modulus, p.carry_modulus, f)
+    msgs = np.arange(4) * max(1, space // 4) % space
+    if p.encryption_key_choice == "Big":
+        big = orc.lwe_encrypt(93, glwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta), p.glwe_modular_std_dev)
+        small = orc.keyswitch(ksk, p.big_lwe_dimension, p.lwe_dimension, p.ks_base_log, p.ks_level, big)
+        assert np.array_equal(eng.keyswitch(big), small), "keyswitch differs from the oracle"
+        out = eng.keyswitch_programmable_bootstrap(big, acc)
+        assert np.array_equal(out, fbsk.pbs(small, acc, threads=4)), "KS -> PBS differs from the oracle"
+        dec = decode(orc.lwe_decrypt(glwe_sk, out), p.delta) % space
+    else:
+        small = orc.lwe_encrypt(93, lwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta), p.lwe_modular_std_dev)
+        big = fbsk.pbs(small, acc, threads=4)
+        out = eng.programmable_bootstrap_keyswitch(small, acc)
+        exp = orc.keyswitch(ksk, p.big_lwe_dimension, p.lwe_dimension, p.ks_base_log, p.ks_level, big)
+        assert np.array_equal(out, exp), "PBS -> KS differs from the oracle"
+        dec = decode(orc.lwe_decrypt(lwe_sk, out), p.delta) % space
+    assert np.array_equal(dec, [f(m) for m in msgs])

@@ -218,12 +218,13 @@ void build_tables(TfheMi355Context *c) {
     check(hipMalloc(&c->tables.twist, bytes), "hipMalloc(twist)");
     check(hipMemcpy(c->tables.W, W.data(), bytes, hipMemcpyHostToDevice), "upload W");
     check(hipMemcpy(c->tables.twist, tw.data(), bytes, hipMemcpyHostToDevice), "upload twist");
-    if (M >= 16 * 1024) {
-        // the large-N top radix-16 stage reads W[a c] for a < M/16: laid out [c-1][a] so that a
-        // wave's 64 consecutive butterflies read 1 KiB contiguously instead of 64 scattered lines
-        const int A = M / 16;
-        std::vector<double2> top((size_t)15 * A);
-        for (int c = 1; c < 16; c++)
+    if (N >= 4096) {
+        // the split CMUX's top radix-R stage (R = M / 1024) reads W[a c] for a < 1024: laid out
+        // [c-1][a] so that a wave's 64 consecutive butterflies read 1 KiB contiguously instead of
+        // 64 scattered lines
+        const int A = 1024, R = M / A;
+        std::vector<double2> top((size_t)(R - 1) * A);
+        for (int c = 1; c < R; c++)
             for (int a = 0; a < A; a++) top[(size_t)(c - 1) * A + a] = W[(size_t)a * c];
         const size_t tb = sizeof(double2) * top.size();
         check(hipMalloc(&c->tables.wtop, tb), "hipMalloc(wtop)");
@@ -253,22 +254,26 @@ bool is_large(const TfheMi355Context *c) {
     return !c->p.grouping_factor && large_pbs_supported((int)c->N(), (int)c->k(), (int)c->p.pbs_level);
 }
 
-// N = 32768: ciphertexts per pass of the three-launch CMUX.  The chunk's accumulators + spectra
-// (1.5 MiB per ciphertext at 4_4) should stay resident in the 256 MiB Infinity Cache.
-size_t large_chunk() {
-    static const size_t v = [] {
+// N >= 4096: ciphertexts per pass of the split CMUX.  The chunk's accumulators + spectra should
+// stay resident in the 256 MiB Infinity Cache: 128 at N = 32768 (1.5 MiB per ciphertext at 4_4,
+// best of 64..1024 measured), otherwise ~160 MiB worth in multiples of 64 (64..1024).
+size_t large_chunk(const TfheMi355Context *c) {
+    static const size_t forced = [] {
         const char *e = std::getenv("TFHE_MI355_LARGE_CHUNK");
         const long x = e ? std::atol(e) : 0;
-        return x > 0 ? (size_t)x : (size_t)128;  // 128: best of 64..1024 at 4_4 (profiles)
+        return x > 0 ? (size_t)x : (size_t)0;
     }();
-    return v;
+    if (forced) return forced;
+    if (c->N() >= 32768) return 128;
+    const size_t per = large_pbs_scratch_per_ct((int)c->N(), (int)c->k(), (int)c->p.pbs_level);
+    return std::min<size_t>(1024, std::max<size_t>(64, ((size_t)160 << 20) / per / 64 * 64));
 }
 
 size_t pbs_scratch_bytes(const TfheMi355Context *c, size_t count) {
     if (count == 0 || c->p.grouping_factor) return 0;
     if (!is_large(c)) return classic_pbs_ticket_bytes((int)c->N(), (int)c->k(), (int)c->p.pbs_level);
     const size_t per_ct = large_pbs_scratch_per_ct((int)c->N(), (int)c->k(), (int)c->p.pbs_level);
-    return per_ct * std::min(count, large_chunk());
+    return per_ct * std::min(count, large_chunk(c));
 }
 
 bool ks_use_mfma(const TfheMi355Context *c) {
@@ -357,7 +362,7 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
         a.base_log = (int)c->p.pbs_base_log;
         a.count = (int)count;
         a.scratch = scratch;
-        a.scratch_bytes = std::min(scratch_bytes, per_ct * large_chunk());
+        a.scratch_bytes = std::min(scratch_bytes, per_ct * large_chunk(c));
         a.timer = c->timer_or_null();
         check(launch_large_pbs((int)c->N(), (int)c->k(), (int)c->p.pbs_level, a, s), "launch large pbs");
         return;
@@ -524,7 +529,7 @@ size_t host_chunk(const TfheMi355Context *c, size_t count) {
         return x > 0 ? (size_t)x : (size_t)0;
     }();
     if (forced) return forced;
-    if (is_large(c)) return large_chunk();
+    if (is_large(c)) return large_chunk(c);
     // >= 4 chunks so that copies hide behind kernels (also with pinned caller buffers: 2 chunks
     // measured 93.5k vs 112.9k PBS/s at 4096); >= one full wave of PBS slots (256 CUs x 4
     // ciphertexts) and <= 4 waves per launch
@@ -902,8 +907,16 @@ int tfhe_mi355_context_create(const TfheMi355Parameters *params, int device, Tfh
                    !large_pbs_supported((int)p.polynomial_size, (int)p.glwe_dimension, (int)p.pbs_level)) {
             fail("no kernel for N=%u k=%u pbs_level=%u", p.polynomial_size, p.glwe_dimension, p.pbs_level);
         }
-        if (p.pbs_base_log < 2 || p.pbs_base_log * p.pbs_level > 30)
-            fail("pbs decomposition base_log*level must be in [2, 30] (got %u x %u)", p.pbs_base_log, p.pbs_level);
+        // the N <= 2048 kernels (and the grouped N = 32768 CMUX) decompose in 32-bit registers;
+        // the split CMUX of N >= 4096 in 64-bit ones (the shortint sets reach 11 x 3 = 33 bits)
+        const bool split = !p.grouping_factor && p.polynomial_size >= 4096;
+        const uint32_t max_bits = split ? 63 : 30;
+        if (p.pbs_base_log < 2 || p.pbs_base_log * p.pbs_level > max_bits)
+            fail("pbs decomposition base_log*level must be in [2, %u] (got %u x %u)", max_bits, p.pbs_base_log,
+                 p.pbs_level);
+        // the split CMUX keeps the lower levels' digits as int16 between passes
+        if (split && p.pbs_level > 1 && p.pbs_base_log > 16)
+            fail("pbs base_log %u > 16 with %u levels at N = %u", p.pbs_base_log, p.pbs_level, p.polynomial_size);
         if (p.ks_level && (p.ks_base_log == 0 || p.ks_base_log * p.ks_level >= 64)) fail("invalid ks decomposition");
         if (p.lwe_dimension == 0) fail("lwe_dimension must be > 0");
         check(hipSetDevice(device), "hipSetDevice");

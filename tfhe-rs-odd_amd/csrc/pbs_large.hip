@@ -106,133 +106,198 @@ __device__ __forceinline__ size_t spec_off(int wave, int h, int s, int lane) {
 
 }  // namespace
 
+// Shapes of the split CMUX (N = 4096 ... 32768, k = 1): M = N / 2 = R x 1024 -- a top radix-R
+// stage and R independent 1024-point sub-blocks ([R | 16, 16, 4], the oracle's radix_plan).
+template <int N>
+struct Split {
+    static constexpr int M = N / 2;
+    static constexpr int R = M / 1024;
+    static constexpr int LOGN = ilog2(N);
+    static constexpr int LOGM = LOGN - 1;
+    static_assert(R == 2 || R == 4 || R == 8 || R == 16, "top radix 2, 4, 8 or 16");
+};
+
 // Accumulator row layout: position p at u64 index 2 (p mod M) + (p div M), so the pair (j, j + M)
 // that one folded complex coefficient is made of sits in one 16-byte word (one load / store in
-// top_inv, one self and one rotated load per row in the digits).
-__device__ __forceinline__ int accx(int p) { return 2 * (p & (LM - 1)) + (p >> 14); }
-static_assert(LM == 1 << 14, "accx assumes M = 2^14");
+// top_inv, one self and one rotated load per row in the digits / top stage).
+template <int M>
+__device__ __forceinline__ int accx_m(int p) { return 2 * (p & (M - 1)) + (p >> ilog2(M)); }
+__device__ __forceinline__ int accx(int p) { return accx_m<LM>(p); }
 typedef unsigned long long acc_pair __attribute__((ext_vector_type(2)));
 // ct1 = X^{a~} acc - acc at positions j and j + M of one row (rem = a~ mod N, full_odd = a~ >= N):
 // the rotated sources j - rem and j + M - rem lie in ONE pair word, q = (j - rem) mod M, with its
 // halves swapped when only the first one wraps
-__device__ __forceinline__ void ct1_pair(const uint64_t *acc, int j, int rem, bool full_odd, uint64_t &d0,
-                                         uint64_t &d1) {
+template <int M>
+__device__ __forceinline__ void ct1_pair_m(const uint64_t *acc, int j, int rem, bool full_odd, uint64_t &d0,
+                                           uint64_t &d1) {
     const acc_pair self = *reinterpret_cast<const acc_pair *>(acc + 2 * j);
     const int jj0 = j - rem;  // in (-N, M)
-    const acc_pair rot = *reinterpret_cast<const acc_pair *>(acc + 2 * (jj0 & (LM - 1)));
-    const bool swap = jj0 < 0 && jj0 >= -LM;
+    const acc_pair rot = *reinterpret_cast<const acc_pair *>(acc + 2 * (jj0 & (M - 1)));
+    const bool swap = jj0 < 0 && jj0 >= -M;
     const uint64_t x0 = swap ? rot.y : rot.x, x1 = swap ? rot.x : rot.y;
-    const bool neg0 = (jj0 < 0) != full_odd, neg1 = (jj0 + LM < 0) != full_odd;
+    const bool neg0 = (jj0 < 0) != full_odd, neg1 = (jj0 + M < 0) != full_odd;
     d0 = (neg0 ? 0 - x0 : x0) - self.x;
     d1 = (neg1 ? 0 - x1 : x1) - self.y;
 }
+__device__ __forceinline__ void ct1_pair(const uint64_t *acc, int j, int rem, bool full_odd, uint64_t &d0,
+                                         uint64_t &d1) {
+    ct1_pair_m<LM>(acc, j, rem, full_odd, d0, d1);
+}
 
 // acc[ct] = LUT[idx] / X^{b~}  (bootstrap.rs:255-275)
-template <int K>
+template <int N, int K>
 __global__ void __launch_bounds__(256) large_init_kernel(LargePbsLaunch a, int ct0, int cnt) {
-    const size_t per = (size_t)(K + 1) * LN;
+    using S = Split<N>;
+    const size_t per = (size_t)(K + 1) * N;
     const size_t e = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= per * cnt) return;
     const int cl = (int)(e / per);
-    const int p = (int)((e % per) / LN), j = (int)(e % LN);
+    const int p = (int)((e % per) / N), j = (int)(e % N);
     const int ct = ct0 + cl;
     const uint64_t *in = a.lwe_in + (size_t)ct * (a.n + 1);
-    const uint32_t bt = pbs_modulus_switch<15>(in[a.n]);
+    const uint32_t bt = pbs_modulus_switch<S::LOGN>(in[a.n]);
     const uint32_t li = a.lut_indexes ? min(a.lut_indexes[ct], a.lut_count - 1u) : 0u;
-    const uint64_t *lut = a.luts + (size_t)li * (K + 1) * LN + (size_t)p * LN;
-    const int full = bt / LN, rem = bt % LN;
+    const uint64_t *lut = a.luts + (size_t)li * (K + 1) * N + (size_t)p * N;
+    const int full = bt / N, rem = bt % N;
     const int src = j + rem;
-    const bool wrap = src >= LN;
-    const uint64_t v = lut[wrap ? src - LN : src];
-    a.acc[(e / LN) * LN + accx(j)] = (wrap != (bool)(full & 1)) ? 0 - v : v;
+    const bool wrap = src >= N;
+    const uint64_t v = lut[wrap ? src - N : src];
+    a.acc[(e / N) * N + accx_m<S::M>(j)] = (wrap != (bool)(full & 1)) ? 0 - v : v;
+}
+
+// radix-R DFTs of the top stage, natural order in and out (the oracle's dft_fwd / dft_inv)
+template <int R>
+__device__ __forceinline__ void dftR_fwd(cx *v) {
+    if constexpr (R == 2) {
+        const cx x = v[0], y = v[1];
+        v[0] = cadd(x, y);
+        v[1] = csub(x, y);
+    } else if constexpr (R == 4) {
+        r4_fwd(v[0], v[1], v[2], v[3]);
+    } else if constexpr (R == 8) {
+        dft8_fwd(v);
+    } else {
+        dft16_fwd(v);
+    }
+}
+template <int R>
+__device__ __forceinline__ void dftR_inv(cx *v) {
+    if constexpr (R == 2) {
+        const cx x = v[0], y = v[1];
+        v[0] = cadd(x, y);
+        v[1] = csub(x, y);
+    } else if constexpr (R == 4) {
+        r4_inv(v[0], v[1], v[2], v[3]);
+    } else if constexpr (R == 8) {
+        dft8_inv(v);
+    } else {
+        dft16_inv(v);
+    }
+}
+
+// all L signed digits of x, level L (least significant) first -- SignedDecomposer::decompose
+// (decomposer.rs:99-153, iter.rs:134-141) in 64-bit arithmetic: any base_log * L <= 63 (the
+// shortint sets go up to 11 x 3 = 33 bits).  A rounding that overflows 2^(base_log L) leaves
+// every digit 0, as in the reference (whose discarded final state differs only there).
+template <int L>
+__device__ __forceinline__ void decompose64(uint64_t x, int beta, int32_t (&d)[L]) {
+    const int nonrep = 64 - beta * L;
+    uint64_t st = ((x >> (nonrep - 1)) + 1) >> 1;
+    const uint64_t mask = (1ull << beta) - 1;
+#pragma unroll
+    for (int l = 0; l < L; l++) {
+        const uint64_t res = st & mask;
+        st >>= beta;
+        uint64_t carry = ((res - 1) | st) & res;
+        carry >>= beta - 1;
+        st += carry;
+        d[l] = (int32_t)(int64_t)(res - (carry << beta));
+    }
 }
 
 // ---------------------------------------------------------------------------------------
-// CMUX: the M = 16384 FFT is [16 | 16, 16, 4], and after its top radix-16 stage
-// the 16 sub-blocks of 1024 positions are independent -- so are the MAC (per frequency) and the
-// inverse up to its own top stage.  Three launches per CMUX, each streaming at full occupancy
-// (one 512-thread workgroup per CU alternating memory and FFT phases was 16% slower):
-//   large_top_fwd : per (ct, row, butterfly a): rotate, decompose, twist, top DIF radix-16
-//                   -> T[ct][lvl][row][a + 1024 c]                        (no LDS)
+// Split CMUX (N = 4096 ... 32768): the accumulator (k+1) N u64 lives in device scratch and the
+// M-point FFT is [R | 16, 16, 4]; after its top radix-R stage the R sub-blocks of 1024 positions
+// are independent, and so are the MAC (per frequency) and the inverse up to its own top stage.
+// Three batch-wide launches per CMUX:
+//   large_top_fwd : per (ct, row, butterfly a < 1024): rotate, decompose (all L levels), twist,
+//                   top DIF radix-R per level -> T[ct][lvl][row][a + 1024 c]           (no LDS)
 //   large_sub     : per (ct, sub-block q): (k+1) L waves run the 1024-point WaveFft of their
-//                   poly's sub-block q, publish to LDS; wave c: MAC with GGSW sub-block q of
-//                   column c, inverse sub-FFT -> T[ct][0][c][q-block]     (79 KiB LDS)
-//   large_top_inv : per (ct, column, butterfly a): top DIT radix-16, backward conversion,
-//                   acc += increments                                     (no LDS)
-// Same DAG as the oracle (dif_rec/dit_rec stage 0 = top, stages 1-3 = WaveFft<1024> with
-// tstride 16), so the outputs stay bit-exact.  Scratch per ciphertext: acc + T (1.5 MiB at 4_4).
+//                   polynomial's sub-block, publish to LDS; wave c: MAC with GGSW sub-block q of
+//                   column c, inverse sub-FFT -> T[ct][lvl 1][row c][q-block]
+//   large_top_inv : per (ct, column, butterfly a): top DIT radix-R, backward conversion,
+//                   acc += increments                                                  (no LDS)
+// Same DAG as the oracle (dif_rec / dit_rec stage 0 = top, stages 1-3 = WaveFft<1024> with
+// tstride R), so the outputs are bit-exact.  At N = 32768, L = 2 the grouped CMUX below replaces
+// it.  Scratch per ciphertext: acc + T.
 // ---------------------------------------------------------------------------------------
 #ifndef LARGE_TOPT
 #define LARGE_TOPT 256
-#endif
-#ifndef LARGE_FUSE_TOP
-#define LARGE_FUSE_TOP 0  // 1: CMUX i's top_inv and CMUX i+1's top_fwd as one launch (large_top_fused_kernel; A/B: slower)
-#endif
-#ifndef LARGE_FUSED_T
-#define LARGE_FUSED_T 512  // threads per fused top workgroup (one workgroup per row: 1024 / T butterflies per thread)
-#endif
-#ifndef LARGE_FUSED_WPE
-#define LARGE_FUSED_WPE 4  // waves per SIMD the fused top kernel's register budget allows
 #endif
 #ifndef LARGE_MAC_SB
 #define LARGE_MAC_SB 4  // MAC slots per scheduling region of large_sub (GGSW loads in flight)
 #endif
 constexpr int TOPT = LARGE_TOPT;  // threads per top-stage workgroup
 
-// rotate, decompose, twist and top DIF radix-16 of butterfly t of row r, CMUX i -> T
-template <int K, int L>
+// rotate, decompose, twist and top DIF radix-R of butterfly t of row r, CMUX i -> T
+template <int N, int K, int L>
 __device__ __forceinline__ void top_fwd_body(const LargePbsLaunch &a, int ct0, int i, int cl, int r, int t) {
-    static_assert(L == 1 || L == 2, "levels L and L-1 only");
+    using S = Split<N>;
+    constexpr int R = S::R, M = S::M;
+    static_assert(L >= 1 && L <= 3, "levels 1..3");
     const uint64_t *in = a.lwe_in + (size_t)(ct0 + cl) * (a.n + 1);
-    const uint32_t at = pbs_modulus_switch<15>(in[i]);
-    const bool full_odd = (at / LN) & 1;
-    const int rem = at % LN;
-    const uint64_t *acc = a.acc + ((size_t)cl * (K + 1) + r) * LN;
+    const uint32_t at = pbs_modulus_switch<S::LOGN>(in[i]);
+    const bool full_odd = (at / N) & 1;
+    const int rem = at % N;
+    const uint64_t *acc = a.acc + ((size_t)cl * (K + 1) + r) * N;
     const int beta = a.base_log;
-    const uint32_t dmask = (1u << beta) - 1;
-    cx u[16];
-    uint32_t pk[L == 2 ? 16 : 1];
+    cx u[R];
+    uint64_t pk[L > 1 ? R : 1];  // levels L-1 .. 1 of both halves as int16 fields, for the later passes
 #pragma unroll
-    for (int b = 0; b < 16; b++) {
+    for (int b = 0; b < R; b++) {
         const int j = t + 1024 * b;
-        int32_t dg[2], dl[2];
         uint64_t dd[2];  // ct1 = X^{a~} acc - acc  (polynomial_wrapping_monic_monomial_mul_and_subtract)
-        ct1_pair(acc, j, rem, full_odd, dd[0], dd[1]);
+        ct1_pair_m<M>(acc, j, rem, full_odd, dd[0], dd[1]);
+        int32_t d0[L], d1[L];
+        decompose64<L>(dd[0], beta, d0);
+        decompose64<L>(dd[1], beta, d1);
+        if constexpr (L > 1) {
+            uint64_t w = 0;
 #pragma unroll
-        for (int half = 0; half < 2; half++) {
-            const uint64_t d = dd[half];
-            uint32_t st = decomp_state32_hi<L>((uint32_t)(d >> 32), beta);
-            dg[half] = decomp_digit32(st, beta, dmask);               // level L
-            dl[half] = L == 2 ? decomp_digit32(st, beta, dmask) : 0;  // level L-1
+            for (int l = 1; l < L; l++)
+                w |= ((uint64_t)((uint32_t)d0[l] & 0xffffu) << (32 * (l - 1))) |
+                     ((uint64_t)((uint32_t)d1[l] & 0xffffu) << (32 * (l - 1) + 16));
+            pk[b] = w;
         }
-        if constexpr (L == 2) pk[b] = ((uint32_t)dl[0] & 0xffffu) | ((uint32_t)dl[1] << 16);
         const cx tw = gld(a.twist + j);
-        u[b] = cmulw(cx{(double)dg[0], (double)dg[1]}, tw.re, tw.im);
+        u[b] = cmulw(cx{(double)d0[0], (double)d1[0]}, tw.re, tw.im);
     }
     auto top_and_store = [&](int lvl) {
-        dft16_fwd(u);
-        double2 *T = a.spectra + (((size_t)cl * L + (lvl - 1)) * (K + 1) + r) * LM + t;
+        dftR_fwd<R>(u);
+        double2 *T = a.spectra + (((size_t)cl * L + (lvl - 1)) * (K + 1) + r) * M + t;
         T[0] = make_double2(u[0].re, u[0].im);
 #pragma unroll
-        for (int c = 1; c < 16; c++) {
+        for (int c = 1; c < R; c++) {
             const cx w = gld(a.wtop + (c - 1) * 1024 + t);  // = W[t c]
             const cx y = cmulw(u[c], w.re, w.im);
             T[1024 * c] = make_double2(y.re, y.im);
         }
     };
     top_and_store(L);
-    if constexpr (L == 2) {
 #pragma unroll
-        for (int b = 0; b < 16; b++) {
-            const int32_t d0 = (int32_t)(int16_t)(pk[b] & 0xffffu), d1 = (int32_t)pk[b] >> 16;
+    for (int l = 1; l < L; l++) {
+#pragma unroll
+        for (int b = 0; b < R; b++) {
+            const int32_t e0 = (int32_t)(int16_t)((pk[b] >> (32 * (l - 1))) & 0xffffu);
+            const int32_t e1 = (int32_t)(int16_t)((pk[b] >> (32 * (l - 1) + 16)) & 0xffffu);
             const cx tw = gld(a.twist + t + 1024 * b);
-            u[b] = cmulw(cx{(double)d0, (double)d1}, tw.re, tw.im);
+            u[b] = cmulw(cx{(double)e0, (double)e1}, tw.re, tw.im);
         }
-        top_and_store(L - 1);
+        top_and_store(L - l);
     }
 }
 
-template <int K, int L>
+template <int N, int K, int L>
 __global__ void __launch_bounds__(TOPT, 4) large_top_fwd_kernel(LargePbsLaunch a, int ct0, int i) {
     constexpr int BPP = 1024 / TOPT;  // workgroups per polynomial
     // XCD-aware: workgroup w runs on XCD w % 8; all (K+1) BPP workgroups of a ciphertext share
@@ -241,10 +306,10 @@ __global__ void __launch_bounds__(TOPT, 4) large_top_fwd_kernel(LargePbsLaunch a
     const int sub = m % ((K + 1) * BPP);
     const int cl = x + 8 * (m / ((K + 1) * BPP));
     if (cl >= a.chunk_count) return;  // whole workgroup
-    top_fwd_body<K, L>(a, ct0, i, cl, sub / BPP, (sub % BPP) * TOPT + threadIdx.x);
+    top_fwd_body<N, K, L>(a, ct0, i, cl, sub / BPP, (sub % BPP) * TOPT + threadIdx.x);
 }
 
-// (k+1) L waves; LDS: sub-block twiddle table + one 1024-entry buffer per wave
+// (k+1) L waves; LDS: one 1024-entry buffer per wave + the sub-block twiddle table
 template <int K, int L>
 struct LargeSubCfg {
     static constexpr int WAVES = (K + 1) * L;
@@ -253,29 +318,43 @@ struct LargeSubCfg {
     static constexpr size_t LDS = sizeof(double2) * (S1 + SubFft::Lds::s1_len);
 };
 
-template <int K, int L>
+// workgroup -> (sub-block q, chunk ciphertext cl): at R >= 8 consecutive workgroups land on
+// consecutive XCDs (8), so XCD x only ever sees sub-blocks q = x (mod 8) -- their GGSW slices stay
+// in its L2
+template <int R>
+__device__ __forceinline__ void sub_block_of(int b, int &q, int &cl) {
+    if constexpr (R >= 8) {
+        const int x = b & 7, y = b >> 3;
+        q = x + 8 * (y % (R / 8));
+        cl = y / (R / 8);
+    } else {
+        q = b % R;
+        cl = b / R;
+    }
+}
+
+template <int N, int K, int L>
 __global__ void __launch_bounds__((LargeSubCfg<K, L>::THREADS), 2) large_sub_kernel(LargePbsLaunch a, int ct0, int i) {
     using Cfg = LargeSubCfg<K, L>;
+    using S = Split<N>;
+    constexpr int M = S::M, R = S::R;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double2 *lds = reinterpret_cast<double2 *>(smem);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // XCD-aware: consecutive workgroups land on consecutive XCDs (8), so XCD x only ever sees
-    // sub-blocks q = x and x + 8 -- their GGSW slices (2 x 128 KiB at 4_4) stay in its L2
-    const int x = blockIdx.x & 7, y = blockIdx.x >> 3;
-    const int q = x + 8 * (y & 1);
-    const int cl = y >> 1;
+    int q, cl;
+    sub_block_of<R>(blockIdx.x, q, cl);
     double2 *s1 = lds + Cfg::S1;
-    // sub-block stage twiddles W_1024[lane c] = W_M[16 lane c]  (oracle dif_rec tstride 16)
-    for (int e = threadIdx.x; e < SubFft::Lds::s1_len; e += Cfg::THREADS) s1[e] = a.W[16 * (e & 63) * ((e >> 6) + 1)];
+    // sub-block stage twiddles W_1024[lane c] = W_M[R lane c]  (oracle dif_rec tstride R)
+    for (int e = threadIdx.x; e < SubFft::Lds::s1_len; e += Cfg::THREADS) s1[e] = a.W[R * (e & 63) * ((e >> 6) + 1)];
     const SubFft::Lds tw{s1, s1};
     cx *xb = reinterpret_cast<cx *>(lds) + wave * SubFft::XL;
     WaveLocalSync wsync;
     // this wave's poly (lvl - 1) (K+1) + r, sub-block q, natural layout
-    double2 *T = a.spectra + (size_t)cl * L * (K + 1) * LM;
+    double2 *T = a.spectra + (size_t)cl * L * (K + 1) * M;
     cx v[16];
     {
-        const double2 *src = T + (size_t)wave * LM + 1024 * q + lane;
+        const double2 *src = T + (size_t)wave * M + 1024 * q + lane;
 #pragma unroll
         for (int b = 0; b < 16; b++) v[b] = gld(src + 64 * b);
     }
@@ -288,7 +367,7 @@ __global__ void __launch_bounds__((LargeSubCfg<K, L>::THREADS), 2) large_sub_ker
     const bool mac = wave <= K;  // wave c computes output column c
     if (mac) {
         // column c: sum over levels L..1 and rows 0..k (ggsw.rs:524-567), oracle order
-        const double2 *G = a.fbsk + (size_t)i * L * (K + 1) * (K + 1) * LM + (size_t)wave * LM + 1024 * q + lane;
+        const double2 *G = a.fbsk + (size_t)i * L * (K + 1) * (K + 1) * M + (size_t)wave * M + 1024 * q + lane;
 #pragma unroll
         for (int s = 0; s < 16; s++) {
             if (s % LARGE_MAC_SB == 0) __builtin_amdgcn_sched_barrier(0);  // bound loads in flight
@@ -298,7 +377,7 @@ __global__ void __launch_bounds__((LargeSubCfg<K, L>::THREADS), 2) large_sub_ker
 #pragma unroll
                 for (int r = 0; r <= K; r++) {
                     const int p = (lvl - 1) * (K + 1) + r;
-                    const double2 gg = G[(size_t)p * (K + 1) * LM + s * 64];
+                    const double2 gg = G[(size_t)p * (K + 1) * M + s * 64];
                     const double2 ff = reinterpret_cast<const double2 *>(lds)[p * SubFft::XL + s * 64 + lane];
                     if (lvl == L && r == 0) {
                         o.re = fma(gg.x, ff.x, -(gg.y * ff.y));
@@ -315,7 +394,7 @@ __global__ void __launch_bounds__((LargeSubCfg<K, L>::THREADS), 2) large_sub_ker
     __syncthreads();  // every column's MAC has read the published spectra
     if (!mac) return;
     SubFft::inverse(v, xb, tw, lane, wsync);
-    double2 *dst = T + (size_t)wave * LM + 1024 * q + lane;  // (lvl 1, row c) slot: read by this WG only
+    double2 *dst = T + (size_t)wave * M + 1024 * q + lane;  // (lvl 1, row c) slot: read by this WG only
 #pragma unroll
     for (int b = 0; b < 16; b++) dst[64 * b] = make_double2(v[b].re, v[b].im);
 }
@@ -692,22 +771,24 @@ __global__ void __launch_bounds__(GroupCfg::THREADS, 2) large_group_cmux_kernel(
     }
 }
 
-// top DIT radix-16 of butterfly t of column col, backward conversion, acc += increments
-template <int K>
+// top DIT radix-R of butterfly t of column col, backward conversion, acc += increments
+template <int N, int K>
 __device__ __forceinline__ void top_inv_body(const LargePbsLaunch &a, int cl, int col, int t) {
-    const double2 *U = a.spectra + ((size_t)cl * a.levels * (K + 1) + col) * LM + t;
-    cx u[16];
+    using S = Split<N>;
+    constexpr int R = S::R, M = S::M;
+    const double2 *U = a.spectra + ((size_t)cl * a.levels * (K + 1) + col) * M + t;
+    cx u[R];
     u[0] = gld(U);
 #pragma unroll
-    for (int c = 1; c < 16; c++) {
+    for (int c = 1; c < R; c++) {
         const cx w = gld(a.wtop + (c - 1) * 1024 + t);  // = W[t c]
         u[c] = cmulw(gld(U + 1024 * c), w.re, -w.im);
     }
-    dft16_inv(u);
-    uint64_t *acc = a.acc + ((size_t)cl * (K + 1) + col) * LN;
+    dftR_inv<R>(u);
+    uint64_t *acc = a.acc + ((size_t)cl * (K + 1) + col) * N;
     const double k32 = torus_k32();
 #pragma unroll
-    for (int b = 0; b < 16; b++) {
+    for (int b = 0; b < R; b++) {
         const int j = t + 1024 * b;
         const cx w = gld(a.twist + j);
         acc_pair pr = *reinterpret_cast<const acc_pair *>(acc + 2 * j);
@@ -719,50 +800,33 @@ __device__ __forceinline__ void top_inv_body(const LargePbsLaunch &a, int cl, in
     }
 }
 
-template <int K>
+template <int N, int K>
 __global__ void __launch_bounds__(TOPT) large_top_inv_kernel(LargePbsLaunch a, int ct0, int i) {
     constexpr int BPP = 1024 / TOPT;
     const int col = (blockIdx.x / BPP) % (K + 1);
-    top_inv_body<K>(a, blockIdx.x / (BPP * (K + 1)), col, (blockIdx.x % BPP) * TOPT + threadIdx.x);
-}
-
-// CMUX i's top inverse stage fused with CMUX i+1's top forward stage (LARGE_FUSE_TOP=1): one
-// workgroup per (ciphertext, row r) owns all 1024 butterflies of the row, so after its inverse half
-// (acc row r updated in place) and a workgroup barrier, the rotated gather of the forward half
-// reads the row that this workgroup has just written instead of re-reading it from the Infinity
-// Cache in a separate launch.  Column c of the inverse is row c of the next CMUX.  Bit-exact, but
-// measured slower (4_4 KS+PBS: 961/s separate, 778/s at 512 threads, 549/s at 256): a whole-row
-// workgroup leaves 256 workgroups per chunk of 128, one per CU, where the separate kernels run
-// 1024 -- the gather saving does not pay for the lost memory-level parallelism.
-template <int K, int L>
-__global__ void __launch_bounds__(LARGE_FUSED_T, LARGE_FUSED_WPE) large_top_fused_kernel(LargePbsLaunch a, int ct0, int i) {
-    constexpr int BPT = 1024 / LARGE_FUSED_T;  // butterflies per thread
-    const int r = blockIdx.x % (K + 1), cl = blockIdx.x / (K + 1);
-#pragma unroll 1
-    for (int h = 0; h < BPT; h++) top_inv_body<K>(a, cl, r, threadIdx.x + h * LARGE_FUSED_T);
-    __syncthreads();  // workgroup-scope release/acquire: the row's new values are visible to every wave
-#pragma unroll 1
-    for (int h = 0; h < BPT; h++) top_fwd_body<K, L>(a, ct0, i + 1, cl, r, threadIdx.x + h * LARGE_FUSED_T);
+    top_inv_body<N, K>(a, blockIdx.x / (BPP * (K + 1)), col, (blockIdx.x % BPP) * TOPT + threadIdx.x);
 }
 
 // sample extract at degree 0 (glwe_sample_extraction.rs:91-147)
-template <int K>
+template <int N, int K>
 __global__ void __launch_bounds__(256) large_extract_kernel(LargePbsLaunch a, int ct0, int cnt) {
-    const size_t per = (size_t)K * LN + 1;
+    using S = Split<N>;
+    const size_t per = (size_t)K * N + 1;
     const size_t e = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= per * cnt) return;
     const int cl = (int)(e / per);
     const size_t q = e % per;
-    const uint64_t *acc = a.acc + (size_t)cl * (K + 1) * LN;
+    const uint64_t *acc = a.acc + (size_t)cl * (K + 1) * N;
     uint64_t v;
-    if (q == (size_t)K * LN) {
-        v = acc[(size_t)K * LN];  // accx(0) = 0
+    if (q == (size_t)K * N) {
+        v = acc[(size_t)K * N];  // accx(0) = 0
     } else {
-        const int p = (int)(q / LN), j = (int)(q % LN);
-        v = j == 0 ? acc[(size_t)p * LN] : 0 - acc[(size_t)p * LN + accx(LN - j)];
+        const int p = (int)(q / N), j = (int)(q % N);
+        v = j == 0 ? acc[(size_t)p * N] : 0 - acc[(size_t)p * N + accx_m<S::M>(N - j)];
     }
     a.lwe_out[(size_t)(ct0 + cl) * per + q] = v;
 }
+
 
 // standard -> Fourier BSK at N = 32768 (forward_as_torus, fft/mod.rs:197-218): one workgroup per poly
 __global__ void __launch_bounds__(LT) large_bsk_to_fourier_kernel(const uint64_t *__restrict__ polys,
@@ -792,33 +856,98 @@ __global__ void __launch_bounds__(LT) large_bsk_to_fourier_kernel(const uint64_t
         for (int s = 0; s < 16; s++) o[spec_off(c.wave, h, s, c.lane)] = make_double2(u[h][s].re, u[h][s].im);
 }
 
-bool large_pbs_supported(int N, int k, int L) { return N == LN && k == 1 && (L == 1 || L == 2); }
+// standard -> Fourier BSK at N = 4096 ... 16384 (forward_as_torus, fft/mod.rs:197-218), in place in
+// two launches: the top DIF radix-R of every polynomial into the natural sub-block order, then the
+// 1024-point WaveFft of each sub-block (one wave each, read whole before it is overwritten in the
+// engine layout: element (q 16 + s) 64 + lane = position 1024 q + 64 (lane & 15) + 16 (lane >> 4) + s)
+template <int N>
+__global__ void __launch_bounds__(256) mid_bsk_top_kernel(const uint64_t *__restrict__ polys, double2 *__restrict__ out,
+                                                          const double2 *__restrict__ wtop,
+                                                          const double2 *__restrict__ twist, size_t npoly) {
+    using S = Split<N>;
+    constexpr int R = S::R, M = S::M;
+    const size_t e = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= npoly * 1024) return;
+    const size_t poly = e / 1024;
+    const int t = (int)(e % 1024);
+    const uint64_t *x = polys + poly * N;
+    cx u[R];
+#pragma unroll
+    for (int b = 0; b < R; b++) {
+        const int j = t + 1024 * b;
+        const double xr = (double)(int64_t)x[j] * fourier_key_scale(M);
+        const double xi = (double)(int64_t)x[j + M] * fourier_key_scale(M);
+        const cx w = gld(twist + j);
+        u[b].re = xr * w.re - xi * w.im;
+        u[b].im = xr * w.im + xi * w.re;
+    }
+    dftR_fwd<R>(u);
+    double2 *o = out + poly * M + t;
+    o[0] = make_double2(u[0].re, u[0].im);
+#pragma unroll
+    for (int c = 1; c < R; c++) {
+        const cx w = gld(wtop + (c - 1) * 1024 + t);  // = W[t c]
+        const cx y = cmulw(u[c], w.re, w.im);
+        o[1024 * c] = make_double2(y.re, y.im);
+    }
+}
+
+template <int N>
+__global__ void __launch_bounds__(256) mid_bsk_sub_kernel(double2 *__restrict__ out, const double2 *__restrict__ W,
+                                                          size_t nblocks) {
+    constexpr int R = Split<N>::R;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double2 *lds = reinterpret_cast<double2 *>(smem);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    double2 *s1 = lds + 4 * SubFft::XL;
+    for (int e = threadIdx.x; e < SubFft::Lds::s1_len; e += 256) s1[e] = W[R * (e & 63) * ((e >> 6) + 1)];
+    __syncthreads();
+    const size_t blk = (size_t)blockIdx.x * 4 + wave;  // (poly, q) = sub-block blk of the key
+    if (blk >= nblocks) return;
+    const SubFft::Lds tw{s1, s1};
+    cx *xb = reinterpret_cast<cx *>(lds) + wave * SubFft::XL;
+    WaveLocalSync wsync;
+    double2 *o = out + blk * 1024;
+    cx v[16];
+#pragma unroll
+    for (int b = 0; b < 16; b++) v[b] = gld(o + lane + 64 * b);
+    SubFft::forward(v, xb, tw, lane, wsync);
+#pragma unroll
+    for (int sl = 0; sl < 16; sl++) o[sl * 64 + lane] = make_double2(v[sl].re, v[sl].im);
+}
+
+bool large_pbs_supported(int N, int k, int L) {
+    return (N == 4096 || N == 8192 || N == 16384 || N == 32768) && k == 1 && L >= 1 && L <= 3;
+}
 
 size_t large_pbs_scratch_per_ct(int N, int k, int L) {
     return (size_t)(k + 1) * N * sizeof(uint64_t) + (size_t)L * (k + 1) * (N / 2) * sizeof(double2);
 }
 
-template <int K, int L>
+template <int N, int K, int L>
 static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
+    using S = Split<N>;
     if (a0.count == 0) return hipSuccess;
-    const size_t per_ct = large_pbs_scratch_per_ct(LN, K, L);
+    const size_t per_ct = large_pbs_scratch_per_ct(N, K, L);
     const int chunk = (int)std::min<size_t>((size_t)a0.count, a0.scratch_bytes / per_ct);
     if (chunk <= 0) return hipErrorInvalidValue;
     LargePbsLaunch a = a0;
     a.levels = L;
     a.acc = reinterpret_cast<uint64_t *>(a0.scratch);
     a.spectra = reinterpret_cast<double2 *>(reinterpret_cast<char *>(a0.scratch) +
-                                            (size_t)chunk * (K + 1) * LN * sizeof(uint64_t));
+                                            (size_t)chunk * (K + 1) * N * sizeof(uint64_t));
     for (int ct0 = 0; ct0 < a.count; ct0 += chunk) {
         const int cnt = std::min(chunk, a.count - ct0);
         a.chunk_count = cnt;
-        const size_t init_elems = (size_t)cnt * (K + 1) * LN;
-        hipLaunchKernelGGL(large_init_kernel<K>, dim3((unsigned)((init_elems + 255) / 256)), dim3(256), 0, s, a,
+        const size_t init_elems = (size_t)cnt * (K + 1) * N;
+        hipLaunchKernelGGL((large_init_kernel<N, K>), dim3((unsigned)((init_elems + 255) / 256)), dim3(256), 0, s, a,
                            ct0, cnt);
         using Sub = LargeSubCfg<K, L>;
         const unsigned top_blocks = (unsigned)cnt * (K + 1) * (1024 / TOPT);
         const unsigned fwd_blocks = (unsigned)((cnt + 7) / 8) * 8 * (K + 1) * (1024 / TOPT);
-        if constexpr (K == 1 && L == 2) {
+        const size_t out_elems = (size_t)cnt * (K * N + 1);
+        if constexpr (N == LN && K == 1 && L == 2) {
             if (LARGE_GROUP_SUB) {
                 const unsigned grp_blocks = (unsigned)((cnt + 7) / 8) * 8 * 4 * GroupCfg::PARTS;
                 const unsigned dig_blocks = (unsigned)((cnt + 7) / 8) * 8 * (LM / LARGE_DIGT);
@@ -833,44 +962,71 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
                                            GroupCfg::LDS, s, a, ct0, i);
                     }
                     TimedLaunch tl(a.timer, "large_top_inv_kernel", s);
-                    hipLaunchKernelGGL((large_top_inv_kernel<K>), dim3(top_blocks), dim3(TOPT), 0, s, a, ct0, i);
+                    hipLaunchKernelGGL((large_top_inv_kernel<N, K>), dim3(top_blocks), dim3(TOPT), 0, s, a, ct0, i);
                 }
-                const size_t out_elems = (size_t)cnt * (K * LN + 1);
-                hipLaunchKernelGGL(large_extract_kernel<K>, dim3((unsigned)((out_elems + 255) / 256)), dim3(256), 0,
-                                   s, a, ct0, cnt);
+                hipLaunchKernelGGL((large_extract_kernel<N, K>), dim3((unsigned)((out_elems + 255) / 256)), dim3(256),
+                                   0, s, a, ct0, cnt);
                 continue;
             }
         }
-        if (a.n > 0)
-            hipLaunchKernelGGL((large_top_fwd_kernel<K, L>), dim3(fwd_blocks), dim3(TOPT), 0, s, a, ct0, 0);
+        const unsigned sub_blocks = (unsigned)cnt * S::R;
         for (int i = 0; i < a.n; i++) {
-            hipLaunchKernelGGL((large_sub_kernel<K, L>), dim3((unsigned)cnt * 16), dim3(Sub::THREADS), Sub::LDS, s, a,
-                               ct0, i);
-            if (LARGE_FUSE_TOP && i + 1 < a.n) {
-                hipLaunchKernelGGL((large_top_fused_kernel<K, L>), dim3((unsigned)cnt * (K + 1)), dim3(LARGE_FUSED_T), 0, s, a,
-                                   ct0, i);
-            } else {
-                hipLaunchKernelGGL((large_top_inv_kernel<K>), dim3(top_blocks), dim3(TOPT), 0, s, a, ct0, i);
-                if (i + 1 < a.n)
-                    hipLaunchKernelGGL((large_top_fwd_kernel<K, L>), dim3(fwd_blocks), dim3(TOPT), 0, s, a, ct0, i + 1);
+            {
+                TimedLaunch tl(a.timer, "large_top_fwd_kernel", s);
+                hipLaunchKernelGGL((large_top_fwd_kernel<N, K, L>), dim3(fwd_blocks), dim3(TOPT), 0, s, a, ct0, i);
             }
+            {
+                TimedLaunch tl(a.timer, "large_sub_kernel", s);
+                hipLaunchKernelGGL((large_sub_kernel<N, K, L>), dim3(sub_blocks), dim3(Sub::THREADS), Sub::LDS, s, a,
+                                   ct0, i);
+            }
+            TimedLaunch tl(a.timer, "large_top_inv_kernel", s);
+            hipLaunchKernelGGL((large_top_inv_kernel<N, K>), dim3(top_blocks), dim3(TOPT), 0, s, a, ct0, i);
         }
-        const size_t out_elems = (size_t)cnt * (K * LN + 1);
-        hipLaunchKernelGGL(large_extract_kernel<K>, dim3((unsigned)((out_elems + 255) / 256)), dim3(256), 0, s, a,
+        hipLaunchKernelGGL((large_extract_kernel<N, K>), dim3((unsigned)((out_elems + 255) / 256)), dim3(256), 0, s, a,
                            ct0, cnt);
     }
     return hipGetLastError();
 }
 
+template <int N>
+static hipError_t launch_large_n(int L, const LargePbsLaunch &a, hipStream_t s) {
+    switch (L) {
+        case 1: return launch_large_t<N, 1, 1>(a, s);
+        case 2: return launch_large_t<N, 1, 2>(a, s);
+        case 3: return launch_large_t<N, 1, 3>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 hipError_t launch_large_pbs(int N, int k, int L, const LargePbsLaunch &a, hipStream_t s) {
-    if (N == LN && k == 1 && L == 2) return launch_large_t<1, 2>(a, s);
-    if (N == LN && k == 1 && L == 1) return launch_large_t<1, 1>(a, s);
-    return hipErrorInvalidValue;
+    if (!large_pbs_supported(N, k, L)) return hipErrorInvalidValue;
+    switch (N) {
+        case 4096: return launch_large_n<4096>(L, a, s);
+        case 8192: return launch_large_n<8192>(L, a, s);
+        case 16384: return launch_large_n<16384>(L, a, s);
+        default: return launch_large_n<32768>(L, a, s);
+    }
+}
+
+template <int N>
+static hipError_t launch_mid_bsk(const uint64_t *std_polys, double2 *fourier, size_t npoly, const FftTables &t,
+                                 hipStream_t s) {
+    hipLaunchKernelGGL((mid_bsk_top_kernel<N>), dim3((unsigned)((npoly * 1024 + 255) / 256)), dim3(256), 0, s,
+                       std_polys, fourier, t.wtop, t.twist, npoly);
+    const size_t nblocks = npoly * Split<N>::R;
+    const size_t lds = sizeof(double2) * (4 * SubFft::XL + SubFft::Lds::s1_len);
+    hipLaunchKernelGGL((mid_bsk_sub_kernel<N>), dim3((unsigned)((nblocks + 3) / 4)), dim3(256), lds, s, fourier, t.W,
+                       nblocks);
+    return hipGetLastError();
 }
 
 hipError_t launch_large_bsk_to_fourier(const uint64_t *std_polys, double2 *fourier, size_t npoly,
                                        const FftTables &t, hipStream_t s) {
     if (npoly == 0) return hipSuccess;
+    if (t.N == 4096) return launch_mid_bsk<4096>(std_polys, fourier, npoly, t, s);
+    if (t.N == 8192) return launch_mid_bsk<8192>(std_polys, fourier, npoly, t, s);
+    if (t.N == 16384) return launch_mid_bsk<16384>(std_polys, fourier, npoly, t, s);
     hipLaunchKernelGGL(large_bsk_to_fourier_kernel, dim3((unsigned)npoly), dim3(LT), LARGE_LDS, s, std_polys,
                        fourier, t.W, t.wtop, t.twist);
     return hipGetLastError();
