@@ -76,3 +76,43 @@ def test_device_conversion_exact_on_gpu():
     bad = np.nonzero(got != exp)[0]
     assert bad.size == 0, [(float(fr[i]).hex(), hex(int(got[i])), hex(int(exp[i]))) for i in bad[:5]]
     assert np.array_equal(acc, acc0 + exp)  # wrapping u64 add
+
+
+def _scalar_backward(z: complex, n: int):
+    """convert_add_backward_torus_scalar (fft/mod.rs:284-302) into zeroed outputs: tmp = inp *
+    (conj(w) * (1/n)) as plain c64 arithmetic, then from_torus (commons/math/torus/mod.rs:72-78):
+    fract = x - round(x) (half away from zero), * 2^64, round, as i64 as u64."""
+    j = np.arange(n)
+    wr, wi = np.cos(j * (np.pi / (2.0 * n))), np.sin(j * (np.pi / (2.0 * n)))
+    norm = 1.0 / n
+    c, d = wr * norm, -wi * norm
+    re = z.real * c - z.imag * d
+    im = z.real * d + z.imag * c
+
+    def from_torus(x):
+        fract = x - np.where(x >= 0, np.floor(x + 0.5), np.ceil(x - 0.5))
+        fract = fract * 2.0 ** 64
+        r = np.where(fract >= 0, np.floor(fract + 0.5), np.ceil(fract - 0.5))
+        return [int(v) % 2 ** 64 for v in r]
+
+    return from_torus(re), from_torus(im), wr, wi
+
+
+def test_fma_backward_within_reference_simd_bound_of_scalar():
+    """x86.rs:1200-1235 (add_backward_torus_v3): the AVX2/FMA backward conversion -- the form the
+    oracle and every PBS kernel compute (ws = w/M, fma products, fract = m - rint(m),
+    rint_half_even(fract 2^64)) -- stays within 2^38 of the reference's scalar path on the
+    reference's own input (z = -34384521907.303154 + 19013399110.689323 i, n = 1024)."""
+    n = 1024
+    z = complex(-34384521907.303154, 19013399110.689323)
+    s_re, s_im, wr, wi = _scalar_backward(z, n)
+    zr, zi = Fraction(z.real), Fraction(z.imag)
+    for j in range(n):
+        wsr, wsi = float(Fraction(wr[j]) / n), float(Fraction(wi[j]) / n)   # w / M: exact (power of two)
+        mr = float(zr * Fraction(wsr) + Fraction(float(zi * Fraction(wsi))))  # fma(zr, wsr, zi*wsi)
+        mi = float(-zr * Fraction(wsi) + Fraction(float(zi * Fraction(wsr))))  # fma(-zr, wsi, zi*wsr)
+        for m, s in ((mr, s_re[j]), (mi, s_im[j])):
+            fr = m - float(round(Fraction(m)))          # rint: half to even
+            v = exact_x(fr)
+            diff = (v - s) % 2 ** 64
+            assert min(diff, 2 ** 64 - diff) < 2 ** 38, (j, v, s)
