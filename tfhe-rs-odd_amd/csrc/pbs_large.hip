@@ -297,8 +297,13 @@ __device__ __forceinline__ void top_fwd_body(const LargePbsLaunch &a, int ct0, i
     }
 }
 
+// waves per SIMD the top stage's register budget allows: 4 (128 VGPRs) except the radix-16 stage
+// with one or three levels, which spills at 128 (the compiler keeps more of it live)
+template <int N, int L>
+constexpr int top_fwd_wpe() { return Split<N>::R == 16 && L != 2 ? 2 : 4; }
+
 template <int N, int K, int L>
-__global__ void __launch_bounds__(TOPT, 4) large_top_fwd_kernel(LargePbsLaunch a, int ct0, int i) {
+__global__ void __launch_bounds__(TOPT, (top_fwd_wpe<N, L>())) large_top_fwd_kernel(LargePbsLaunch a, int ct0, int i) {
     constexpr int BPP = 1024 / TOPT;  // workgroups per polynomial
     // XCD-aware: workgroup w runs on XCD w % 8; all (K+1) BPP workgroups of a ciphertext share
     // one XCD, so the rotated gather re-reads the accumulator rows from that XCD's L2
