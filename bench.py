@@ -808,45 +808,44 @@ def host_abi_rate(eng, P, cts, acc, with_ks: bool, reps: int = 3) -> dict:
 def single_ct_rates(eng, cts, acc, with_ks: bool, batched_rate: float, secs: float = 2.0) -> dict:
     """The reference's own calling pattern through the synchronous host-pointer ABI: ONE ciphertext
     per call (keyswitch_programmable_bootstrap_assign, shortint/server_key/mod.rs:783-857), from T
-    concurrent caller threads (rayon workers, radix_parallel/mul.rs:347-407).  The engine coalesces
-    concurrent small calls into batches (capi.cpp "request coalescing").  Reports the single-call
-    latency with one caller and the ciphertexts per second reached by 16 and 64 closed-loop callers
-    (each issues its next call when the previous returns), against the batched device rate."""
-    import threading
+    native threads at once (rayon workers, radix_parallel/mul.rs:347-407), each issuing its next
+    call when the previous returns (lib/libtfhe_mi355_loadgen.so: std::threads, no GIL).  The
+    engine coalesces concurrent small calls into batches.  Every output is compared
+    with the same ciphertext's row from one batched call.  By Little's law T callers cannot exceed
+    T / latency (`little_bound`)."""
+    import ctypes
 
+    from tfhe_mi355 import _lib
+
+    lg = ctypes.CDLL(os.path.join(ROOT, "tfhe-rs-odd_amd", "lib", "libtfhe_mi355_loadgen.so"))
+    lg.tfhe_mi355_loadgen_run.restype = ctypes.c_int
+    n_in = min(cts.shape[0], 1024)
+    x = np.ascontiguousarray(cts[:n_in])
     f = eng.keyswitch_programmable_bootstrap if with_ks else eng.programmable_bootstrap
-    f(cts[:1], acc)
-    lat = []
-    for i in range(10):
-        t = time.perf_counter()
-        f(cts[i:i + 1], acc)
-        lat.append(time.perf_counter() - t)
+    exp = f(x, acc)   # one batched call: the expected rows
+    a = np.ascontiguousarray(acc, dtype=np.uint64)
+    u64p = ctypes.POINTER(ctypes.c_uint64)
     res = {"entry_point": ("tfhe_mi355_keyswitch_programmable_bootstrap" if with_ks
-                           else "tfhe_mi355_programmable_bootstrap"),
-           "single_call_latency_ms": 1e3 * float(np.median(lat)), "callers": {}}
-    for T in (16, 64):
-        done = [0] * T
-        stop = time.perf_counter() + secs
-
-        def worker(t):
-            i = t
-            while time.perf_counter() < stop:
-                f(cts[i % cts.shape[0]:i % cts.shape[0] + 1], acc)
-                done[t] += 1
-                i += T
-
-        ths = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
-        t0 = time.perf_counter()
-        for th in ths:
-            th.start()
-        for th in ths:
-            th.join()
-        wall = time.perf_counter() - t0
-        rate = sum(done) / wall
+                           else "tfhe_mi355_programmable_bootstrap"), "callers": {}}
+    for T in (1, 16, 64, 256):
+        calls, bad, fails = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        wall, lat = ctypes.c_double(), ctypes.c_double()
+        rc = lg.tfhe_mi355_loadgen_run(
+            eng._h, ctypes.c_int(1 if with_ks else 0), x.ctypes.data_as(u64p), ctypes.c_size_t(x.shape[1]),
+            ctypes.c_size_t(n_in), exp.ctypes.data_as(u64p), ctypes.c_size_t(exp.shape[1]), a.ctypes.data_as(u64p),
+            ctypes.c_int(T), ctypes.c_double(secs if T > 1 else secs / 2), ctypes.byref(calls), ctypes.byref(wall),
+            ctypes.byref(lat), ctypes.byref(bad), ctypes.byref(fails))
+        if rc != 0:
+            raise _lib.EngineError("loadgen failed")
+        rate = calls.value / wall.value
         res["callers"][str(T)] = {"value": rate, "frac_of_batched_device_rate": rate / batched_rate,
-                                  "little_bound": T / (res["single_call_latency_ms"] * 1e-3)}
-    res["note"] = ("closed-loop callers, count = 1 per call; by Little's law T callers cannot exceed T / latency "
-                   "(little_bound); the batched device rate is the headline step's")
+                                  "mean_call_latency_ms": lat.value * 1e3,
+                                  "little_bound": T / lat.value if lat.value else None,
+                                  "calls": calls.value, "mismatching_rows": bad.value, "failed_calls": fails.value}
+    res["single_call_latency_ms"] = res["callers"]["1"]["mean_call_latency_ms"]
+    res["note"] = ("T native threads (libtfhe_mi355_loadgen), closed loop, count = 1 per call, every output "
+                   "compared with a batched call's row; T callers cannot exceed T / latency (little_bound); "
+                   "the batched device rate is the headline step's")
     return res
 
 

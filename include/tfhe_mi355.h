@@ -21,10 +21,14 @@
  *     and return immediately; the others take HOST pointers and return after the outputs are
  *     written (synchronous).  The host-pointer forms pipeline the batch in chunks through
  *     page-locked staging on two streams (copies of one chunk overlap the kernels of the next);
- *   - a context is bound to one GPU; host-pointer calls on one context are serialised by an
- *     internal mutex, so rayon-style concurrent callers sharing a key are safe (SURVEY.md 8b
- *     "Threading").  The _async calls hold no per-context mutable state: every device scratch
- *     buffer they need comes from the caller (d_scratch, sized by the matching *_scratch query;
+ *   - a context is bound to one GPU; host-pointer calls on one context are thread-safe, so
+ *     rayon-style concurrent callers sharing a key are safe (SURVEY.md 8b "Threading"): calls of
+ *     more than 64 ciphertexts are serialised by an internal mutex, smaller concurrent calls of
+ *     the same entry point are coalesced into shared batches that run on their own streams, each
+ *     caller receiving exactly its own rows (the reference's one-ciphertext-per-call pattern,
+ *     shortint/server_key/mod.rs:783-857; TFHE_MI355_COALESCE_MAX_COUNT=0 turns it off).
+ *     The _async calls hold no per-context mutable state: every device scratch buffer they
+ *     need comes from the caller (d_scratch, sized by the matching *_scratch query;
  *     a query returning 0 means d_scratch may be NULL), so concurrent callers on different
  *     streams only need scratch buffers of their own, and the calls can be captured into a
  *     hipGraph (no allocation or synchronisation inside);

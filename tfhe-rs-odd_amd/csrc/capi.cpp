@@ -157,7 +157,7 @@ struct TfheMi355Context {
     // at a time from rayon workers: shortint/server_key/mod.rs:783-857, radix_parallel/mul.rs:
     // 347-407).  Concurrent calls of one op are queued; one caller collects the queue into a
     // batch (after a short window or when the batch is full) and runs it on one of the batch
-    // slots, each with its own stream, staging and scratch, so several batches can be in flight;
+    // slots (8), each with its own stream, staging and scratch, so several batches can be in flight;
     // every caller gets its rows back bit-identical to a call of its own.
     struct Coalescer {
         std::mutex m;
@@ -170,7 +170,7 @@ struct TfheMi355Context {
             PinnedBuffer h_in, h_out, h_luts, h_idx;
             DeviceBuffer d_in, d_out, d_luts, d_idx, d_scratch;
             bool busy = false;
-        } slots[4];
+        } slots[8];
     } co;
     KernelTimer *timer_or_null() { return timer.every > 0 ? &timer : nullptr; }
 
@@ -675,6 +675,11 @@ size_t coalesce_batch() {
     static const size_t v = std::max<size_t>(env_size("TFHE_MI355_COALESCE_BATCH", 1024), 1);
     return v;
 }
+// batch slots in use (up to 8): batches in flight at once, each on its own stream
+size_t coalesce_slots() {
+    static const size_t v = std::min<size_t>(std::max<size_t>(env_size("TFHE_MI355_COALESCE_SLOTS", 8), 1), 8);
+    return v;
+}
 std::chrono::microseconds coalesce_window() {
     static const size_t v = env_size("TFHE_MI355_COALESCE_WINDOW_US", 200);
     return std::chrono::microseconds(v);
@@ -798,9 +803,9 @@ void coalesced_call(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
         co.cv.notify_all();
         TfheMi355Context::Coalescer::Slot *sl = nullptr;
         co.cv.wait(lk, [&] {
-            for (auto &x : co.slots)
-                if (!x.busy) {
-                    sl = &x;
+            for (size_t q = 0; q < coalesce_slots(); q++)
+                if (!co.slots[q].busy) {
+                    sl = &co.slots[q];
                     return true;
                 }
             return false;
