@@ -16,11 +16,14 @@ ONCE over RCCL (xGMI); each rank converts it to the Fourier domain on its own GP
 its shard -- no collective in the timed loop except the bracketing barriers.  value = sum of PBS
 over ranks / max wall time over ranks.
 
-The JSON line also carries the roofline of the dominant kernel (FP64-VALU bound for the
-N <= 2048 kernels; BSK-streaming HBM model at N = 32768 -- DESIGN.md 6), the measured HBM traffic
-from the committed rocprofv3 PMC summaries (profiles/r02_pmc_*.json), the rate of the
-host-pointer C ABI (PCIe-inclusive; never `value`) and the CPU baseline (oracle C restatement,
-1 PBS per thread on the host's CPU share, rank 0, N = 1 only).
+The JSON line also carries the roofline of the dominant kernel (FP64-VALU bound; its duration from
+the engine's per-kernel HIP-event timer on the launch stream -- DESIGN.md 6), the measured traffic
+and issue counters of that same kernel from the committed per-kernel rocprofv3 PMC summaries
+(profiles/r03_pmc_*.json), the rates of the host-pointer C ABI (PCIe-inclusive, and the
+reference's one-ciphertext-per-call pattern from native threads; never `value`) and the CPU
+baseline (oracle C restatement, 1 PBS per thread on the host's CPU share, rank 0, N = 1 only).
+The default run also measures the other BASELINE configurations (`other_workloads`), at N > 1
+on every rank of the job.
 
 `--launch-selftest` runs the rank/shard/aggregation code with a stub step on the CPU (gloo), so
 that the multi-rank path is testable without a GPU (tests/test_bench_launch.py).

@@ -31,5 +31,8 @@ for s in $STAGES; do
     kstats:*) t=${s#kstats:}; step kstats_$t 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kstats_$t -o run \
                 --output-format csv -- python3 bench.py $(kargs $t) --no-cpu-baseline --no-host-abi ;;
     pmc:*) t=${s#pmc:}; step pmc_$t 1100 bash scripts/pmc_workload.sh $t ;;
+    # two ranks sharing the box's one GPU over gloo: the multi-rank default run (every
+    # configuration merged into one line), as the driver's N-GPU run executes it
+    rehearse2) step rehearse2 900 env BENCH_DIST_BACKEND=gloo python -u bench.py --gpus 2 --steps 5 --warmup 1 ;;
   esac
 done
