@@ -164,7 +164,7 @@ def test_server_key_round_trip_and_layout():
         S.inspect_server_key(S.serialize_server_key(p.with_(lwe_dimension=4), ksk4, fb))
 
 
-@pytest.mark.parametrize("N", [2048, 32768])
+@pytest.mark.parametrize("N", [2048, 4096, 8192, 16384, 32768])
 def test_engine_frequency_matches_oracle_position_order(orc, N):
     """freq[e] = pos_freq(position of engine element e): the layout DESIGN.md 2 documents,
     against the oracle's digit-reversal map of its FFT plan."""

@@ -363,12 +363,13 @@ int tfhe_mi355_fourier_engine_frequency(uint32_t N, uint32_t *freq) {
         };
         if (N == 2048) {
             for (uint32_t e = 0; e < 1024; e++) freq[e] = f1024(e);
-        } else if (N == 32768) {
-            // element ((q 16 + s) 64 + lane): sub-block q (top DIF radix-16 output digit) of the
-            // [16 | 16, 16, 4] plan, then the 1024-point layout inside it
-            for (uint32_t e = 0; e < 16384; e++) freq[e] = (e >> 10) + 16 * f1024(e & 1023);
+        } else if (N == 4096 || N == 8192 || N == 16384 || N == 32768) {
+            // element ((q 16 + s) 64 + lane): sub-block q (top DIF radix-R output digit, R = N/2048)
+            // of the [R | 16, 16, 4] plan, then the 1024-point layout inside it
+            const uint32_t R = N / 2048;
+            for (uint32_t e = 0; e < N / 2; e++) freq[e] = (e >> 10) + R * f1024(e & 1023);
         } else {
-            fail("Fourier key ingestion supports N = 2048 and N = 32768 (got %u)", N);
+            fail("Fourier key ingestion supports N = 2048 ... 32768 (got %u)", N);
         }
     });
 }
