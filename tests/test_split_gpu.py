@@ -202,3 +202,67 @@ def test_every_shortint_parameter_set_bit_exact(orc, name):
         assert np.array_equal(out, exp), "PBS -> KS differs from the oracle"
         dec = decode(orc.lwe_decrypt(lwe_sk, out), p.delta) % space
     assert np.array_equal(dec, [f(m) for m in msgs])
+
+
+MB_SPLIT = ["PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_2_KS_PBS",   # N = 8192, L = 2, g = 2 (multi_bit.rs:134)
+            "PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_3_KS_PBS"]   # N = 8192, L = 2, g = 3 (multi_bit.rs:192)
+
+
+@pytest.mark.parametrize("name", MB_SPLIT)
+def test_split_multi_bit_pbs_bit_exact_vs_oracle(orc, name):
+    """Multi-bit PBS through the split CMUX (keybundle built inside large_sub_kernel from the
+    2^g - 1 resident GGSWs of each group): KS -> PBS bit-exact against the oracle's
+    MultiBitFourierBsk at n = 6 (both groupings divide it), per-ciphertext LUTs, edge inputs,
+    outputs decrypting to f(m)."""
+    from tfhe_mi355 import client
+    from tfhe_mi355.parameters import MULTI_BIT_ALL
+
+    p = MULTI_BIT_ALL[name].with_(lwe_dimension=6)
+    N, g, space = p.polynomial_size, p.grouping_factor, p.message_modulus * p.carry_modulus
+    lwe_sk = client.gen_binary_key(101, 1, p.lwe_dimension)
+    glwe_sk = client.gen_binary_key(101, 2, p.big_lwe_dimension)
+    bsk = client.gen_multi_bit_bootstrap_key(102, lwe_sk, glwe_sk, 1, N, p.pbs_base_log, p.pbs_level, g,
+                                             p.glwe_modular_std_dev, threads=8)
+    fb = orc.MultiBitFourierBsk(bsk, p.lwe_dimension, 1, N, p.pbs_base_log, p.pbs_level, g)
+    ksk = client.gen_keyswitch_key(103, glwe_sk, lwe_sk, p.ks_base_log, p.ks_level, p.lwe_modular_std_dev)
+    eng = _engine(p, bsk, ksk)
+    fs = [lambda x: (x + 7) % space, lambda x: (5 * x) % space]
+    luts = np.stack([orc.fill_accumulator(N, 1, p.message_modulus, p.carry_modulus, f) for f in fs])
+    msgs = np.array([0, 1, 31, 63, 40, 17])
+    idx = np.array([0, 1, 0, 1, 1, 0], dtype=np.uint32)
+    big = orc.lwe_encrypt(104, glwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta), p.glwe_modular_std_dev)
+    small = orc.keyswitch(ksk, p.big_lwe_dimension, p.lwe_dimension, p.ks_base_log, p.ks_level, big)
+    out = eng.keyswitch_programmable_bootstrap(big, luts, lut_indexes=idx)
+    exp = fb.pbs(small, luts, lut_idx=idx, threads=6)
+    bad = np.nonzero(np.any(out != exp, axis=1))[0]
+    assert bad.size == 0, f"{name}: ciphertexts {bad} differ"
+    assert np.array_equal(decode(orc.lwe_decrypt(glwe_sk, out), p.delta) % space,
+                          [fs[i](m) for i, m in zip(idx, msgs)])
+    edge = np.random.default_rng(11).integers(0, 2 ** 64, (3, p.lwe_dimension + 1), dtype=np.uint64)
+    edge[0, :-1] = 0
+    edge[1, :-1] = np.uint64(1 << 63)
+    edge[2, -1] = np.uint64((1 << 64) - 1)
+    assert np.array_equal(eng.programmable_bootstrap(edge, luts[0]), fb.pbs(edge, luts[0], threads=3))
+
+
+@pytest.mark.timeout(900)
+def test_full_multi_bit_3_3_group_3_decrypts(orc):
+    """Full PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_3_KS_PBS (n = 972, N = 8192): KS -> PBS of 64
+    ciphertexts decrypts to f(m); one ciphertext bit-exact against the oracle."""
+    from tfhe_mi355 import client
+    from tfhe_mi355.parameters import PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_3_KS_PBS as P
+
+    lwe_sk = client.gen_binary_key(111, 1, P.lwe_dimension)
+    glwe_sk = client.gen_binary_key(111, 2, P.big_lwe_dimension)
+    bsk = client.gen_multi_bit_bootstrap_key(112, lwe_sk, glwe_sk, 1, P.polynomial_size, P.pbs_base_log,
+                                             P.pbs_level, 3, P.glwe_modular_std_dev, threads=16)
+    ksk = client.gen_keyswitch_key(113, glwe_sk, lwe_sk, P.ks_base_log, P.ks_level, P.lwe_modular_std_dev)
+    eng = _engine(P, bsk, ksk)
+    msgs = np.random.default_rng(5).integers(0, 64, 64)
+    big = orc.lwe_encrypt(114, glwe_sk, msgs.astype(np.uint64) * np.uint64(P.delta), P.glwe_modular_std_dev)
+    acc = orc.fill_accumulator(P.polynomial_size, 1, 8, 8, lambda x: (x * 3 + 2) % 64)
+    out = eng.keyswitch_programmable_bootstrap(big, acc)
+    assert np.array_equal(decode(orc.lwe_decrypt(glwe_sk, out), P.delta) % 64, (msgs * 3 + 2) % 64)
+    fb = orc.MultiBitFourierBsk(bsk, P.lwe_dimension, 1, P.polynomial_size, P.pbs_base_log, P.pbs_level, 3)
+    small = orc.keyswitch(ksk, P.big_lwe_dimension, P.lwe_dimension, P.ks_base_log, P.ks_level, big[:1])
+    assert np.array_equal(out[:1], fb.pbs(small, acc, threads=1))

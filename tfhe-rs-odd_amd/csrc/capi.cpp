@@ -250,8 +250,11 @@ hipError_t convert_bsk(TfheMi355Context *c, const uint64_t *d_std, size_t npoly,
 // Every launcher takes its device scratch explicitly: the _async entry points pass the caller's
 // d_scratch (sized by the *_scratch queries), the host-pointer entry points a lane's own buffer.
 
+// the split CMUX of N >= 4096 (classic, or multi-bit at the N = 8192 sets): accumulators in scratch
 bool is_large(const TfheMi355Context *c) {
-    return !c->p.grouping_factor && large_pbs_supported((int)c->N(), (int)c->k(), (int)c->p.pbs_level);
+    if (c->p.grouping_factor)
+        return large_multibit_supported((int)c->N(), (int)c->k(), (int)c->p.pbs_level, (int)c->p.grouping_factor);
+    return large_pbs_supported((int)c->N(), (int)c->k(), (int)c->p.pbs_level);
 }
 
 // N >= 4096: ciphertexts per pass of the split CMUX.  The chunk's accumulators + spectra should
@@ -270,7 +273,7 @@ size_t large_chunk(const TfheMi355Context *c) {
 }
 
 size_t pbs_scratch_bytes(const TfheMi355Context *c, size_t count) {
-    if (count == 0 || c->p.grouping_factor) return 0;
+    if (count == 0 || (c->p.grouping_factor && !is_large(c))) return 0;
     if (!is_large(c)) return classic_pbs_ticket_bytes((int)c->N(), (int)c->k(), (int)c->p.pbs_level);
     const size_t per_ct = large_pbs_scratch_per_ct((int)c->N(), (int)c->k(), (int)c->p.pbs_level);
     return per_ct * std::min(count, large_chunk(c));
@@ -323,7 +326,7 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
     if (lut_count > 0xffffffffu) fail("lut_count too large");
     if (count > 0x7fffffff) fail("batch too large");
     if (count == 0) return;
-    if (c->p.grouping_factor) {
+    if (c->p.grouping_factor && !is_large(c)) {
         MultiBitPbsLaunch a;
         a.lwe_in = d_in;
         a.lwe_out = d_out;
@@ -364,6 +367,7 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
         a.scratch = scratch;
         a.scratch_bytes = std::min(scratch_bytes, per_ct * large_chunk(c));
         a.timer = c->timer_or_null();
+        a.grouping = (int)c->p.grouping_factor;
         check(launch_large_pbs((int)c->N(), (int)c->k(), (int)c->p.pbs_level, a, s), "launch large pbs");
         return;
     }
@@ -903,7 +907,9 @@ int tfhe_mi355_context_create(const TfheMi355Parameters *params, int device, Tfh
         if (!is_pow2(p.polynomial_size)) fail("polynomial_size must be a power of two");
         if (p.grouping_factor != 0) {
             if (!multibit_pbs_supported((int)p.polynomial_size, (int)p.glwe_dimension, (int)p.pbs_level,
-                                        (int)p.grouping_factor))
+                                        (int)p.grouping_factor) &&
+                !large_multibit_supported((int)p.polynomial_size, (int)p.glwe_dimension, (int)p.pbs_level,
+                                          (int)p.grouping_factor))
                 fail("no multi-bit kernel for N=%u k=%u pbs_level=%u grouping_factor=%u", p.polynomial_size,
                      p.glwe_dimension, p.pbs_level, p.grouping_factor);
             if (p.lwe_dimension % p.grouping_factor)

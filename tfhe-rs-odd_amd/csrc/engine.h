@@ -166,8 +166,10 @@ struct LargePbsLaunch {
     int levels;                  // set by the launcher (= pbs_level)
     int chunk_count;             // set by the launcher: ciphertexts in the current chunk
     KernelTimer *timer = nullptr;  // optional per-kernel timing
+    int grouping = 0;              // > 0: multi-bit PBS (fbsk = [n/g][2^g][L][k+1][k+1] polys)
 };
 bool large_pbs_supported(int N, int k, int L);
+bool large_multibit_supported(int N, int k, int L, int g);
 size_t large_pbs_scratch_per_ct(int N, int k, int L);
 hipError_t launch_large_pbs(int N, int k, int L, const LargePbsLaunch &a, hipStream_t s);
 hipError_t launch_large_bsk_to_fourier(const uint64_t *std_polys, double2 *fourier, size_t npoly,

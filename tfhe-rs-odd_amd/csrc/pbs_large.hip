@@ -239,14 +239,16 @@ __device__ __forceinline__ void decompose64(uint64_t x, int beta, int32_t (&d)[L
 #endif
 constexpr int TOPT = LARGE_TOPT;  // threads per top-stage workgroup
 
-// rotate, decompose, twist and top DIF radix-R of butterfly t of row r, CMUX i -> T
-template <int N, int K, int L>
+// rotate, decompose, twist and top DIF radix-R of butterfly t of row r, CMUX i -> T.
+// G > 0 (multi-bit, step i = group i): the external product's input is the accumulator itself
+// (acc <- ExtProd(KB_i, acc), lwe_multi_bit_programmable_bootstrapping.rs:548-828): no rotation.
+template <int N, int K, int L, int G>
 __device__ __forceinline__ void top_fwd_body(const LargePbsLaunch &a, int ct0, int i, int cl, int r, int t) {
     using S = Split<N>;
     constexpr int R = S::R, M = S::M;
     static_assert(L >= 1 && L <= 3, "levels 1..3");
     const uint64_t *in = a.lwe_in + (size_t)(ct0 + cl) * (a.n + 1);
-    const uint32_t at = pbs_modulus_switch<S::LOGN>(in[i]);
+    const uint32_t at = G ? 0u : pbs_modulus_switch<S::LOGN>(in[i]);
     const bool full_odd = (at / N) & 1;
     const int rem = at % N;
     const uint64_t *acc = a.acc + ((size_t)cl * (K + 1) + r) * N;
@@ -257,7 +259,13 @@ __device__ __forceinline__ void top_fwd_body(const LargePbsLaunch &a, int ct0, i
     for (int b = 0; b < R; b++) {
         const int j = t + 1024 * b;
         uint64_t dd[2];  // ct1 = X^{a~} acc - acc  (polynomial_wrapping_monic_monomial_mul_and_subtract)
-        ct1_pair_m<M>(acc, j, rem, full_odd, dd[0], dd[1]);
+        if constexpr (G > 0) {
+            const acc_pair self = *reinterpret_cast<const acc_pair *>(acc + 2 * j);
+            dd[0] = self.x;
+            dd[1] = self.y;
+        } else {
+            ct1_pair_m<M>(acc, j, rem, full_odd, dd[0], dd[1]);
+        }
         int32_t d0[L], d1[L];
         decompose64<L>(dd[0], beta, d0);
         decompose64<L>(dd[1], beta, d1);
@@ -302,7 +310,7 @@ __device__ __forceinline__ void top_fwd_body(const LargePbsLaunch &a, int ct0, i
 template <int N, int L>
 constexpr int top_fwd_wpe() { return Split<N>::R == 16 && L != 2 ? 2 : 4; }
 
-template <int N, int K, int L>
+template <int N, int K, int L, int G>
 __global__ void __launch_bounds__(TOPT, (top_fwd_wpe<N, L>())) large_top_fwd_kernel(LargePbsLaunch a, int ct0, int i) {
     constexpr int BPP = 1024 / TOPT;  // workgroups per polynomial
     // XCD-aware: workgroup w runs on XCD w % 8; all (K+1) BPP workgroups of a ciphertext share
@@ -311,7 +319,7 @@ __global__ void __launch_bounds__(TOPT, (top_fwd_wpe<N, L>())) large_top_fwd_ker
     const int sub = m % ((K + 1) * BPP);
     const int cl = x + 8 * (m / ((K + 1) * BPP));
     if (cl >= a.chunk_count) return;  // whole workgroup
-    top_fwd_body<N, K, L>(a, ct0, i, cl, sub / BPP, (sub % BPP) * TOPT + threadIdx.x);
+    top_fwd_body<N, K, L, G>(a, ct0, i, cl, sub / BPP, (sub % BPP) * TOPT + threadIdx.x);
 }
 
 // (k+1) L waves; LDS: one 1024-entry buffer per wave + the sub-block twiddle table
@@ -338,11 +346,30 @@ __device__ __forceinline__ void sub_block_of(int b, int &q, int &cl) {
     }
 }
 
-template <int N, int K, int L>
-__global__ void __launch_bounds__((LargeSubCfg<K, L>::THREADS), 2) large_sub_kernel(LargePbsLaunch a, int ct0, int i) {
+// multi-bit: spectrum of X^d at frequency f, i^q twist[r] with t = d (1 - 4 f) mod 2N = q M + r
+// (exact; the oracle's mono_spectrum, the same sign/swap per quadrant)
+template <int N>
+__device__ __forceinline__ cx mono_spectrum(const double2 *__restrict__ twist, uint32_t d, uint32_t f) {
+    constexpr int M = N / 2;
+    const uint32_t t = (d - 4u * d * f) & (uint32_t)(2 * N - 1);
+    const uint32_t q = t / (uint32_t)M, r = t % (uint32_t)M;
+    const cx w = gld(twist + r);
+    switch (q) {
+        case 0: return w;
+        case 1: return cx{-w.im, w.re};
+        case 2: return cx{-w.re, -w.im};
+        default: return cx{w.im, -w.re};
+    }
+}
+
+// the multi-bit keybundle (2^g operands per GGSW element) needs more than the 256 registers of
+// two waves per SIMD: one wave per SIMD there
+template <int N, int K, int L, int G>
+__global__ void __launch_bounds__((LargeSubCfg<K, L>::THREADS), (G ? 1 : 2)) large_sub_kernel(LargePbsLaunch a, int ct0, int i) {
     using Cfg = LargeSubCfg<K, L>;
     using S = Split<N>;
     constexpr int M = S::M, R = S::R;
+    constexpr int NSEL = G ? 1 << G : 1;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double2 *lds = reinterpret_cast<double2 *>(smem);
     const int lane = threadIdx.x & 63;
@@ -371,18 +398,67 @@ __global__ void __launch_bounds__((LargeSubCfg<K, L>::THREADS), 2) large_sub_ker
     __syncthreads();
     const bool mac = wave <= K;  // wave c computes output column c
     if (mac) {
-        // column c: sum over levels L..1 and rows 0..k (ggsw.rs:524-567), oracle order
-        const double2 *G = a.fbsk + (size_t)i * L * (K + 1) * (K + 1) * M + (size_t)wave * M + 1024 * q + lane;
+        // column c: sum over levels L..1 and rows 0..k (ggsw.rs:524-567), oracle order.  Multi-bit:
+        // the GGSW is the keybundle KB_i = GGSW_0 + sum_sel X^{deg_sel} GGSW_sel, built per
+        // frequency in selector order (the oracle's mb_keybundle; key layout [n/g][2^g][L][k+1][k+1])
+        constexpr size_t ggsw_len = (size_t)L * (K + 1) * (K + 1) * M;
+        const double2 *Gp = a.fbsk + (size_t)i * NSEL * ggsw_len + (size_t)wave * M + 1024 * q + lane;
+        // multi-bit: the 2^g GGSWs of the group through a buffer resource (wave-uniform base and
+        // scalar offsets per selector / row / slot, one per-lane VGPR offset), so the 2^g x 4
+        // operand addresses per slot cost no VALU and are not precomputed into registers
+        const __amdgpu_buffer_rsrc_t grs = make_rsrc(a.fbsk + (size_t)i * NSEL * ggsw_len);
+        const uint32_t gvo = 16u * (uint32_t)((size_t)wave * M + 1024 * q + lane);
+        uint32_t deg[NSEL];
+        if constexpr (G > 0) {
+            const uint64_t *in = a.lwe_in + (size_t)(ct0 + cl) * (a.n + 1) + (size_t)i * G;
+#pragma unroll
+            for (int sel = 1; sel < NSEL; sel++) {
+                uint64_t d = 0;
+#pragma unroll
+                for (int b = 0; b < G; b++)
+                    if ((sel >> (G - 1 - b)) & 1) d += in[b];
+                deg[sel] = pbs_modulus_switch<S::LOGN>(d);
+            }
+        }
+        const uint32_t fl = (uint32_t)q + (uint32_t)R * SubFft::freq_lane(lane);
+        uint32_t gw = gvo;  // per-slot opaque copy of the GGSW lane offset (issue window)
 #pragma unroll
         for (int s = 0; s < 16; s++) {
-            if (s % LARGE_MAC_SB == 0) __builtin_amdgcn_sched_barrier(0);  // bound loads in flight
+            // bound the loads in flight: LARGE_MAC_SB slots per region; one slot (2^g GGSW
+            // operands per row and level) for the multi-bit keybundle
+            if (G > 0 || s % LARGE_MAC_SB == 0) __builtin_amdgcn_sched_barrier(0);
+            cx mono[NSEL];
+            if constexpr (G > 0) {
+                // issue window: slot s's monomial gathers take their index from an opaque copy that
+                // depends on slot s-2's result (hoisted all at once, the 2^g x 16 gathers spill)
+                uint32_t fw = fl;
+                gw = gvo;
+                if (s >= 2) asm volatile("" : "+v"(fw), "+v"(gw) : "v"(v[s >= 2 ? s - 2 : 0].re));
+                const uint32_t f = fw + (uint32_t)R * SubFft::freq_slot(s);  // frequency of (q, lane, s)
+#pragma unroll
+                for (int sel = 1; sel < NSEL; sel++) mono[sel] = mono_spectrum<N>(a.twist, deg[sel], f);
+            }
             cx o{0.0, 0.0};
 #pragma unroll
             for (int lvl = L; lvl >= 1; lvl--) {
 #pragma unroll
                 for (int r = 0; r <= K; r++) {
                     const int p = (lvl - 1) * (K + 1) + r;
-                    const double2 gg = G[(size_t)p * (K + 1) * M + s * 64];
+                    double2 gg;
+                    if constexpr (G > 0) {
+                        __builtin_amdgcn_sched_barrier(0);  // one (level, row) of 2^g operands in flight
+                        constexpr uint32_t rowb = 16u * (uint32_t)((K + 1) * M);
+                        gg = buffer_ld_d2(grs, gw, (uint32_t)p * rowb + 1024u * (uint32_t)s);
+#pragma unroll
+                        for (int sel = 1; sel < NSEL; sel++) {
+                            const double2 g2 = buffer_ld_d2(grs, gw, (uint32_t)(16u * sel * ggsw_len) + (uint32_t)p * rowb +
+                                                                          1024u * (uint32_t)s);
+                            gg.x = fma(g2.x, mono[sel].re, fma(-g2.y, mono[sel].im, gg.x));
+                            gg.y = fma(g2.x, mono[sel].im, fma(g2.y, mono[sel].re, gg.y));
+                        }
+                    } else {
+                        gg = Gp[(size_t)p * (K + 1) * M + s * 64];
+                    }
                     const double2 ff = reinterpret_cast<const double2 *>(lds)[p * SubFft::XL + s * 64 + lane];
                     if (lvl == L && r == 0) {
                         o.re = fma(gg.x, ff.x, -(gg.y * ff.y));
@@ -776,8 +852,9 @@ __global__ void __launch_bounds__(GroupCfg::THREADS, 2) large_group_cmux_kernel(
     }
 }
 
-// top DIT radix-R of butterfly t of column col, backward conversion, acc += increments
-template <int N, int K>
+// top DIT radix-R of butterfly t of column col, backward conversion, acc += increments (G > 0,
+// multi-bit: acc = the external product, the reference's zeroed ping-pong destination)
+template <int N, int K, int G = 0>
 __device__ __forceinline__ void top_inv_body(const LargePbsLaunch &a, int cl, int col, int t) {
     using S = Split<N>;
     constexpr int R = S::R, M = S::M;
@@ -796,20 +873,27 @@ __device__ __forceinline__ void top_inv_body(const LargePbsLaunch &a, int cl, in
     for (int b = 0; b < R; b++) {
         const int j = t + 1024 * b;
         const cx w = gld(a.twist + j);
-        acc_pair pr = *reinterpret_cast<const acc_pair *>(acc + 2 * j);
-        uint64_t lo = pr.x, hi = pr.y;
-        backward_add(u[b], w, lo, hi, k32);  // the resident key carries the 1/M
+        acc_pair pr;
+        uint64_t lo, hi;
+        if constexpr (G > 0) {
+            backward_convert(u[b], w, lo, hi, k32);
+        } else {
+            pr = *reinterpret_cast<const acc_pair *>(acc + 2 * j);
+            lo = pr.x;
+            hi = pr.y;
+            backward_add(u[b], w, lo, hi, k32);  // the resident key carries the 1/M
+        }
         pr.x = lo;
         pr.y = hi;
         *reinterpret_cast<acc_pair *>(acc + 2 * j) = pr;
     }
 }
 
-template <int N, int K>
+template <int N, int K, int G = 0>
 __global__ void __launch_bounds__(TOPT) large_top_inv_kernel(LargePbsLaunch a, int ct0, int i) {
     constexpr int BPP = 1024 / TOPT;
     const int col = (blockIdx.x / BPP) % (K + 1);
-    top_inv_body<N, K>(a, blockIdx.x / (BPP * (K + 1)), col, (blockIdx.x % BPP) * TOPT + threadIdx.x);
+    top_inv_body<N, K, G>(a, blockIdx.x / (BPP * (K + 1)), col, (blockIdx.x % BPP) * TOPT + threadIdx.x);
 }
 
 // sample extract at degree 0 (glwe_sample_extraction.rs:91-147)
@@ -930,7 +1014,7 @@ size_t large_pbs_scratch_per_ct(int N, int k, int L) {
     return (size_t)(k + 1) * N * sizeof(uint64_t) + (size_t)L * (k + 1) * (N / 2) * sizeof(double2);
 }
 
-template <int N, int K, int L>
+template <int N, int K, int L, int G = 0>
 static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
     using S = Split<N>;
     if (a0.count == 0) return hipSuccess;
@@ -952,7 +1036,7 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
         const unsigned top_blocks = (unsigned)cnt * (K + 1) * (1024 / TOPT);
         const unsigned fwd_blocks = (unsigned)((cnt + 7) / 8) * 8 * (K + 1) * (1024 / TOPT);
         const size_t out_elems = (size_t)cnt * (K * N + 1);
-        if constexpr (N == LN && K == 1 && L == 2) {
+        if constexpr (N == LN && K == 1 && L == 2 && G == 0) {
             if (LARGE_GROUP_SUB) {
                 const unsigned grp_blocks = (unsigned)((cnt + 7) / 8) * 8 * 4 * GroupCfg::PARTS;
                 const unsigned dig_blocks = (unsigned)((cnt + 7) / 8) * 8 * (LM / LARGE_DIGT);
@@ -975,18 +1059,19 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
             }
         }
         const unsigned sub_blocks = (unsigned)cnt * S::R;
-        for (int i = 0; i < a.n; i++) {
+        const int steps = G ? a.n / G : a.n;  // CMUXes, or multi-bit groups
+        for (int i = 0; i < steps; i++) {
             {
                 TimedLaunch tl(a.timer, "large_top_fwd_kernel", s);
-                hipLaunchKernelGGL((large_top_fwd_kernel<N, K, L>), dim3(fwd_blocks), dim3(TOPT), 0, s, a, ct0, i);
+                hipLaunchKernelGGL((large_top_fwd_kernel<N, K, L, G>), dim3(fwd_blocks), dim3(TOPT), 0, s, a, ct0, i);
             }
             {
                 TimedLaunch tl(a.timer, "large_sub_kernel", s);
-                hipLaunchKernelGGL((large_sub_kernel<N, K, L>), dim3(sub_blocks), dim3(Sub::THREADS), Sub::LDS, s, a,
-                                   ct0, i);
+                hipLaunchKernelGGL((large_sub_kernel<N, K, L, G>), dim3(sub_blocks), dim3(Sub::THREADS), Sub::LDS, s,
+                                   a, ct0, i);
             }
             TimedLaunch tl(a.timer, "large_top_inv_kernel", s);
-            hipLaunchKernelGGL((large_top_inv_kernel<N, K>), dim3(top_blocks), dim3(TOPT), 0, s, a, ct0, i);
+            hipLaunchKernelGGL((large_top_inv_kernel<N, K, G>), dim3(top_blocks), dim3(TOPT), 0, s, a, ct0, i);
         }
         hipLaunchKernelGGL((large_extract_kernel<N, K>), dim3((unsigned)((out_elems + 255) / 256)), dim3(256), 0, s, a,
                            ct0, cnt);
@@ -1004,7 +1089,16 @@ static hipError_t launch_large_n(int L, const LargePbsLaunch &a, hipStream_t s) 
     }
 }
 
+// multi-bit through the split CMUX: the reference's multi-bit sets above N = 2048
+// (PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_{2,3}_KS_PBS: N = 8192, L = 2, shortint/parameters/
+// multi_bit.rs:134-153, 192-210)
+bool large_multibit_supported(int N, int k, int L, int g) { return N == 8192 && k == 1 && L == 2 && (g == 2 || g == 3); }
+
 hipError_t launch_large_pbs(int N, int k, int L, const LargePbsLaunch &a, hipStream_t s) {
+    if (a.grouping) {
+        if (!large_multibit_supported(N, k, L, a.grouping) || a.n % a.grouping) return hipErrorInvalidValue;
+        return a.grouping == 2 ? launch_large_t<8192, 1, 2, 2>(a, s) : launch_large_t<8192, 1, 2, 3>(a, s);
+    }
     if (!large_pbs_supported(N, k, L)) return hipErrorInvalidValue;
     switch (N) {
         case 4096: return launch_large_n<4096>(L, a, s);

@@ -6,6 +6,7 @@ authoritative -- see SURVEY.md 0.4 for the BASELINE.json annotation mismatch).
   PARAM_MESSAGE_4_CARRY_4_KS_PBS   shortint/parameters/mod.rs:1063-1077 (alias :1271)
   PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS   shortint/parameters/multi_bit.rs:173-190
   PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS   shortint/parameters/multi_bit.rs:115-132
+  PARAM_MULTI_BIT_MESSAGE_{1_CARRY_1,3_CARRY_3}_GROUP_{2,3}_KS_PBS   multi_bit.rs:96-114,134-153,154-172,192-210
   MANTICORE_PARAMETERS (fork)      gadget/parameters/mod.rs:224-235
   GADGET_* (fork)                  gadget/parameters/mod.rs:84-222 (DEFAULT, SIMON_40,
                                    ZAMA_TRIVIUM, ASCON_40, SHA3_40, AES_40, AES_23, TFHE_LIB)
@@ -78,6 +79,32 @@ PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS = ClassicPBSParameters(
     pbs_base_log=22, pbs_level=1, ks_base_log=5, ks_level=3,
     message_modulus=4, carry_modulus=4, grouping_factor=2,
     name="PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS")
+
+# the other multi-bit sets (shortint/parameters/multi_bit.rs:96-153, 154-210)
+PARAM_MULTI_BIT_MESSAGE_1_CARRY_1_GROUP_2_KS_PBS = ClassicPBSParameters(
+    lwe_dimension=764, glwe_dimension=3, polynomial_size=512,
+    lwe_modular_std_dev=0.000006025673585415336, glwe_modular_std_dev=0.0000000000039666089171633006,
+    pbs_base_log=18, pbs_level=1, ks_base_log=6, ks_level=2, message_modulus=2, carry_modulus=2,
+    grouping_factor=2, name="PARAM_MULTI_BIT_MESSAGE_1_CARRY_1_GROUP_2_KS_PBS")
+PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_2_KS_PBS = ClassicPBSParameters(
+    lwe_dimension=922, glwe_dimension=1, polynomial_size=8192,
+    lwe_modular_std_dev=0.0000003272369292345697, glwe_modular_std_dev=0.0000000000000000002168404344971009,
+    pbs_base_log=14, pbs_level=2, ks_base_log=4, ks_level=4, message_modulus=8, carry_modulus=8,
+    grouping_factor=2, name="PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_2_KS_PBS")
+PARAM_MULTI_BIT_MESSAGE_1_CARRY_1_GROUP_3_KS_PBS = ClassicPBSParameters(
+    lwe_dimension=765, glwe_dimension=3, polynomial_size=512,
+    lwe_modular_std_dev=0.000005915594083804978, glwe_modular_std_dev=0.0000000000039666089171633006,
+    pbs_base_log=18, pbs_level=1, ks_base_log=6, ks_level=2, message_modulus=2, carry_modulus=2,
+    grouping_factor=3, name="PARAM_MULTI_BIT_MESSAGE_1_CARRY_1_GROUP_3_KS_PBS")
+PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_3_KS_PBS = ClassicPBSParameters(
+    lwe_dimension=972, glwe_dimension=1, polynomial_size=8192,
+    lwe_modular_std_dev=0.00000013016688349592805, glwe_modular_std_dev=0.0000000000000000002168404344971009,
+    pbs_base_log=14, pbs_level=2, ks_base_log=6, ks_level=3, message_modulus=8, carry_modulus=8,
+    grouping_factor=3, name="PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_3_KS_PBS")
+MULTI_BIT_ALL = {p.name: p for p in [
+    PARAM_MULTI_BIT_MESSAGE_1_CARRY_1_GROUP_2_KS_PBS, PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS,
+    PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_2_KS_PBS, PARAM_MULTI_BIT_MESSAGE_1_CARRY_1_GROUP_3_KS_PBS,
+    PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS, PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_3_KS_PBS]}
 
 # fork: GadgetParameters carry no message/carry moduli; 2 x 2 used here for LUT boxes
 MANTICORE_PARAMETERS = ClassicPBSParameters(
@@ -220,3 +247,4 @@ ALL = {p.name: p for p in [PARAM_MESSAGE_2_CARRY_2_KS_PBS, PARAM_MESSAGE_4_CARRY
                            PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS,
                            PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS, MANTICORE_PARAMETERS] + GADGET_ALL}
 ALL.update(SHORTINT_ALL)
+ALL.update(MULTI_BIT_ALL)
