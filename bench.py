@@ -110,8 +110,20 @@ def _split_params():
         out[tag] = (name, f"shortint apply_lookup_table (keyswitch -> PBS) at {name} (shortint/parameters/mod.rs:"
                           f"{SHORTINT_SOURCE_LINE[name]}), N={p.polynomial_size}, batch per GPU; the reference publishes "
                           + ("121 ms per KS+PBS at 3_3 (benchmarks.md:42)" if tag == "3_3" else "no number for this set"),
-                    f"large_sub_kernel<{p.polynomial_size},1,{p.pbs_level}> (+ large_top_fwd/top_inv per CMUX, "
+                    f"large_sub_kernel<{p.polynomial_size},1,{p.pbs_level},0> (+ large_top_fwd/top_inv per CMUX, "
                     "ks_mfma_kernel)")
+    # the multi-bit sets at N = 8192 (shortint/parameters/multi_bit.rs:134-153, 192-210): the split
+    # CMUX with the keybundle built inside large_sub_kernel, one CMUX per group of g
+    from tfhe_mi355.parameters import MULTI_BIT_ALL
+
+    for g, line in ((2, 134), (3, 192)):
+        name = f"PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_{g}_KS_PBS"
+        p = MULTI_BIT_ALL[name]
+        out[f"mb3_3g{g}"] = (name, f"shortint apply_lookup_table (keyswitch -> multi-bit PBS, grouping {g}) at {name} "
+                                   f"(shortint/parameters/multi_bit.rs:{line}), N={p.polynomial_size}, batch per GPU; "
+                                   "the reference publishes no number for this set",
+                             f"large_sub_kernel<{p.polynomial_size},1,{p.pbs_level},{g}> (+ large_top_fwd/top_inv "
+                             "per group, ks_mfma_kernel)")
     return out
 
 
@@ -191,6 +203,18 @@ DOMINANT = {
 DOMINANT.update({t: ("large_sub_kernel", PARAMS[t][2].split(" ")[0]) for t in SPLIT_TAGS})
 
 
+def pmc_entry(by_kernel: dict, kernel: str):
+    """The entry of `kernel` in a per-kernel PMC summary: its exact normalised rocprofv3 name, else
+    (a timer family name without template arguments) the one instantiation of that family."""
+    if kernel in by_kernel:
+        return by_kernel[kernel]
+    if "<" not in kernel:
+        hits = [v for k, v in by_kernel.items() if k == kernel or k.startswith(kernel + "<")]
+        if len(hits) == 1:
+            return hits[0]
+    return None
+
+
 def load_pmc(tag: str, kernel: str):
     """The committed rocprofv3 PMC summary of this workload (scripts/pmc_workload.sh ->
     profiles/r03_pmc_<tag>.json) and its entry for `kernel`.  A file without an entry for the
@@ -201,7 +225,7 @@ def load_pmc(tag: str, kernel: str):
     if not os.path.exists(path):
         return None, f"no PMC summary profiles/{name}"
     d = json.load(open(path))
-    e = (d.get("by_kernel") or {}).get(kernel)
+    e = pmc_entry(d.get("by_kernel") or {}, kernel)
     if e is None:
         return None, (f"refused: profiles/{name} holds counters for {sorted(d.get('by_kernel') or {})}, "
                       f"not for the timed kernel {kernel}")
@@ -229,7 +253,11 @@ def split_sub_flops(p) -> float:
     in large_top_fwd / large_top_inv."""
     M = p.polynomial_size // 2
     k1, L = p.glwe_dimension + 1, p.pbs_level
-    return k1 * L * 5 * M * 10 + k1 * k1 * L * M * 8 + k1 * 5 * M * 10
+    g = p.grouping_factor
+    # multi-bit: one launch per group of g, the keybundle's (2^g - 1) monomial-weighted GGSW sums
+    # (8 flop per element, as pbs_flops) built in the same kernel
+    kb = ((1 << g) - 1) * k1 * k1 * L * M * 8 if g else 0
+    return k1 * L * 5 * M * 10 + k1 * k1 * L * M * 8 + k1 * 5 * M * 10 + kb
 
 
 def split_chunk(p, units: int) -> int:
@@ -316,7 +344,7 @@ def roofline(tag, p, units_per_launch: int, step_ms: float, kname: str, with_ks:
             t = ktimes.get(kn)
             if not t:
                 continue
-            e = (pmc or {}).get("_all", {}).get(kn) or {}
+            e = pmc_entry((pmc or {}).get("_all") or {}, kn) or {}
             ach = b * chunk / (t[0] * 1e-3) / 1e9
             mem[kn] = {"bound": "fabric (L2 <-> Infinity Cache / HBM)", "model_bytes_per_launch": b * chunk,
                        "kernel_ms": t[0], "achieved_GBps": ach, "frac_of_hbm_peak": ach / HBM_PEAK_GBS,

@@ -16,7 +16,7 @@ step() {  # step NAME TIMEOUT CMD...
 kargs() {  # bench arguments of a kernel-trace / PMC run of one workload
   case $1 in
     4_4) echo "--params 4_4 --batch 1024 --steps 2 --warmup 1" ;;
-    3_3|2_4|1_5|4_2|5_1|6_0|1_4|2_3|3_2|4_1|5_0|1_6|2_5|3_4|4_3|5_2|6_1|7_0|1_7) echo "--params $1 --steps 2 --warmup 1" ;;
+    3_3|mb3_3g2|mb3_3g3|2_4|1_5|4_2|5_1|6_0|1_4|2_3|3_2|4_1|5_0|1_6|2_5|3_4|4_3|5_2|6_1|7_0|1_7) echo "--params $1 --steps 2 --warmup 1" ;;
     *) echo "--params $1 --steps 5 --warmup 1" ;;
   esac
 }
