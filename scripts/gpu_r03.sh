@@ -8,8 +8,12 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 step() {  # step NAME TIMEOUT CMD...
   local name=$1 to=$2; shift 2
-  echo "== $name $(date +%T)"; timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
-  local rc=$?; echo "== $name rc=$rc $(date +%T)"; tail -4 "gpurun_out/$name.log"
+  echo "== $name $(date +%T)"
+  # heartbeat: a step that prints nothing for minutes (keygen, rocprofv3 passes) is not hung
+  ( while sleep 45; do echo "   $name running $(date +%T)"; done ) & local hb=$!
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?; kill $hb 2>/dev/null; wait $hb 2>/dev/null
+  echo "== $name rc=$rc $(date +%T)"; tail -4 "gpurun_out/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
@@ -28,6 +32,8 @@ for s in $STAGES; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 900 python -u bench.py ;;
     bench:*) step bench_${s#bench:} 600 python -u bench.py $(kargs ${s#bench:}) ;;
+    # the N = 32768, L = 2 CMUX through the split path instead of the grouped one (A/B)
+    splitab:*) step splitab_${s#splitab:} 600 env TFHE_MI355_LARGE_SPLIT=1 python -u bench.py $(kargs ${s#splitab:}) --no-cpu-baseline --no-host-abi ;;
     kstats:*) t=${s#kstats:}; step kstats_$t 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kstats_$t -o run \
                 --output-format csv -- python3 bench.py $(kargs $t) --no-cpu-baseline --no-host-abi ;;
     pmc:*) t=${s#pmc:}; step pmc_$t 1100 bash scripts/pmc_workload.sh $t ;;

@@ -13,6 +13,8 @@
 // batch-wide launches (below), each streaming at full occupancy.  Twiddles: top stage W_M[a c]
 // from a [c-1][a] copy of the table (coalesced); sub-blocks W_M[16 x] through an LDS table (the
 // oracle's tstride-16 reads of the same table, so bit-identical).
+#include <cstdlib>
+
 #include "engine.h"
 #include "pbs_common.h"
 
@@ -1014,6 +1016,16 @@ size_t large_pbs_scratch_per_ct(int N, int k, int L) {
     return (size_t)(k + 1) * N * sizeof(uint64_t) + (size_t)L * (k + 1) * (N / 2) * sizeof(double2);
 }
 
+// TFHE_MI355_LARGE_SPLIT=1: the N = 32768, L = 2 CMUX through the split path (top_fwd / sub /
+// top_inv) instead of the grouped one -- same Fourier key layout, same outputs (A/B switch)
+static bool large_grouped_enabled() {
+    static const bool v = [] {
+        const char *e = std::getenv("TFHE_MI355_LARGE_SPLIT");
+        return !(e && e[0] && e[0] != '0');
+    }();
+    return v;
+}
+
 template <int N, int K, int L, int G = 0>
 static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
     using S = Split<N>;
@@ -1037,7 +1049,7 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
         const unsigned fwd_blocks = (unsigned)((cnt + 7) / 8) * 8 * (K + 1) * (1024 / TOPT);
         const size_t out_elems = (size_t)cnt * (K * N + 1);
         if constexpr (N == LN && K == 1 && L == 2 && G == 0) {
-            if (LARGE_GROUP_SUB) {
+            if (LARGE_GROUP_SUB && large_grouped_enabled()) {
                 const unsigned grp_blocks = (unsigned)((cnt + 7) / 8) * 8 * 4 * GroupCfg::PARTS;
                 const unsigned dig_blocks = (unsigned)((cnt + 7) / 8) * 8 * (LM / LARGE_DIGT);
                 for (int i = 0; i < a.n; i++) {

@@ -39,6 +39,43 @@ namespace tfhe_mi355 {
 #ifndef PBS_MB_BUFLD
 #define PBS_MB_BUFLD 1  // GGSW loads through a buffer resource: scalar offsets, no 64-bit VALU address adds
 #endif
+// Twist table in LDS, shared by the linear twist reads (digits, backward conversion) and the
+// keybundle's monomial reads.  A monomial read fetches entry r of t = d (1 - 4 f) mod 2N, lanes
+// 16 apart in f stepping t by 4d and the two 16-lane halves of a ds_read_b64 group by 256d.  As one
+// [M] double2 array the 32 lanes of a group put 8.1 distinct entries on one bank on average (PMC:
+// 56 % of the g = 3 kernel's LDS cycles were conflict cycles, profiles/r03_pmc_mb3.json).  Here re
+// and im are two [M] double planes and entry r sits at position r ^ ((r >> 5) & 31): 2.36 on
+// average (exhaustive over d and slots), and a linear read (r = lane + 64 b) stays conflict-free.
+template <int M>
+struct TwistLds {
+    static_assert(M == 1024, "swizzle sized for M = 1024 (r >> 5 < 32)");
+    static constexpr uint32_t IM = 8u * M;  // byte offset of the im plane (table at LDS byte 0)
+    __device__ static uint32_t pos(uint32_t r) { return r ^ ((r >> 5) & 31u); }
+    __device__ static void fill(double *t, const double2 *twist, int tid, int nt) {
+        for (int e = tid; e < M; e += nt) {
+            const uint32_t p = pos((uint32_t)e);
+            t[p] = twist[e].x;
+            t[M + p] = twist[e].y;
+        }
+    }
+    // 8 (lane ^ (lane >> 5)): position of twist[lane + 64 b] is 64 b + (lane ^ (lane >> 5) ^ 2 b)
+    __device__ static uint32_t lane_base(int lane) { return 8u * (uint32_t)(lane ^ (lane >> 5)); }
+    __device__ static cx linear(uint32_t lb, int b) {  // twist[lane + 64 b]; b compile-time: one XOR
+        const uint32_t a = (lb ^ (16u * (uint32_t)b)) + 512u * (uint32_t)b;
+        return {lds_ld_f64(a), lds_ld_f64(a + IM)};
+    }
+    // i^q twist[r] for t = q M + r (t mod 2^32, bits 0 .. log2 M + 1 used): the swap for odd q is
+    // the plane choice of the two reads (re at the returned address, im at address ^ IM), the signs
+    // (re: q0 ^ q1, im: q1) are XORed into the high words -- no selects
+    __device__ static cx mono(uint32_t t) {
+        constexpr int LOG2M = ilog2(M);
+        const uint32_t are = ((t & (2u * M - 1)) ^ ((t >> 5) & 31u)) << 3;
+        const double re = lds_ld_f64(are), im = lds_ld_f64(are ^ IM);
+        const uint32_t sim = t << (30 - LOG2M);  // q1 at bit 31; + 2^30 carries q0 into it
+        return {flip_sign(re, sim + 0x40000000u), flip_sign(im, sim)};
+    }
+};
+
 constexpr int mb_wpe() { return PBS_WAVES_PER_EU > 0 ? PBS_WAVES_PER_EU : (PBS_MB_CPW >= 4 ? 2 : 1); }
 
 template <int N, int K, int L, int G>
@@ -48,7 +85,6 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
     constexpr int M = N / 2;
     constexpr int V = M / 64;
     constexpr int LOG2N = ilog2(N);
-    constexpr int LOG2M = LOG2N - 1;
     constexpr int NSEL = 1 << G;
     using Fft = WaveFft<M>;
     using Lay = PbsLds<M>;
@@ -57,7 +93,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double2 *lds = reinterpret_cast<double2 *>(smem);
-    const double2 *s_twist = lds + Lay::twist_off;
+    using Tw = TwistLds<M>;
 
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wave = wid % (K + 1);  // polynomial / column
@@ -74,7 +110,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
     BlockSync sync;
     WaveLocalSync wsync;
 
-    for (int e = threadIdx.x; e < M; e += blockDim.x) lds[Lay::twist_off + e] = a.twist[e];
+    Tw::fill(reinterpret_cast<double *>(lds + Lay::twist_off), a.twist, threadIdx.x, blockDim.x);
     // spectrum exchange among this ciphertext's waves (GroupSync, pbs_common.h): flags after the buffers
     uint32_t *gflags = reinterpret_cast<uint32_t *>(smem + Lay::bytes((K + 1) * CPW));
     if (PBS_GROUP_SYNC && threadIdx.x < (K + 1) * CPW) gflags[threadIdx.x] = 0;
@@ -137,13 +173,12 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
         // the twist table is the first LDS object and the kernel has no static LDS, so its byte
         // address is 0 and the monomial read addresses need no base
         static_assert(Lay::twist_off == 0, "twist table at LDS offset 0");
+        const uint32_t lb = Tw::lane_base(lane);
         uint32_t tb[NSEL];
 #pragma unroll
         for (int sel = 1; sel < NSEL; sel++) {
-            // kept as 16 t (mod 2^32): masked to 16 bits it is the byte offset of table entry t
-            // mod M in its low bits and the quadrant q in bits 14-15 (t < 2N = 4M)
-            tb[sel] = 16u * (d4[sel] - 4u * d4[sel] * fl);
-            d4[sel] *= 64u;
+            tb[sel] = d4[sel] - 4u * d4[sel] * fl;  // t mod 2^32 at freq_slot 0
+            d4[sel] *= 4u;
         }
         const double2 *grp = gcol + (size_t)j * NSEL * ggsw_len;
         const uint32_t gsoff = (uint32_t)((size_t)j * NSEL * ggsw_len * 16);  // < 2^31 (MB-BSK bytes)
@@ -169,8 +204,8 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
                     d1 = decomp_digit32(st[V + b], beta, dmask);
                 }
                 const cx z = {(double)d0, (double)d1};
-                const double2 w = s_twist[lane + 64 * b];
-                v[b] = cmulw(z, w.x, w.y);
+                const cx w = Tw::linear(lb, b);
+                v[b] = cmulw(z, w.re, w.im);
             }
             Fft::forward(v, xb, tw, lane, wsync);
             wsync();
@@ -196,19 +231,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
                 // monomial spectra at this frequency: i^q twist[r], t = q M + r
                 cx mono[NSEL];
 #pragma unroll
-                for (int sel = 1; sel < NSEL; sel++) {
-                    // i^q twist[r]: the swap for odd q is done by the two 8-byte reads' addresses,
-                    // the signs (re: q0 ^ q1, im: q1) by XOR into the high words -- no selects
-                    // 16 t mod 2^32; only bits 4 .. LOG2M + 5 (r, q0, q1) are used below
-                    const uint32_t t16 = tb[sel] - d4[sel] * Fft::freq_slot(s);
-                    const uint32_t are = (t16 & (uint32_t)(16 * M - 16)) | ((t16 >> (LOG2M + 1)) & 8u);
-                    const double re = lds_ld_f64(are), im = lds_ld_f64(are ^ 8u);
-                    // q1 at bit 31; adding 2^30 there carries q0 into it: bit 31 = q0 ^ q1
-                    const uint32_t sim = t16 << (31 - (LOG2M + 5));
-                    const uint32_t sre = sim + 0x40000000u;
-                    mono[sel].re = flip_sign(re, sre);
-                    mono[sel].im = flip_sign(im, sim);
-                }
+                for (int sel = 1; sel < NSEL; sel++) mono[sel] = Tw::mono(tb[sel] - d4[sel] * Fft::freq_slot(s));
                 cx o = (L > 1 && lvl != L) ? acc[L > 1 ? s : 0] : cx{0.0, 0.0};
 #pragma unroll
                 for (int r = 0; r <= K; r++) {
@@ -246,19 +269,14 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
             if constexpr (L == 1) {
                 Fft::inverse(v, xb, tw, lane, wsync);
 #pragma unroll
-                for (int b = 0; b < V; b++) {
-                    const double2 w = s_twist[lane + 64 * b];  // the resident key carries the 1/M
-                    backward_convert(v[b], cx{w.x, w.y}, c0[b], c0[V + b], k32);
-                }
+                for (int b = 0; b < V; b++)  // the resident key carries the 1/M
+                    backward_convert(v[b], Tw::linear(lb, b), c0[b], c0[V + b], k32);
             }
         }
         if constexpr (L > 1) {
             Fft::inverse(acc, xb, tw, lane, wsync);
 #pragma unroll
-            for (int b = 0; b < V; b++) {
-                const double2 w = s_twist[lane + 64 * b];
-                backward_convert(acc[b], cx{w.x, w.y}, c0[b], c0[V + b], k32);
-            }
+            for (int b = 0; b < V; b++) backward_convert(acc[b], Tw::linear(lb, b), c0[b], c0[V + b], k32);
         }
     }
 
@@ -311,7 +329,6 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
     static_assert(V % W == 0, "spectrum slots split evenly over the waves");
     constexpr int SPW = V / W;        // slots per wave in phase 2
     constexpr int LOG2N = ilog2(N);
-    constexpr int LOG2M = LOG2N - 1;
     constexpr int NSEL = 1 << G;
     static_assert((K + 1) * (K + 1) * NSEL <= 32, "a slot's GGSW operands must fit the register budget");
     using Fft = WaveFft<M>;
@@ -322,7 +339,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double2 *lds = reinterpret_cast<double2 *>(smem);
-    const double2 *s_twist = lds + Lay::twist_off;
+    using Tw = TwistLds<M>;
 
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wave = wid % (K + 1);  // row in phase 1, column in phase 3
@@ -333,7 +350,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
     const DigitL1 digit_l1(beta);
     WaveLocalSync wsync;
 
-    for (int e = threadIdx.x; e < M; e += blockDim.x) lds[Lay::twist_off + e] = a.twist[e];
+    Tw::fill(reinterpret_cast<double *>(lds + Lay::twist_off), a.twist, threadIdx.x, blockDim.x);
     Fft::Lds::template fill<M>(lds + Lay::s1_off, lds + Lay::s2_off, a.W, threadIdx.x, blockDim.x);
     const typename Fft::Lds tw{lds + Lay::s1_off, lds + Lay::s2_off};
     __syncthreads();
@@ -371,6 +388,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
     for (int j = 0; j < groups; j++) {
         int lane = lane0;
         asm volatile("" : "+v"(lane));
+        const uint32_t lb = Tw::lane_base(lane);
         // ---- phase 1: forward FFT of row `wave` of ciphertext `slot`, published to xb ----
         {
             cx v[V];
@@ -378,8 +396,8 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
             for (int b = 0; b < V; b++) {
                 const int32_t d0 = digit_l1((uint32_t)(c0[b] >> 32));
                 const int32_t d1 = digit_l1((uint32_t)(c0[V + b] >> 32));
-                const double2 w = s_twist[lane + 64 * b];
-                v[b] = cmulw(cx{(double)d0, (double)d1}, w.x, w.y);
+                const cx w = Tw::linear(lb, b);
+                v[b] = cmulw(cx{(double)d0, (double)d1}, w.re, w.im);
             }
             Fft::forward(v, xb, tw, lane, wsync);
             wsync();
@@ -436,7 +454,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
                     load_slot(s);
                 }
                 // t = d (1 - 4 f) mod 2N, f = freq_lane + freq_slot(s) < M: |1 - 4 f| < 2^12 and
-                // d <= 2^12, so a 24-bit signed multiply is exact; 16 t mod 2^32 is a shift of it
+                // d <= 2^12, so a 24-bit signed multiply is exact
                 const int32_t w = 1 - 4 * (fl + 16 * (s >> 2) + 256 * (s & 3));
 #pragma unroll
                 for (int c = 0; c < CPW; c++) {
@@ -444,14 +462,7 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
                     // monomial spectra of ciphertext c at frequency f: i^q twist[r], t = q M + r
                     cx mono[NSEL];
 #pragma unroll
-                    for (int sel = 1; sel < NSEL; sel++) {
-                        const uint32_t t16 = (uint32_t)__mul24(dd[c][sel], w) << 4;
-                        const uint32_t are = (t16 & (uint32_t)(16 * M - 16)) | ((t16 >> (LOG2M + 1)) & 8u);
-                        const double re = lds_ld_f64(are), im = lds_ld_f64(are ^ 8u);
-                        const uint32_t sim = t16 << (31 - (LOG2M + 5));
-                        mono[sel].re = flip_sign(re, sim + 0x40000000u);
-                        mono[sel].im = flip_sign(im, sim);
-                    }
+                    for (int sel = 1; sel < NSEL; sel++) mono[sel] = Tw::mono((uint32_t)__mul24(dd[c][sel], w));
                     double2 ff[K + 1];
 #pragma unroll
                     for (int r = 0; r <= K; r++)
@@ -498,10 +509,8 @@ __global__ void __launch_bounds__(64 * (K + 1) * PBS_MB_CPW, mb_wpe())
             wsync();
             Fft::inverse(v, xb, tw, lane, wsync);
 #pragma unroll
-            for (int b = 0; b < V; b++) {
-                const double2 w = s_twist[lane + 64 * b];  // the resident key carries the 1/M
-                backward_convert(v[b], cx{w.x, w.y}, c0[b], c0[V + b], k32);
-            }
+            for (int b = 0; b < V; b++)  // the resident key carries the 1/M
+                backward_convert(v[b], Tw::linear(lb, b), c0[b], c0[V + b], k32);
         }
     }
 
