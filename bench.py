@@ -122,13 +122,13 @@ def _split_params():
         out[f"mb3_3g{g}"] = (name, f"shortint apply_lookup_table (keyswitch -> multi-bit PBS, grouping {g}) at {name} "
                                    f"(shortint/parameters/multi_bit.rs:{line}), N={p.polynomial_size}, batch per GPU; "
                                    "the reference publishes no number for this set",
-                             f"large_sub_kernel<{p.polynomial_size},1,{p.pbs_level},{g}> (+ large_top_fwd/top_inv "
+                             f"large_mb_sub_kernel<{p.polynomial_size},1,{p.pbs_level},{g},1> (+ large_top_fwd/top_inv "
                              "per group, ks_mfma_kernel)")
     return out
 
 
 PARAMS.update(_split_params())
-SPLIT_TAGS = {t for t, v in PARAMS.items() if v[2].startswith("large_sub_kernel")}
+SPLIT_TAGS = {t for t, v in PARAMS.items() if v[2].startswith(("large_sub_kernel", "large_mb_sub_kernel"))}
 WITH_KS = {"4_4", "2_2ks"} | SPLIT_TAGS
 
 
@@ -200,7 +200,7 @@ DOMINANT = {
     "aes40": ("pbs_classic_kernel", "pbs_classic_kernel<512,3,4>"),
     "sha3": ("pbs_classic_kernel", "pbs_classic_kernel<256,5,1>"),
 }
-DOMINANT.update({t: ("large_sub_kernel", PARAMS[t][2].split(" ")[0]) for t in SPLIT_TAGS})
+DOMINANT.update({t: (PARAMS[t][2].split("<")[0], PARAMS[t][2].split(" ")[0]) for t in SPLIT_TAGS})
 
 
 def pmc_entry(by_kernel: dict, kernel: str):
@@ -313,9 +313,10 @@ def roofline(tag, p, units_per_launch: int, step_ms: float, kname: str, with_ks:
          "model": ((f"large_group_cmux_kernel FP64 flop per ciphertext and CMUX {large_group_flops(p):,.0f} "
                     f"(twist, forward FFTs incl. the top radix-16 share, MAC, inverse sub-FFTs) x {chunk} ciphertexts "
                     f"per launch / its average launch duration") if grouped else
-                   (f"large_sub_kernel FP64 flop per ciphertext and CMUX {split_sub_flops(p):,.0f} (1024-point "
-                    f"forward and inverse sub-FFTs, MAC) x {chunk} ciphertexts per launch / its average launch "
-                    f"duration") if large else
+                   (f"{fam} FP64 flop per ciphertext and {'group' if p.grouping_factor else 'CMUX'} "
+                    f"{split_sub_flops(p):,.0f} (1024-point forward and inverse sub-FFTs, MAC"
+                    f"{', keybundle' if p.grouping_factor else ''}) x {chunk} ciphertexts per launch / its average "
+                    f"launch duration") if large else
                    (f"FP64 flop model (SURVEY.md 8d): {pbs_flops(p):,.0f} flop per PBS x {units_per_launch} PBS per "
                     f"launch / the kernel's average launch duration")),
          "traffic_note": ("L2<->fabric bytes per launch of this kernel (2 FETCH_SIZE + WRITE_SIZE, gfx950 correction; "

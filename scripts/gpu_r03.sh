@@ -32,6 +32,8 @@ for s in $STAGES; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 900 python -u bench.py ;;
     bench:*) step bench_${s#bench:} 600 python -u bench.py $(kargs ${s#bench:}) ;;
+    # ab:<tag>:<VAR>=<value>: the bench of <tag> under one engine environment switch (A/B)
+    ab:*) r=${s#ab:}; t=${r%%:*}; kv=${r#*:}; step ab_${t}_${kv//=/_} 600 env "$kv" python -u bench.py $(kargs $t) --no-cpu-baseline --no-host-abi ;;
     # the N = 32768, L = 2 CMUX through the split path instead of the grouped one (A/B)
     splitab:*) step splitab_${s#splitab:} 600 env TFHE_MI355_LARGE_SPLIT=1 python -u bench.py $(kargs ${s#splitab:}) --no-cpu-baseline --no-host-abi ;;
     kstats:*) t=${s#kstats:}; step kstats_$t 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kstats_$t -o run \

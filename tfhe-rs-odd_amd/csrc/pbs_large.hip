@@ -483,6 +483,197 @@ __global__ void __launch_bounds__((LargeSubCfg<K, L>::THREADS), (G ? 1 : 2)) lar
 }
 
 // ---------------------------------------------------------------------------------------
+// Paired sub-block kernel (split CMUX, L <= 2).  The MAC needs the GGSW operands of
+// every (level, row, column, frequency) -- for multi-bit the 2^g GGSWs of the group, 1 MiB per
+// sub-block at g = 3, k = 1, L = 2.  One workgroup per sub-block q and PAIR of ciphertexts,
+// 2 (k+1) L waves:
+//   phase 1  wave (c, p): forward sub-FFT of polynomial p of ciphertext c, published to LDS;
+//   phase 2  wave w owns spectrum slots SPW w .. SPW w + SPW - 1 of BOTH ciphertexts and all
+//            columns: per (slot, level, column) it loads the (k+1) (x 2^g) operands once (so each
+//            GGSW byte is read once per pair of ciphertexts), builds each ciphertext's keybundle
+//            entries with its own monomials (multi-bit) and MACs them into registers; the slot's outputs go
+//            over the (level 1, row = column) spectra, which no other wave reads;
+//   phase 3  wave (c, column), c < 2: inverse sub-FFT, store to the spectra scratch.
+// Every wave of the 2 (k+1) L works in phases 1 and 2 (the single-ciphertext kernel above leaves
+// L - 1 of every L waves idle in its MAC), the operands of the next (level, column) are in flight
+// while the current one is consumed, and at R <= 8 all workgroups of sub-block q run on the XCDs
+// x = q (mod R), so a group's GGSW slice stays in their L2.  Per (ciphertext, column, frequency)
+// the arithmetic and its order are those of large_sub_kernel (keybundle in selector order, MAC
+// over levels L..1 and rows 0..k), so the outputs are bit-identical.
+// ---------------------------------------------------------------------------------------
+template <int K, int L>
+struct PairSubCfg {
+    static constexpr int CPW = 2;                    // ciphertexts per workgroup
+    static constexpr int PW = (K + 1) * L;           // polynomials per ciphertext
+    static constexpr int WAVES = CPW * PW;
+    static constexpr int THREADS = 64 * WAVES;
+    static constexpr int SPW = 16 / WAVES;           // phase-2 slots per wave
+    static_assert(16 % WAVES == 0, "slots split evenly over the waves");
+    static constexpr int S1 = WAVES * SubFft::XL;    // twiddle table offset (double2 units)
+    static constexpr size_t LDS = sizeof(double2) * (S1 + SubFft::Lds::s1_len);
+    static_assert(LDS <= 160 * 1024, "LDS per workgroup exceeds a CU");
+};
+
+// workgroup -> (sub-block q, ciphertext pair cp): at R <= 8 XCD x = b % 8 serves q = x % R only
+template <int R>
+__device__ __forceinline__ void pair_sub_block_of(int b, int &q, int &cp) {
+    const int x = b & 7, y = b >> 3;
+    if constexpr (R >= 8) {
+        q = x + 8 * (y % (R / 8));
+        cp = y / (R / 8);
+    } else {
+        q = x % R;
+        cp = y * (8 / R) + x / R;
+    }
+}
+template <int R>
+constexpr unsigned pair_sub_blocks(int pairs) {
+    return R >= 8 ? (unsigned)pairs * R : (unsigned)((pairs + 8 / R - 1) / (8 / R)) * 8u;
+}
+
+// SB: (level, column) operand batches per scheduling region (loads of SB batches in flight)
+template <int N, int K, int L, int G, int SB>
+__global__ void __launch_bounds__((PairSubCfg<K, L>::THREADS), 2) large_pair_sub_kernel(LargePbsLaunch a, int ct0, int i) {
+    using Cfg = PairSubCfg<K, L>;
+    using S = Split<N>;
+    constexpr int M = S::M, R = S::R;
+    constexpr int NSEL = G ? 1 << G : 1;
+    constexpr int CPW = Cfg::CPW, PW = Cfg::PW, SPW = Cfg::SPW;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double2 *lds = reinterpret_cast<double2 *>(smem);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int q, cp;
+    pair_sub_block_of<R>(blockIdx.x, q, cp);
+    const int cnt = a.chunk_count;
+    if (2 * cp >= cnt) return;  // whole workgroup
+    double2 *s1 = lds + Cfg::S1;
+    for (int e = threadIdx.x; e < SubFft::Lds::s1_len; e += Cfg::THREADS) s1[e] = a.W[R * (e & 63) * ((e >> 6) + 1)];
+    const SubFft::Lds tw{s1, s1};
+    WaveLocalSync wsync;
+    auto buf = [&](int c, int p) { return reinterpret_cast<cx *>(lds) + (c * PW + p) * SubFft::XL; };
+    auto ct_of = [&](int c) { return min(2 * cp + c, cnt - 1); };  // idle slot: a valid ciphertext
+    auto spectra = [&](int c) { return a.spectra + (size_t)ct_of(c) * L * (K + 1) * M; };
+
+    // ---- phase 1: forward sub-FFT of polynomial p of ciphertext c ----
+    {
+        const int c = wave / PW, p = wave % PW;
+        cx v[16];
+        const double2 *src = spectra(c) + (size_t)p * M + 1024 * q + lane;
+#pragma unroll
+        for (int b = 0; b < 16; b++) v[b] = gld(src + 64 * b);
+        __syncthreads();  // twiddle table
+        cx *xb = buf(c, p);
+        SubFft::forward(v, xb, tw, lane, wsync);
+        wsync();
+#pragma unroll
+        for (int s = 0; s < 16; s++) reinterpret_cast<double2 *>(xb)[s * 64 + lane] = make_double2(v[s].re, v[s].im);
+    }
+    // monomial degrees of each ciphertext's 2^g - 1 non-constant GGSWs (wave-uniform)
+    uint32_t deg[CPW][NSEL];
+#pragma unroll
+    for (int c = 0; c < (G ? CPW : 0); c++) {
+        const uint64_t *in = a.lwe_in + (size_t)(ct0 + ct_of(c)) * (a.n + 1) + (size_t)i * G;
+#pragma unroll
+        for (int sel = 1; sel < NSEL; sel++) {
+            uint64_t d = 0;
+#pragma unroll
+            for (int b = 0; b < G; b++)
+                if ((sel >> (G - 1 - b)) & 1) d += in[b];
+            deg[c][sel] = pbs_modulus_switch<S::LOGN>(d);
+        }
+    }
+    // the group's 2^g GGSWs through a buffer resource: element (sel, lvl, r, col, position) at
+    // ((sel L + lvl - 1) (K+1) + r) (K+1) M + col M + position
+    constexpr size_t ggsw_len = (size_t)L * (K + 1) * (K + 1) * M;
+    constexpr uint32_t rowb = 16u * (uint32_t)((K + 1) * M);
+    const __amdgpu_buffer_rsrc_t grs = make_rsrc(a.fbsk + (size_t)i * NSEL * ggsw_len);
+    const uint32_t gvo = 16u * (uint32_t)(1024 * q + lane);
+    const uint32_t fl = (uint32_t)q + (uint32_t)R * SubFft::freq_lane(lane);
+    __syncthreads();  // spectra published
+
+    // ---- phase 2: keybundle + MAC of this wave's slots for both ciphertexts ----
+#pragma unroll
+    for (int si = 0; si < SPW; si++) {
+        const int s = wave * SPW + si;  // wave-uniform
+        const uint32_t f = fl + (uint32_t)R * SubFft::freq_slot(s);
+        cx mono[CPW][NSEL];
+#pragma unroll
+        for (int c = 0; c < CPW; c++)
+#pragma unroll
+            for (int sel = 1; sel < NSEL; sel++) mono[c][sel] = mono_spectrum<N>(a.twist, deg[c][sel], f);
+        cx o[CPW][K + 1];
+#pragma unroll
+        for (int lvl = L; lvl >= 1; lvl--) {
+            cx ff[CPW][K + 1];
+#pragma unroll
+            for (int c = 0; c < CPW; c++)
+#pragma unroll
+                for (int r = 0; r <= K; r++) {
+                    const double2 t = reinterpret_cast<const double2 *>(buf(c, (lvl - 1) * (K + 1) + r))[s * 64 + lane];
+                    ff[c][r] = cx{t.x, t.y};
+                }
+#pragma unroll
+            for (int col = 0; col <= K; col++) {
+                if (((L - lvl) * (K + 1) + col) % SB == 0) __builtin_amdgcn_sched_barrier(0);
+                double2 g[K + 1][NSEL];
+#pragma unroll
+                for (int r = 0; r <= K; r++)
+#pragma unroll
+                    for (int sel = 0; sel < NSEL; sel++)
+                        g[r][sel] = buffer_ld_d2(grs, gvo,
+                                                 (uint32_t)(16u * sel * ggsw_len) + (uint32_t)((lvl - 1) * (K + 1) + r) * rowb +
+                                                     16u * (uint32_t)(col * M) + 1024u * (uint32_t)s);
+#pragma unroll
+                for (int c = 0; c < CPW; c++) {
+#pragma unroll
+                    for (int r = 0; r <= K; r++) {
+                        double2 kb = g[r][0];
+#pragma unroll
+                        for (int sel = 1; sel < NSEL; sel++) {
+                            kb.x = fma(g[r][sel].x, mono[c][sel].re, fma(-g[r][sel].y, mono[c][sel].im, kb.x));
+                            kb.y = fma(g[r][sel].x, mono[c][sel].im, fma(g[r][sel].y, mono[c][sel].re, kb.y));
+                        }
+                        cx &oc = o[c][col];
+                        if (lvl == L && r == 0) {
+                            oc.re = fma(kb.x, ff[c][r].re, -(kb.y * ff[c][r].im));
+                            oc.im = fma(kb.x, ff[c][r].im, kb.y * ff[c][r].re);
+                        } else {
+                            oc.re = fma(kb.x, ff[c][r].re, fma(-kb.y, ff[c][r].im, oc.re));
+                            oc.im = fma(kb.x, ff[c][r].im, fma(kb.y, ff[c][r].re, oc.im));
+                        }
+                    }
+                }
+            }
+        }
+        // outputs over the (level 1, row = column) spectra of slot s: read only by this wave, and
+        // every read of slot s is above
+#pragma unroll
+        for (int c = 0; c < CPW; c++)
+#pragma unroll
+            for (int col = 0; col <= K; col++)
+                reinterpret_cast<double2 *>(buf(c, col))[s * 64 + lane] = make_double2(o[c][col].re, o[c][col].im);
+    }
+    __syncthreads();
+    // ---- phase 3: inverse sub-FFT of column col of ciphertext c ----
+    if (wave >= CPW * (K + 1)) return;
+    const int c = wave / (K + 1), col = wave % (K + 1);
+    cx *xb = buf(c, col);
+    cx v[16];
+#pragma unroll
+    for (int s = 0; s < 16; s++) {
+        const double2 t = reinterpret_cast<const double2 *>(xb)[s * 64 + lane];
+        v[s] = cx{t.x, t.y};
+    }
+    wsync();
+    SubFft::inverse(v, xb, tw, lane, wsync);
+    if (2 * cp + c >= cnt) return;
+    double2 *dst = spectra(c) + (size_t)col * M + 1024 * q + lane;  // (lvl 1, row col) slot: this WG only
+#pragma unroll
+    for (int b = 0; b < 16; b++) dst[64 * b] = make_double2(v[b].re, v[b].im);
+}
+
+// ---------------------------------------------------------------------------------------
 // Grouped CMUX (k = 1, L = 2).  The top DIF radix-16 is R4 over stride 4, twiddles
 // omega_16^{A c}, R4 (dft16_fwd): its outputs c = G, G+4, G+8, G+12 come from ONE second-layer
 // R4, which needs only output G of each first-layer R4.  So a workgroup per (ciphertext, group G,
@@ -1026,6 +1217,26 @@ static bool large_grouped_enabled() {
     return v;
 }
 
+// TFHE_MI355_SUB_OLD=1: the split CMUX through the one-ciphertext large_sub_kernel at every L
+// (A/B switch; L = 3 always uses it)
+static bool large_sub_old() {
+    static const bool v = [] {
+        const char *e = std::getenv("TFHE_MI355_SUB_OLD");
+        return e && e[0] && e[0] != '0';
+    }();
+    return v;
+}
+
+// TFHE_MI355_PAIR_SB = 1 / 2 / 4: operand batches per scheduling region of large_pair_sub_kernel
+static int large_pair_sb() {
+    static const int v = [] {
+        const char *e = std::getenv("TFHE_MI355_PAIR_SB");
+        const int x = e ? std::atoi(e) : 1;
+        return x == 2 || x == 4 ? x : 1;
+    }();
+    return v;
+}
+
 template <int N, int K, int L, int G = 0>
 static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
     using S = Split<N>;
@@ -1077,11 +1288,25 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
                 TimedLaunch tl(a.timer, "large_top_fwd_kernel", s);
                 hipLaunchKernelGGL((large_top_fwd_kernel<N, K, L, G>), dim3(fwd_blocks), dim3(TOPT), 0, s, a, ct0, i);
             }
+            if constexpr (16 % (2 * (K + 1) * L) == 0) {  // L <= 2 at k = 1
+                if (!large_sub_old()) {
+                    using PairSub = PairSubCfg<K, L>;
+                    TimedLaunch tl(a.timer, "large_pair_sub_kernel", s);
+                    const dim3 grid(pair_sub_blocks<S::R>((cnt + 1) / 2)), block(PairSub::THREADS);
+                    switch (large_pair_sb()) {
+                        case 2: hipLaunchKernelGGL((large_pair_sub_kernel<N, K, L, G, 2>), grid, block, PairSub::LDS, s, a, ct0, i); break;
+                        case 4: hipLaunchKernelGGL((large_pair_sub_kernel<N, K, L, G, 4>), grid, block, PairSub::LDS, s, a, ct0, i); break;
+                        default: hipLaunchKernelGGL((large_pair_sub_kernel<N, K, L, G, 1>), grid, block, PairSub::LDS, s, a, ct0, i);
+                    }
+                    goto sub_done;
+                }
+            }
             {
                 TimedLaunch tl(a.timer, "large_sub_kernel", s);
                 hipLaunchKernelGGL((large_sub_kernel<N, K, L, G>), dim3(sub_blocks), dim3(Sub::THREADS), Sub::LDS, s,
                                    a, ct0, i);
             }
+        sub_done:
             TimedLaunch tl(a.timer, "large_top_inv_kernel", s);
             hipLaunchKernelGGL((large_top_inv_kernel<N, K, G>), dim3(top_blocks), dim3(TOPT), 0, s, a, ct0, i);
         }
