@@ -122,13 +122,13 @@ def _split_params():
         out[f"mb3_3g{g}"] = (name, f"shortint apply_lookup_table (keyswitch -> multi-bit PBS, grouping {g}) at {name} "
                                    f"(shortint/parameters/multi_bit.rs:{line}), N={p.polynomial_size}, batch per GPU; "
                                    "the reference publishes no number for this set",
-                             f"large_mb_sub_kernel<{p.polynomial_size},1,{p.pbs_level},{g},1> (+ large_top_fwd/top_inv "
+                             f"large_pair_sub_kernel<{p.polynomial_size},1,{p.pbs_level},{g},1> (+ large_top_fwd/top_inv "
                              "per group, ks_mfma_kernel)")
     return out
 
 
 PARAMS.update(_split_params())
-SPLIT_TAGS = {t for t, v in PARAMS.items() if v[2].startswith(("large_sub_kernel", "large_mb_sub_kernel"))}
+SPLIT_TAGS = {t for t, v in PARAMS.items() if v[2].startswith(("large_sub_kernel", "large_pair_sub_kernel"))}
 WITH_KS = {"4_4", "2_2ks"} | SPLIT_TAGS
 
 
@@ -837,7 +837,8 @@ def host_abi_rate(eng, P, cts, acc, with_ks: bool, reps: int = 3) -> dict:
                      "directly, same outputs); PCIe-inclusive, rank 0's GPU, not the headline value")}
 
 
-def single_ct_rates(eng, cts, acc, with_ks: bool, batched_rate: float, secs: float = 2.0) -> dict:
+def single_ct_rates(eng, cts, acc, with_ks: bool, batched_rate: float, secs: float = 2.0,
+                    callers=(1, 16, 64, 256)) -> dict:
     """The reference's own calling pattern through the synchronous host-pointer ABI: ONE ciphertext
     per call (keyswitch_programmable_bootstrap_assign, shortint/server_key/mod.rs:783-857), from T
     native threads at once (rayon workers, radix_parallel/mul.rs:347-407), each issuing its next
@@ -859,7 +860,8 @@ def single_ct_rates(eng, cts, acc, with_ks: bool, batched_rate: float, secs: flo
     u64p = ctypes.POINTER(ctypes.c_uint64)
     res = {"entry_point": ("tfhe_mi355_keyswitch_programmable_bootstrap" if with_ks
                            else "tfhe_mi355_programmable_bootstrap"), "callers": {}}
-    for T in (1, 16, 64, 256):
+    for T in callers:
+        eng.coalesce_stats(reset=True)
         calls, bad, fails = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         wall, lat = ctypes.c_double(), ctypes.c_double()
         rc = lg.tfhe_mi355_loadgen_run(
@@ -873,8 +875,10 @@ def single_ct_rates(eng, cts, acc, with_ks: bool, batched_rate: float, secs: flo
         res["callers"][str(T)] = {"value": rate, "frac_of_batched_device_rate": rate / batched_rate,
                                   "mean_call_latency_ms": lat.value * 1e3,
                                   "little_bound": T / lat.value if lat.value else None,
-                                  "calls": calls.value, "mismatching_rows": bad.value, "failed_calls": fails.value}
-    res["single_call_latency_ms"] = res["callers"]["1"]["mean_call_latency_ms"]
+                                  "calls": calls.value, "mismatching_rows": bad.value, "failed_calls": fails.value,
+                                  "coalescing": eng.coalesce_stats()}
+    if "1" in res["callers"]:
+        res["single_call_latency_ms"] = res["callers"]["1"]["mean_call_latency_ms"]
     res["note"] = ("T native threads (libtfhe_mi355_loadgen), closed loop, count = 1 per call, every output "
                    "compared with a batched call's row; T callers cannot exceed T / latency (little_bound); "
                    "the batched device rate is the headline step's")

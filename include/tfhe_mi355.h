@@ -85,6 +85,13 @@ int tfhe_mi355_kernel_timing_enable(TfheMi355Context *ctx, int every);
 int tfhe_mi355_kernel_timing_entry(TfheMi355Context *ctx, size_t index, char *name, size_t name_len,
                                    double *total_ms, uint64_t *launches);
 
+/* Request-coalescing counters of this context (all ops): batches run, ciphertexts in them, the
+ * most batches in flight at once, and the summed wall time of the batches (staging, copies,
+ * kernels, sync); `reset` != 0 clears them after reading.  Profiling aid, no reference
+ * counterpart (the reference has no batching layer). */
+int tfhe_mi355_coalesce_stats(TfheMi355Context *ctx, int reset, uint64_t *batches, uint64_t *rows,
+                              uint64_t *max_in_flight, double *batch_seconds);
+
 /* Page-locked (pinned) host memory for batch buffers.  The synchronous host-pointer entry points
  * detect pinned input/output buffers and DMA them directly, chunk by chunk, overlapped with the
  * kernels (no host staging copies); pageable buffers go through the engine's pinned staging.

@@ -12,14 +12,15 @@ case $tag in
   mb3)   K='pbs_multibit'; U='pbs_multibit'; UPD=4096; M='pbs_multibit'; ARGS="--params mb3" ;;
   mb2)   K='pbs_multibit'; U='pbs_multibit'; UPD=4096; M='pbs_multibit'; ARGS="--params mb2" ;;
   4_4)   K='large_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=128; M='large_group_cmux_kernel'; ARGS="--params 4_4 --batch 128" ;;
-  3_3)   K='large_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=1024; M='large_sub_kernel|large_group'; ARGS="--params 3_3 --batch 1024" ;;
-  mb3_3g2|mb3_3g3) K='large_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=1024; M='large_sub_kernel'; ARGS="--params $tag --batch 1024" ;;
+  3_3)   K='large_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=384; M='large_sub_kernel|large_pair_sub_kernel'; ARGS="--params 3_3 --batch 384" ;;
+  mb3_3g2|mb3_3g3) K='large_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=384; M='large_pair_sub_kernel|large_sub_kernel'; ARGS="--params $tag --batch 384" ;;
   *) echo "unknown tag $tag"; exit 2 ;;
 esac
 B="$ARGS --steps 2 --warmup 1 --no-cpu-baseline --no-host-abi"
 run() {  # run NAME COUNTERS...
   local n=$1; shift
-  timeout -s KILL 240 rocprofv3 --pmc "$@" -d gpurun_out/pmc_$tag/$n -o run --output-format csv -- python3 bench.py $B \
+  # counters only for the workload's own kernels (copy / fill kernels of the runtime excluded)
+  timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-include-regex "$K" -d gpurun_out/pmc_$tag/$n -o run --output-format csv -- python3 bench.py $B \
     > gpurun_out/pmc_$tag/$n.log 2>&1
   local rc=$?; echo "pmc $tag $n rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/pmc_$tag/$n.log; exit $rc; }
 }

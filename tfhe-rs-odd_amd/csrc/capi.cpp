@@ -171,6 +171,9 @@ struct TfheMi355Context {
             DeviceBuffer d_in, d_out, d_luts, d_idx, d_scratch;
             bool busy = false;
         } slots[8];
+        // statistics (tfhe_mi355_coalesce_stats), under m
+        uint64_t batches = 0, rows = 0, in_flight = 0, max_in_flight = 0;
+        double batch_seconds = 0;
     } co;
     KernelTimer *timer_or_null() { return timer.every > 0 ? &timer : nullptr; }
 
@@ -815,15 +818,22 @@ void coalesced_call(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
             return false;
         });
         sl->busy = true;
+        co.max_in_flight = std::max(co.max_in_flight, ++co.in_flight);
         lk.unlock();
         std::string err;
+        const auto t0 = std::chrono::steady_clock::now();
         try {
             run_coalesced_batch(c, *sl, op, batch);
         } catch (const std::exception &ex) {
             err = ex.what();
         }
+        const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         lk.lock();
         sl->busy = false;
+        co.in_flight--;
+        co.batches++;
+        co.rows += cts;
+        co.batch_seconds += dt;
         for (auto *x : batch) {
             x->err = err;
             x->done = true;
@@ -878,6 +888,24 @@ int tfhe_mi355_kernel_timing_entry(TfheMi355Context *ctx, size_t index, char *na
         std::snprintf(name, name_len, "%s", it->first.c_str());
         *total_ms = it->second.first;
         *launches = it->second.second;
+    });
+}
+
+int tfhe_mi355_coalesce_stats(TfheMi355Context *ctx, int reset, uint64_t *batches, uint64_t *rows,
+                              uint64_t *max_in_flight, double *batch_seconds) {
+    return guarded([&] {
+        if (!ctx || !batches || !rows || !max_in_flight || !batch_seconds) fail("null argument");
+        auto &co = ctx->co;
+        std::lock_guard<std::mutex> g(co.m);
+        *batches = co.batches;
+        *rows = co.rows;
+        *max_in_flight = co.max_in_flight;
+        *batch_seconds = co.batch_seconds;
+        if (reset) {
+            co.batches = co.rows = 0;
+            co.max_in_flight = co.in_flight;
+            co.batch_seconds = 0;
+        }
     });
 }
 

@@ -364,14 +364,12 @@ __device__ __forceinline__ cx mono_spectrum(const double2 *__restrict__ twist, u
     }
 }
 
-// the multi-bit keybundle (2^g operands per GGSW element) needs more than the 256 registers of
-// two waves per SIMD: one wave per SIMD there
-template <int N, int K, int L, int G>
-__global__ void __launch_bounds__((LargeSubCfg<K, L>::THREADS), (G ? 1 : 2)) large_sub_kernel(LargePbsLaunch a, int ct0, int i) {
+// classic CMUX sub-blocks (the multi-bit sets run large_pair_sub_kernel below)
+template <int N, int K, int L>
+__global__ void __launch_bounds__((LargeSubCfg<K, L>::THREADS), 2) large_sub_kernel(LargePbsLaunch a, int ct0, int i) {
     using Cfg = LargeSubCfg<K, L>;
     using S = Split<N>;
     constexpr int M = S::M, R = S::R;
-    constexpr int NSEL = G ? 1 << G : 1;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double2 *lds = reinterpret_cast<double2 *>(smem);
     const int lane = threadIdx.x & 63;
@@ -400,67 +398,19 @@ __global__ void __launch_bounds__((LargeSubCfg<K, L>::THREADS), (G ? 1 : 2)) lar
     __syncthreads();
     const bool mac = wave <= K;  // wave c computes output column c
     if (mac) {
-        // column c: sum over levels L..1 and rows 0..k (ggsw.rs:524-567), oracle order.  Multi-bit:
-        // the GGSW is the keybundle KB_i = GGSW_0 + sum_sel X^{deg_sel} GGSW_sel, built per
-        // frequency in selector order (the oracle's mb_keybundle; key layout [n/g][2^g][L][k+1][k+1])
+        // column c: sum over levels L..1 and rows 0..k (ggsw.rs:524-567), oracle order
         constexpr size_t ggsw_len = (size_t)L * (K + 1) * (K + 1) * M;
-        const double2 *Gp = a.fbsk + (size_t)i * NSEL * ggsw_len + (size_t)wave * M + 1024 * q + lane;
-        // multi-bit: the 2^g GGSWs of the group through a buffer resource (wave-uniform base and
-        // scalar offsets per selector / row / slot, one per-lane VGPR offset), so the 2^g x 4
-        // operand addresses per slot cost no VALU and are not precomputed into registers
-        const __amdgpu_buffer_rsrc_t grs = make_rsrc(a.fbsk + (size_t)i * NSEL * ggsw_len);
-        const uint32_t gvo = 16u * (uint32_t)((size_t)wave * M + 1024 * q + lane);
-        uint32_t deg[NSEL];
-        if constexpr (G > 0) {
-            const uint64_t *in = a.lwe_in + (size_t)(ct0 + cl) * (a.n + 1) + (size_t)i * G;
-#pragma unroll
-            for (int sel = 1; sel < NSEL; sel++) {
-                uint64_t d = 0;
-#pragma unroll
-                for (int b = 0; b < G; b++)
-                    if ((sel >> (G - 1 - b)) & 1) d += in[b];
-                deg[sel] = pbs_modulus_switch<S::LOGN>(d);
-            }
-        }
-        const uint32_t fl = (uint32_t)q + (uint32_t)R * SubFft::freq_lane(lane);
-        uint32_t gw = gvo;  // per-slot opaque copy of the GGSW lane offset (issue window)
+        const double2 *Gp = a.fbsk + (size_t)i * ggsw_len + (size_t)wave * M + 1024 * q + lane;
 #pragma unroll
         for (int s = 0; s < 16; s++) {
-            // bound the loads in flight: LARGE_MAC_SB slots per region; one slot (2^g GGSW
-            // operands per row and level) for the multi-bit keybundle
-            if (G > 0 || s % LARGE_MAC_SB == 0) __builtin_amdgcn_sched_barrier(0);
-            cx mono[NSEL];
-            if constexpr (G > 0) {
-                // issue window: slot s's monomial gathers take their index from an opaque copy that
-                // depends on slot s-2's result (hoisted all at once, the 2^g x 16 gathers spill)
-                uint32_t fw = fl;
-                gw = gvo;
-                if (s >= 2) asm volatile("" : "+v"(fw), "+v"(gw) : "v"(v[s >= 2 ? s - 2 : 0].re));
-                const uint32_t f = fw + (uint32_t)R * SubFft::freq_slot(s);  // frequency of (q, lane, s)
-#pragma unroll
-                for (int sel = 1; sel < NSEL; sel++) mono[sel] = mono_spectrum<N>(a.twist, deg[sel], f);
-            }
+            if (s % LARGE_MAC_SB == 0) __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight
             cx o{0.0, 0.0};
 #pragma unroll
             for (int lvl = L; lvl >= 1; lvl--) {
 #pragma unroll
                 for (int r = 0; r <= K; r++) {
                     const int p = (lvl - 1) * (K + 1) + r;
-                    double2 gg;
-                    if constexpr (G > 0) {
-                        __builtin_amdgcn_sched_barrier(0);  // one (level, row) of 2^g operands in flight
-                        constexpr uint32_t rowb = 16u * (uint32_t)((K + 1) * M);
-                        gg = buffer_ld_d2(grs, gw, (uint32_t)p * rowb + 1024u * (uint32_t)s);
-#pragma unroll
-                        for (int sel = 1; sel < NSEL; sel++) {
-                            const double2 g2 = buffer_ld_d2(grs, gw, (uint32_t)(16u * sel * ggsw_len) + (uint32_t)p * rowb +
-                                                                          1024u * (uint32_t)s);
-                            gg.x = fma(g2.x, mono[sel].re, fma(-g2.y, mono[sel].im, gg.x));
-                            gg.y = fma(g2.x, mono[sel].im, fma(g2.y, mono[sel].re, gg.y));
-                        }
-                    } else {
-                        gg = Gp[(size_t)p * (K + 1) * M + s * 64];
-                    }
+                    const double2 gg = Gp[(size_t)p * (K + 1) * M + s * 64];
                     const double2 ff = reinterpret_cast<const double2 *>(lds)[p * SubFft::XL + s * 64 + lane];
                     if (lvl == L && r == 0) {
                         o.re = fma(gg.x, ff.x, -(gg.y * ff.y));
@@ -1217,22 +1167,11 @@ static bool large_grouped_enabled() {
     return v;
 }
 
-// TFHE_MI355_SUB_OLD=1: the split CMUX through the one-ciphertext large_sub_kernel at every L
-// (A/B switch; L = 3 always uses it)
-static bool large_sub_old() {
+// TFHE_MI355_PAIR_SUB=1: the classic split CMUX (L <= 2) through large_pair_sub_kernel too (A/B)
+static bool large_pair_sub_classic() {
     static const bool v = [] {
-        const char *e = std::getenv("TFHE_MI355_SUB_OLD");
+        const char *e = std::getenv("TFHE_MI355_PAIR_SUB");
         return e && e[0] && e[0] != '0';
-    }();
-    return v;
-}
-
-// TFHE_MI355_PAIR_SB = 1 / 2 / 4: operand batches per scheduling region of large_pair_sub_kernel
-static int large_pair_sb() {
-    static const int v = [] {
-        const char *e = std::getenv("TFHE_MI355_PAIR_SB");
-        const int x = e ? std::atoi(e) : 1;
-        return x == 2 || x == 4 ? x : 1;
     }();
     return v;
 }
@@ -1288,25 +1227,32 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
                 TimedLaunch tl(a.timer, "large_top_fwd_kernel", s);
                 hipLaunchKernelGGL((large_top_fwd_kernel<N, K, L, G>), dim3(fwd_blocks), dim3(TOPT), 0, s, a, ct0, i);
             }
-            if constexpr (16 % (2 * (K + 1) * L) == 0) {  // L <= 2 at k = 1
-                if (!large_sub_old()) {
-                    using PairSub = PairSubCfg<K, L>;
-                    TimedLaunch tl(a.timer, "large_pair_sub_kernel", s);
-                    const dim3 grid(pair_sub_blocks<S::R>((cnt + 1) / 2)), block(PairSub::THREADS);
-                    switch (large_pair_sb()) {
-                        case 2: hipLaunchKernelGGL((large_pair_sub_kernel<N, K, L, G, 2>), grid, block, PairSub::LDS, s, a, ct0, i); break;
-                        case 4: hipLaunchKernelGGL((large_pair_sub_kernel<N, K, L, G, 4>), grid, block, PairSub::LDS, s, a, ct0, i); break;
-                        default: hipLaunchKernelGGL((large_pair_sub_kernel<N, K, L, G, 1>), grid, block, PairSub::LDS, s, a, ct0, i);
+            if constexpr (G > 0) {
+                // multi-bit: the paired kernel (3283 -> 8921 KS+PBS/s at
+                // PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_3; for the classic sets it measured slower
+                // than large_sub_kernel: 4640 vs 4895 KS+PBS/s at 3_3, 939 vs 1036 at 4_4 split)
+                using PairSub = PairSubCfg<K, L>;
+                TimedLaunch tl(a.timer, "large_pair_sub_kernel", s);
+                hipLaunchKernelGGL((large_pair_sub_kernel<N, K, L, G, 1>), dim3(pair_sub_blocks<S::R>((cnt + 1) / 2)),
+                                   dim3(PairSub::THREADS), PairSub::LDS, s, a, ct0, i);
+            } else {
+                bool paired = false;
+                if constexpr (16 % (2 * (K + 1) * L) == 0) {  // L <= 2 at k = 1
+                    if (large_pair_sub_classic()) {
+                        using PairSub = PairSubCfg<K, L>;
+                        TimedLaunch tl(a.timer, "large_pair_sub_kernel", s);
+                        hipLaunchKernelGGL((large_pair_sub_kernel<N, K, L, G, 1>),
+                                           dim3(pair_sub_blocks<S::R>((cnt + 1) / 2)), dim3(PairSub::THREADS),
+                                           PairSub::LDS, s, a, ct0, i);
+                        paired = true;
                     }
-                    goto sub_done;
+                }
+                if (!paired) {
+                    TimedLaunch tl(a.timer, "large_sub_kernel", s);
+                    hipLaunchKernelGGL((large_sub_kernel<N, K, L>), dim3(sub_blocks), dim3(Sub::THREADS), Sub::LDS, s,
+                                       a, ct0, i);
                 }
             }
-            {
-                TimedLaunch tl(a.timer, "large_sub_kernel", s);
-                hipLaunchKernelGGL((large_sub_kernel<N, K, L, G>), dim3(sub_blocks), dim3(Sub::THREADS), Sub::LDS, s,
-                                   a, ct0, i);
-            }
-        sub_done:
             TimedLaunch tl(a.timer, "large_top_inv_kernel", s);
             hipLaunchKernelGGL((large_top_inv_kernel<N, K, G>), dim3(top_blocks), dim3(TOPT), 0, s, a, ct0, i);
         }

@@ -161,6 +161,17 @@ class Engine:
             i += 1
         return out
 
+    def coalesce_stats(self, reset: bool = False) -> dict:
+        """Request-coalescing counters: batches, ciphertexts, most batches in flight, batch wall
+        seconds (summed); `reset` clears them after reading."""
+        b, r, m = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        t = ctypes.c_double()
+        _lib.call("tfhe_mi355_coalesce_stats", self._h, int(bool(reset)), ctypes.byref(b), ctypes.byref(r),
+                  ctypes.byref(m), ctypes.byref(t))
+        return {"batches": b.value, "rows": r.value, "max_in_flight": m.value, "batch_seconds": t.value,
+                "mean_batch_rows": r.value / b.value if b.value else None,
+                "mean_batch_ms": 1e3 * t.value / b.value if b.value else None}
+
     # -- host (numpy) batched ops ---------------------------------------------------------
     def _luts(self, luts):
         luts = _u64(luts)
