@@ -110,7 +110,7 @@ def _split_params():
         out[tag] = (name, f"shortint apply_lookup_table (keyswitch -> PBS) at {name} (shortint/parameters/mod.rs:"
                           f"{SHORTINT_SOURCE_LINE[name]}), N={p.polynomial_size}, batch per GPU; the reference publishes "
                           + ("121 ms per KS+PBS at 3_3 (benchmarks.md:42)" if tag == "3_3" else "no number for this set"),
-                    f"large_sub_kernel<{p.polynomial_size},1,{p.pbs_level},0> (+ large_top_fwd/top_inv per CMUX, "
+                    f"large_sub_kernel<{p.polynomial_size},1,{p.pbs_level}> (+ large_top_fwd/top_inv per CMUX, "
                     "ks_mfma_kernel)")
     # the multi-bit sets at N = 8192 (shortint/parameters/multi_bit.rs:134-153, 192-210): the split
     # CMUX with the keybundle built inside large_sub_kernel, one CMUX per group of g

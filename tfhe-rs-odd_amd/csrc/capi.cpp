@@ -682,9 +682,13 @@ size_t coalesce_batch() {
     static const size_t v = std::max<size_t>(env_size("TFHE_MI355_COALESCE_BATCH", 1024), 1);
     return v;
 }
-// batch slots in use (up to 8): batches in flight at once, each on its own stream
+// batch slots in use (up to 8): batches in flight at once, each on its own stream.  A PBS batch
+// takes about one CMUX chain (~8 ms at 2_2) whatever its size up to a chip-full, so by Little's
+// law T callers get at most T / (chain + window) calls/s; more slots only split the callers into
+// smaller concurrent batches, which the device runs less than fully concurrently (measured at
+// 64 callers: 8 slots 21 ms per 16-row batch).  2: one batch gathers while one runs.
 size_t coalesce_slots() {
-    static const size_t v = std::min<size_t>(std::max<size_t>(env_size("TFHE_MI355_COALESCE_SLOTS", 8), 1), 8);
+    static const size_t v = std::min<size_t>(std::max<size_t>(env_size("TFHE_MI355_COALESCE_SLOTS", 2), 1), 8);
     return v;
 }
 std::chrono::microseconds coalesce_window() {
@@ -794,6 +798,19 @@ void coalesced_call(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
             continue;
         }
         co.collecting[op] = true;
+        // a free slot first, then the window: while every slot is busy the queue keeps growing
+        // and the next batch takes all of it (collecting first and then waiting for a slot left
+        // many collectors each holding a few rows: 4-row batches at 256 callers)
+        TfheMi355Context::Coalescer::Slot *sl = nullptr;
+        co.cv.wait(lk, [&] {
+            for (size_t q = 0; q < coalesce_slots(); q++)
+                if (!co.slots[q].busy) {
+                    sl = &co.slots[q];
+                    return true;
+                }
+            return false;
+        });
+        sl->busy = true;
         co.cv.wait_until(lk, std::chrono::steady_clock::now() + coalesce_window(),
                          [&] { return co.queued[op] >= cap; });
         std::vector<CoalescedReq *> batch;
@@ -808,16 +825,6 @@ void coalesced_call(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
         co.queued[op] -= cts;
         co.collecting[op] = false;  // the next batch can gather while this one runs
         co.cv.notify_all();
-        TfheMi355Context::Coalescer::Slot *sl = nullptr;
-        co.cv.wait(lk, [&] {
-            for (size_t q = 0; q < coalesce_slots(); q++)
-                if (!co.slots[q].busy) {
-                    sl = &co.slots[q];
-                    return true;
-                }
-            return false;
-        });
-        sl->busy = true;
         co.max_in_flight = std::max(co.max_in_flight, ++co.in_flight);
         lk.unlock();
         std::string err;
