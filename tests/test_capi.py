@@ -127,14 +127,3 @@ def test_unsupported_multi_bit_parameters_are_rejected():
     with pytest.raises(EngineError, match="multiple of grouping_factor"):
         Engine(mb.with_(lwe_dimension=889), 0)
 
-
-@pytest.mark.parametrize("name", ["PARAM_MULTI_BIT_MESSAGE_1_CARRY_1_GROUP_2_KS_PBS",
-                                  "PARAM_MULTI_BIT_MESSAGE_1_CARRY_1_GROUP_3_KS_PBS"])
-def test_multi_bit_sets_without_a_kernel_fail_loudly(name):
-    """The N = 512, k = 3 multi-bit sets (multi_bit.rs:96,154) have no kernel here: context creation
-    fails with an error naming the shape (no silent fallback)."""
-    from tfhe_mi355 import Engine, EngineError
-    from tfhe_mi355.parameters import MULTI_BIT_ALL
-
-    with pytest.raises(EngineError, match="multi-bit"):
-        Engine(MULTI_BIT_ALL[name], 0)

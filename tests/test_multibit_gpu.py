@@ -103,3 +103,41 @@ def test_multi_bit_full_batch_decrypts(orc, keys_mb, engine_mb):
     # spot-check a sample of the batch bit-exactly against the oracle
     sel = np.arange(0, 4096, 512)
     assert np.array_equal(got[sel], keys_mb.fbsk.pbs(cts[sel], acc, threads=8))
+
+
+@pytest.mark.parametrize("name", ["PARAM_MULTI_BIT_MESSAGE_1_CARRY_1_GROUP_2_KS_PBS",
+                                  "PARAM_MULTI_BIT_MESSAGE_1_CARRY_1_GROUP_3_KS_PBS"])
+def test_multi_bit_k3_sets_bit_exact(orc, name):
+    """The N = 512, k = 3 multi-bit sets (multi_bit.rs:96,154; per-ciphertext keybundle kernel):
+    KS -> PBS bit-exact against the oracle at n = 6, per-ciphertext LUTs, edge inputs, and the
+    full-n set decrypting to f(m)."""
+    from tfhe_mi355 import Engine, client
+    from tfhe_mi355.parameters import MULTI_BIT_ALL
+
+    for n in (6, None):
+        p = MULTI_BIT_ALL[name] if n is None else MULTI_BIT_ALL[name].with_(lwe_dimension=n)
+        N, k, g, space = p.polynomial_size, p.glwe_dimension, p.grouping_factor, p.message_modulus * p.carry_modulus
+        lwe_sk = client.gen_binary_key(121, 1, p.lwe_dimension)
+        glwe_sk = client.gen_binary_key(121, 2, p.big_lwe_dimension)
+        bsk = client.gen_multi_bit_bootstrap_key(122, lwe_sk, glwe_sk, k, N, p.pbs_base_log, p.pbs_level, g,
+                                                 p.glwe_modular_std_dev, threads=8)
+        ksk = client.gen_keyswitch_key(123, glwe_sk, lwe_sk, p.ks_base_log, p.ks_level, p.lwe_modular_std_dev)
+        eng = Engine(p, 0)
+        eng.upload_bootstrap_key(bsk)
+        eng.upload_keyswitch_key(ksk)
+        fs = [lambda x: (x + 1) % space, lambda x: (3 * x) % space]
+        luts = np.stack([orc.fill_accumulator(N, k, p.message_modulus, p.carry_modulus, f) for f in fs])
+        msgs = np.arange(8) % space
+        idx = (np.arange(8) % 2).astype(np.uint32)
+        big = orc.lwe_encrypt(124, glwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta), p.glwe_modular_std_dev)
+        out = eng.keyswitch_programmable_bootstrap(big, luts, lut_indexes=idx)
+        assert np.array_equal(decode(orc.lwe_decrypt(glwe_sk, out), p.delta) % space,
+                              [fs[i](m) for i, m in zip(idx, msgs)])
+        if n is not None:
+            fb = orc.MultiBitFourierBsk(bsk, p.lwe_dimension, k, N, p.pbs_base_log, p.pbs_level, g)
+            small = orc.keyswitch(ksk, p.big_lwe_dimension, p.lwe_dimension, p.ks_base_log, p.ks_level, big)
+            assert np.array_equal(out, fb.pbs(small, luts, lut_idx=idx, threads=8)), f"{name}: KS -> PBS differs"
+            edge = np.random.default_rng(12).integers(0, 2 ** 64, (3, p.lwe_dimension + 1), dtype=np.uint64)
+            edge[0, :-1] = 0
+            edge[1, :-1] = np.uint64(1 << 63)
+            assert np.array_equal(eng.programmable_bootstrap(edge, luts[1]), fb.pbs(edge, luts[1], threads=3))

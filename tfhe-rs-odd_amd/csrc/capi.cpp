@@ -14,6 +14,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/tfhe_mi355.h"
@@ -119,6 +120,10 @@ struct CoalescedReq {
     size_t lut_count;
     const uint32_t *idx;
     size_t count;
+    // completion: set by the dispatcher, waited on by the caller alone (no shared mutex, so a
+    // finished batch wakes its callers without a thundering herd on the queue lock)
+    std::mutex m;
+    std::condition_variable cv;
     bool done = false;
     std::string err;
 };
@@ -155,21 +160,21 @@ struct TfheMi355Context {
     KernelTimer timer;  // per-kernel durations (tfhe_mi355_kernel_timing_*), off by default
     // Request coalescing of small host-pointer calls (the reference calls the PBS one ciphertext
     // at a time from rayon workers: shortint/server_key/mod.rs:783-857, radix_parallel/mul.rs:
-    // 347-407).  Concurrent calls of one op are queued; one caller collects the queue into a
-    // batch (after a short window or when the batch is full) and runs it on one of the batch
-    // slots (8), each with its own stream, staging and scratch, so several batches can be in flight;
+    // 347-407).  Concurrent calls are queued per op; dispatcher threads (one per batch slot,
+    // started with the first coalesced call) each gather a queue into a batch (after a short
+    // window or when the batch is full) and run it on their slot's stream, staging and scratch;
     // every caller gets its rows back bit-identical to a call of its own.
     struct Coalescer {
         std::mutex m;
-        std::condition_variable cv;
+        std::condition_variable cv;  // dispatchers: work queued / stop
         std::vector<CoalescedReq *> queue[CO_OPS];
         size_t queued[CO_OPS] = {};
-        bool collecting[CO_OPS] = {};
+        bool stop = false;
+        std::vector<std::thread> workers;
         struct Slot {
             hipStream_t stream = nullptr;
             PinnedBuffer h_in, h_out, h_luts, h_idx;
             DeviceBuffer d_in, d_out, d_luts, d_idx, d_scratch;
-            bool busy = false;
         } slots[8];
         // statistics (tfhe_mi355_coalesce_stats), under m
         uint64_t batches = 0, rows = 0, in_flight = 0, max_in_flight = 0;
@@ -783,71 +788,86 @@ void run_coalesced_batch(TfheMi355Context *c, TfheMi355Context::Coalescer::Slot 
     }
 }
 
-// the calling thread's request joins the op's queue; whichever caller finds no collector becomes
-// it, waits up to the window for a full batch, takes the queue and runs it on a free slot
-void coalesced_call(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
+// dispatcher of batch slot q: waits for queued work, lets the window fill the batch, takes the
+// longest-waiting op's queue (up to a full batch) and runs it; callers are woken one by one
+void coalesce_dispatcher(TfheMi355Context *c, size_t q) {
     auto &co = c->co;
-    std::unique_lock<std::mutex> lk(co.m);
-    co.queue[op].push_back(&r);
-    co.queued[op] += r.count;
-    co.cv.notify_all();
+    auto &sl = co.slots[q];
     const size_t cap = coalesce_batch();
-    while (!r.done) {
-        if (co.collecting[op] || co.queue[op].empty()) {
-            co.cv.wait(lk);
-            continue;
-        }
-        co.collecting[op] = true;
-        // a free slot first, then the window: while every slot is busy the queue keeps growing
-        // and the next batch takes all of it (collecting first and then waiting for a slot left
-        // many collectors each holding a few rows: 4-row batches at 256 callers)
-        TfheMi355Context::Coalescer::Slot *sl = nullptr;
-        co.cv.wait(lk, [&] {
-            for (size_t q = 0; q < coalesce_slots(); q++)
-                if (!co.slots[q].busy) {
-                    sl = &co.slots[q];
-                    return true;
-                }
-            return false;
-        });
-        sl->busy = true;
-        co.cv.wait_until(lk, std::chrono::steady_clock::now() + coalesce_window(),
-                         [&] { return co.queued[op] >= cap; });
+    size_t rr = 0;  // round robin over the ops
+    for (;;) {
         std::vector<CoalescedReq *> batch;
+        CoalescedOp op = CO_PBS;
         size_t cts = 0;
-        auto &q = co.queue[op];
-        size_t take = 0;
-        while (take < q.size() && (batch.empty() || cts + q[take]->count <= cap)) {
-            cts += q[take]->count;
-            batch.push_back(q[take++]);
+        {
+            std::unique_lock<std::mutex> lk(co.m);
+            auto pending = [&] {
+                for (int o = 0; o < CO_OPS; o++)
+                    if (!co.queue[o].empty()) return true;
+                return false;
+            };
+            co.cv.wait(lk, [&] { return co.stop || pending(); });
+            if (co.stop && !pending()) return;
+            for (int k = 0; k < CO_OPS; k++) {
+                const int o = (int)((rr + k) % CO_OPS);
+                if (!co.queue[o].empty()) {
+                    op = (CoalescedOp)o;
+                    break;
+                }
+            }
+            rr = (size_t)op + 1;
+            co.cv.wait_until(lk, std::chrono::steady_clock::now() + coalesce_window(),
+                             [&] { return co.stop || co.queued[op] >= cap; });
+            auto &qu = co.queue[op];
+            size_t take = 0;
+            while (take < qu.size() && (batch.empty() || cts + qu[take]->count <= cap)) {
+                cts += qu[take]->count;
+                batch.push_back(qu[take++]);
+            }
+            qu.erase(qu.begin(), qu.begin() + take);
+            co.queued[op] -= cts;
+            co.max_in_flight = std::max(co.max_in_flight, ++co.in_flight);
+            if (pending()) co.cv.notify_one();  // another dispatcher can gather the rest
         }
-        q.erase(q.begin(), q.begin() + take);
-        co.queued[op] -= cts;
-        co.collecting[op] = false;  // the next batch can gather while this one runs
-        co.cv.notify_all();
-        co.max_in_flight = std::max(co.max_in_flight, ++co.in_flight);
-        lk.unlock();
         std::string err;
         const auto t0 = std::chrono::steady_clock::now();
         try {
-            run_coalesced_batch(c, *sl, op, batch);
+            run_coalesced_batch(c, sl, op, batch);
         } catch (const std::exception &ex) {
             err = ex.what();
         }
         const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        lk.lock();
-        sl->busy = false;
-        co.in_flight--;
-        co.batches++;
-        co.rows += cts;
-        co.batch_seconds += dt;
-        for (auto *x : batch) {
-            x->err = err;
-            x->done = true;
+        {
+            std::lock_guard<std::mutex> g(co.m);
+            co.in_flight--;
+            co.batches++;
+            co.rows += cts;
+            co.batch_seconds += dt;
         }
-        co.cv.notify_all();
+        for (auto *x : batch) {
+            {
+                std::lock_guard<std::mutex> g(x->m);
+                x->err = err;
+                x->done = true;
+            }
+            x->cv.notify_one();
+        }
     }
-    lk.unlock();
+}
+
+// the calling thread's request joins its op's queue and waits for its own completion
+void coalesced_call(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
+    auto &co = c->co;
+    {
+        std::lock_guard<std::mutex> g(co.m);
+        if (co.workers.empty())
+            for (size_t q = 0; q < coalesce_slots(); q++) co.workers.emplace_back(coalesce_dispatcher, c, q);
+        co.queue[op].push_back(&r);
+        co.queued[op] += r.count;
+    }
+    co.cv.notify_one();
+    std::unique_lock<std::mutex> lk(r.m);
+    r.cv.wait(lk, [&] { return r.done; });
     if (!r.err.empty()) fail("%s", r.err.c_str());
 }
 
@@ -1001,6 +1021,12 @@ int tfhe_mi355_context_destroy(TfheMi355Context *ctx) {
             if (L.stream) (void)hipStreamDestroy(L.stream);
         }
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+        {  // the coalescer's dispatchers drain their queues and exit
+            std::lock_guard<std::mutex> g(ctx->co.m);
+            ctx->co.stop = true;
+        }
+        ctx->co.cv.notify_all();
+        for (auto &t : ctx->co.workers) t.join();
         for (auto &sl : ctx->co.slots)
             if (sl.stream) {
                 (void)hipStreamSynchronize(sl.stream);

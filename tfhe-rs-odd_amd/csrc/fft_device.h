@@ -599,6 +599,11 @@ struct WaveFft<256> {
     static constexpr int V = 4;
     static constexpr int XL = xbuf_len(256);
     using Lds = LdsTwiddles256;
+    // Spectrum element (slot q, lane) is output c1 = (lane >> 4) + 4 q of the stage-2 block
+    // C = lane & 15 (FFT position 16 C + c1), so its frequency is C + 16 c1 (oracle pos_freq of the
+    // [16, 16] plan).
+    __device__ __forceinline__ static uint32_t freq_lane(int lane) { return (lane & 15) + 16 * (lane >> 4); }
+    static constexpr uint32_t freq_slot(int q) { return 64 * q; }
 
     template <class TW, class Sync>
     __device__ __forceinline__ static void forward(cx *v, cx *xb, const TW &tw, int lane, Sync sync) {

@@ -46,11 +46,14 @@ namespace tfhe_mi355 {
 // 56 % of the g = 3 kernel's LDS cycles were conflict cycles, profiles/r03_pmc_mb3.json).  Here re
 // and im are two [M] double planes and entry r sits at position r ^ ((r >> 5) & 31): 2.36 on
 // average (exhaustive over d and slots), and a linear read (r = lane + 64 b) stays conflict-free.
+// (M = 256, the k = 3 sets: plain planes, no swizzle.)
 template <int M>
 struct TwistLds {
-    static_assert(M == 1024, "swizzle sized for M = 1024 (r >> 5 < 32)");
+    static_assert(M == 1024 || M == 256, "twist table layouts for M = 1024 (swizzled) and 256");
+    static constexpr bool SW = M == 1024;
     static constexpr uint32_t IM = 8u * M;  // byte offset of the im plane (table at LDS byte 0)
-    __device__ static uint32_t pos(uint32_t r) { return r ^ ((r >> 5) & 31u); }
+    __device__ static uint32_t swz(uint32_t r) { return SW ? (r >> 5) & 31u : 0u; }
+    __device__ static uint32_t pos(uint32_t r) { return r ^ swz(r); }
     __device__ static void fill(double *t, const double2 *twist, int tid, int nt) {
         for (int e = tid; e < M; e += nt) {
             const uint32_t p = pos((uint32_t)e);
@@ -59,9 +62,9 @@ struct TwistLds {
         }
     }
     // 8 (lane ^ (lane >> 5)): position of twist[lane + 64 b] is 64 b + (lane ^ (lane >> 5) ^ 2 b)
-    __device__ static uint32_t lane_base(int lane) { return 8u * (uint32_t)(lane ^ (lane >> 5)); }
+    __device__ static uint32_t lane_base(int lane) { return 8u * (uint32_t)(SW ? lane ^ (lane >> 5) : lane); }
     __device__ static cx linear(uint32_t lb, int b) {  // twist[lane + 64 b]; b compile-time: one XOR
-        const uint32_t a = (lb ^ (16u * (uint32_t)b)) + 512u * (uint32_t)b;
+        const uint32_t a = (SW ? lb ^ (16u * (uint32_t)b) : lb) + 512u * (uint32_t)b;
         return {lds_ld_f64(a), lds_ld_f64(a + IM)};
     }
     // i^q twist[r] for t = q M + r (t mod 2^32, bits 0 .. log2 M + 1 used): the swap for odd q is
@@ -69,7 +72,7 @@ struct TwistLds {
     // (re: q0 ^ q1, im: q1) are XORed into the high words -- no selects
     __device__ static cx mono(uint32_t t) {
         constexpr int LOG2M = ilog2(M);
-        const uint32_t are = ((t & (2u * M - 1)) ^ ((t >> 5) & 31u)) << 3;
+        const uint32_t are = ((t & (2u * M - 1)) ^ swz(t)) << 3;
         const double re = lds_ld_f64(are), im = lds_ld_f64(are ^ IM);
         const uint32_t sim = t << (30 - LOG2M);  // q1 at bit 31; + 2^30 carries q0 into it
         return {flip_sign(re, sim + 0x40000000u), flip_sign(im, sim)};
@@ -543,22 +546,26 @@ static hipError_t launch_mb_t(const MultiBitPbsLaunch &a, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
     if (a.n % G) return hipErrorInvalidValue;
     const int blocks = (a.count + PBS_MB_CPW - 1) / PBS_MB_CPW;
-    if constexpr (PBS_MB_SHARED && L == 1)
+    if constexpr (PBS_MB_SHARED && L == 1 && (K + 1) * (K + 1) * (1 << G) <= 32)
         hipLaunchKernelGGL((pbs_multibit_shared_kernel<N, K, L, G>), dim3(blocks), dim3(64 * (K + 1) * PBS_MB_CPW), lds, s, a);
     else
         hipLaunchKernelGGL((pbs_multibit_kernel<N, K, L, G>), dim3(blocks), dim3(64 * (K + 1) * PBS_MB_CPW), lds, s, a);
     return hipGetLastError();
 }
 
-// The reference's multi-bit parameter sets at N = 2048 (shortint/parameters/multi_bit.rs) all
-// use a single decomposition level; L > 1 is compiled by the template but not instantiated.
+// The reference's multi-bit parameter sets at N <= 2048 (shortint/parameters/multi_bit.rs): the
+// 2_2 sets (N = 2048, k = 1; the slot-split kernel) and the 1_1 sets (N = 512, k = 3, :96,154; the
+// per-ciphertext kernel: their (k+1)^2 2^g GGSW operands per slot exceed the slot-split register
+// budget).  All use one decomposition level; the 3_3 sets (N = 8192) run the split CMUX.
 bool multibit_pbs_supported(int N, int k, int L, int g) {
-    return N == 2048 && k == 1 && L == 1 && (g == 2 || g == 3);
+    return ((N == 2048 && k == 1) || (N == 512 && k == 3)) && L == 1 && (g == 2 || g == 3);
 }
 
 hipError_t launch_multibit_pbs(int N, int k, int L, int g, const MultiBitPbsLaunch &a, hipStream_t s) {
     if (N == 2048 && k == 1 && L == 1 && g == 3) return launch_mb_t<2048, 1, 1, 3>(a, s);
     if (N == 2048 && k == 1 && L == 1 && g == 2) return launch_mb_t<2048, 1, 1, 2>(a, s);
+    if (N == 512 && k == 3 && L == 1 && g == 3) return launch_mb_t<512, 3, 1, 3>(a, s);
+    if (N == 512 && k == 3 && L == 1 && g == 2) return launch_mb_t<512, 3, 1, 2>(a, s);
     return hipErrorInvalidValue;
 }
 
