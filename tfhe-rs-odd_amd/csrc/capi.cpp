@@ -687,13 +687,13 @@ size_t coalesce_batch() {
     static const size_t v = std::max<size_t>(env_size("TFHE_MI355_COALESCE_BATCH", 1024), 1);
     return v;
 }
-// batch slots in use (up to 8): batches in flight at once, each on its own stream.  A PBS batch
-// takes about one CMUX chain (~8 ms at 2_2) whatever its size up to a chip-full, so by Little's
-// law T callers get at most T / (chain + window) calls/s; more slots only split the callers into
-// smaller concurrent batches, which the device runs less than fully concurrently (measured at
-// 64 callers: 8 slots 21 ms per 16-row batch).  2: one batch gathers while one runs.
+// batch slots (dispatcher threads, up to 8): batches in flight at once, each on its own stream.
+// A PBS batch takes about one CMUX chain (6-9 ms at 2_2) whatever its size up to a chip-full, so
+// by Little's law T callers get at most T / (chain + window) calls/s, and a second slot only
+// splits the callers into two half batches that the device does not overlap (measured at 64 / 256
+// callers: 1 slot 6.8k / 25.9k calls/s, 2 slots 3.8k / 14.6k, 4 slots 2.3k / 7.4k).  Default 1.
 size_t coalesce_slots() {
-    static const size_t v = std::min<size_t>(std::max<size_t>(env_size("TFHE_MI355_COALESCE_SLOTS", 2), 1), 8);
+    static const size_t v = std::min<size_t>(std::max<size_t>(env_size("TFHE_MI355_COALESCE_SLOTS", 1), 1), 8);
     return v;
 }
 std::chrono::microseconds coalesce_window() {

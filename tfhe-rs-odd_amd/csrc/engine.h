@@ -122,6 +122,7 @@ struct ClassicPbsLaunch {
     int count;
     int glwe_out;                // 1: write the rotated accumulator [count][(k+1)N] (no sample extract)
     uint32_t *ticket = nullptr;  // zeroed device word: dynamic ciphertext queue of the persistent grid (null: one pass)
+    int cpw_eff = 0;             // set by the launcher: ciphertexts per workgroup actually used (0: all slots)
 };
 
 // Returns false if (N, k, L) has no compiled specialisation.

@@ -379,7 +379,10 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
         // its partner waves through LDS; the GroupSyncs that every wave of the slot executes once
         // per ciphertext order the handover.
         uint32_t *tslot = reinterpret_cast<uint32_t *>(smem + Cfg::ticket_off()) + slot;
-        int ct_raw = blockIdx.x * CPW + slot;
+        // a small batch is spread over the CUs (cpw_eff < CPW slots per workgroup, no tickets): a
+        // ciphertext alone on its CU runs its CMUX chain ~1.5x faster than four sharing it
+        const int cpw = a.cpw_eff > 0 ? a.cpw_eff : CPW;
+        int ct_raw = slot < cpw ? (int)blockIdx.x * cpw + slot : a.count;
         while (ct_raw < a.count) {
             run_ct(ct_raw);
             if (!a.ticket) break;
@@ -405,8 +408,20 @@ static hipError_t launch_pbs_t(const ClassicPbsLaunch &a, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
     const int threads = 64 * (K + 1) * CPW;
     int blocks = (a.count + CPW - 1) / CPW;
-    if (PbsConfig<N, K, L>::PERSIST && a.ticket)
-        blocks = std::min(blocks, resident_blocks((const void *)pbs_classic_kernel<N, K, L>, threads, lds));
+    if (PbsConfig<N, K, L>::PERSIST && a.ticket) {
+        const int res = resident_blocks((const void *)pbs_classic_kernel<N, K, L>, threads, lds);
+        if (CPW > 1 && a.count <= res * (CPW - 1)) {
+            // fewer ciphertexts than a packed resident grid: spread them, ceil(count / res) per
+            // workgroup (latency of the coalesced small batches: 9.0 -> 5.8 ms at 2_2 alone on a CU)
+            ClassicPbsLaunch b = a;
+            b.cpw_eff = (a.count + res - 1) / res;
+            b.ticket = nullptr;
+            blocks = (a.count + b.cpw_eff - 1) / b.cpw_eff;
+            hipLaunchKernelGGL((pbs_classic_kernel<N, K, L>), dim3(blocks), dim3(threads), lds, s, b);
+            return hipGetLastError();
+        }
+        blocks = std::min(blocks, res);
+    }
     hipLaunchKernelGGL((pbs_classic_kernel<N, K, L>), dim3(blocks), dim3(threads), lds, s, a);
     return hipGetLastError();
 }
