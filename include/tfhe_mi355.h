@@ -24,8 +24,9 @@
  *   - a context is bound to one GPU; host-pointer calls on one context are thread-safe, so
  *     rayon-style concurrent callers sharing a key are safe (SURVEY.md 8b "Threading"): calls of
  *     more than 64 ciphertexts are serialised by an internal mutex, smaller concurrent calls of
- *     the same entry point are coalesced into shared batches that run on their own streams, each
- *     caller receiving exactly its own rows (the reference's one-ciphertext-per-call pattern,
+ *     the same entry point are coalesced into shared batches that a dispatcher thread of the
+ *     context runs on its own stream, each caller blocking until its own rows are written
+ *     (TFHE_MI355_COALESCE_WINDOW_US, _BATCH, _SLOTS tune it; the one-ciphertext-per-call pattern,
  *     shortint/server_key/mod.rs:783-857; TFHE_MI355_COALESCE_MAX_COUNT=0 turns it off).
  *     The _async calls hold no per-context mutable state: every device scratch buffer they
  *     need comes from the caller (d_scratch, sized by the matching *_scratch query;
