@@ -45,6 +45,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "tfhe-rs-odd_amd"))
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
+# measured ceiling of a streaming kernel (2 reads : 1 write, 16-byte lanes) whose 96-255 MiB working
+# set stays in the Infinity Cache: 6.5-7.0 TB/s; 5.0-5.6 TB/s from HBM (768 MiB)
+# (scripts/probes/mall_stream_probe.hip, profiles/r03_mall_stream_probe.log)
+MALL_STREAM_GBS = 6970.0
 FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 vector (= matrix) spec, SURVEY.md 8d
 
 
@@ -349,11 +353,14 @@ def roofline(tag, p, units_per_launch: int, step_ms: float, kname: str, with_ks:
             ach = b * chunk / (t[0] * 1e-3) / 1e9
             mem[kn] = {"bound": "fabric (L2 <-> Infinity Cache / HBM)", "model_bytes_per_launch": b * chunk,
                        "kernel_ms": t[0], "achieved_GBps": ach, "frac_of_hbm_peak": ach / HBM_PEAK_GBS,
+                       "frac_of_mall_stream_ceiling": ach / MALL_STREAM_GBS,
                        "pmc_bytes_per_launch": e.get("hbm_bytes_per_dispatch")}
         r["memory_kernels"] = mem
         r["memory_kernels_note"] = (f"per-CMUX memory kernels on a chunk of {chunk}: the chunk's accumulators, digits "
                                     "and sub-block outputs (~1.5 MiB per ciphertext) stay in the 256 MB Infinity Cache, "
-                                    "so these byte rates are fabric rates, not DRAM rates (MI355X_MICROARCH.md 'HBM')")
+                                    "so these byte rates are fabric rates, not DRAM rates (MI355X_MICROARCH.md 'HBM'); "
+                                    "a streaming probe with a cache-resident working set tops out at 6.97 TB/s "
+                                    "(profiles/r03_mall_stream_probe.log)")
     if ktimes:
         r["kernel_times_ms"] = {k: v[0] for k, v in ktimes.items()}
     return r
