@@ -21,6 +21,11 @@ CASES = [
     ("classic_manticore", "MANTICORE_PARAMETERS", 101, None, [0, 1, 2, 3], (1, 1)),
     ("multibit_g3", "PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS", 102, None, [2, 9], (5, 0)),
     ("large_4_4_n16", "PARAM_MESSAGE_4_CARRY_4_KS_PBS", 103, 16, [7, 200], (1, 3)),
+    # split CMUX (round 3): N = 8192 L = 2 (the reference's 121 ms set), N = 16384 L = 3 (64-bit
+    # decomposition of 33 bits), multi-bit at N = 8192 (keybundle in the paired sub-block kernel)
+    ("split_3_3_n8", "PARAM_MESSAGE_3_CARRY_3_KS_PBS", 104, 8, [5, 60], (3, 7)),
+    ("split_1_6_n6", "PARAM_MESSAGE_1_CARRY_6_KS_PBS", 105, 6, [1, 100], (1, 1)),
+    ("multibit_3_3_g3_n6", "PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_3_KS_PBS", 106, 6, [3, 44], (2, 5)),
 ]
 
 
@@ -37,11 +42,15 @@ def inputs(O, name, pname, seed, n_override, msgs, lut):
     if n_override:
         p = p.with_(lwe_dimension=n_override)
     N, k = p.polynomial_size, p.glwe_dimension
-    if N > 4096:   # schoolbook oracle keygen is too slow at N = 32768: engine client keygen
+    if N > 4096:   # schoolbook oracle keygen is too slow at N >= 8192: engine client keygen
         lwe_sk = client.gen_binary_key(seed, 1, p.lwe_dimension)
         glwe_sk = client.gen_binary_key(seed, 2, k * N)
-        bsk = client.gen_bootstrap_key(seed + 1, lwe_sk, glwe_sk, k, N, p.pbs_base_log, p.pbs_level,
-                                       p.glwe_modular_std_dev)
+        if p.grouping_factor:
+            bsk = client.gen_multi_bit_bootstrap_key(seed + 1, lwe_sk, glwe_sk, k, N, p.pbs_base_log, p.pbs_level,
+                                                     p.grouping_factor, p.glwe_modular_std_dev, threads=8)
+        else:
+            bsk = client.gen_bootstrap_key(seed + 1, lwe_sk, glwe_sk, k, N, p.pbs_base_log, p.pbs_level,
+                                           p.glwe_modular_std_dev)
     else:
         lwe_sk = O.binary_key(seed, 1, p.lwe_dimension)
         glwe_sk = O.binary_key(seed, 2, k * N)

@@ -85,6 +85,48 @@ def test_single_cmux_4_4_n32768_within_reference_fft_tolerance(orc):
     _check_single_cmux(orc, p, bsk, False, 45, count=4)   # sample-extracted (no glwe_out at N = 32768)
 
 
+@pytest.mark.parametrize("name", ["PARAM_MESSAGE_1_CARRY_4_KS_PBS",    # N = 4096, L = 2 (top radix 2)
+                                  "PARAM_MESSAGE_3_CARRY_3_KS_PBS",    # N = 8192, L = 2 (top radix 4)
+                                  "PARAM_MESSAGE_1_CARRY_6_KS_PBS"])   # N = 16384, L = 3 (64-bit digits)
+def test_single_cmux_split_within_reference_fft_tolerance(orc, name):
+    """The split CMUX (pbs_large.hip, [R | 16, 16, 4] DAG) against the exact product, one CMUX."""
+    from tfhe_mi355 import client
+    from tfhe_mi355.parameters import SHORTINT_ALL
+
+    p = SHORTINT_ALL[name].with_(lwe_dimension=4)
+    lwe_sk = client.gen_binary_key(46, 1, 4)
+    glwe_sk = client.gen_binary_key(46, 2, p.big_lwe_dimension)
+    bsk = client.gen_bootstrap_key(47, lwe_sk, glwe_sk, 1, p.polynomial_size, p.pbs_base_log, p.pbs_level,
+                                   p.glwe_modular_std_dev)
+    _check_single_cmux(orc, p, bsk, False, 48, count=4)
+
+
+def test_single_group_multibit_n8192_within_reference_fft_tolerance(orc):
+    """Multi-bit g = 3 at N = 8192, L = 2 (PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_3, the paired
+    sub-block kernel): one group against the exact keybundle and external product."""
+    from tfhe_mi355 import Engine, client
+    from tfhe_mi355.parameters import PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_3_KS_PBS as MB
+
+    g, N = MB.grouping_factor, MB.polynomial_size
+    p = MB.with_(lwe_dimension=g)
+    lwe_sk = client.gen_binary_key(73, 1, g)
+    glwe_sk = client.gen_binary_key(73, 2, N)
+    bsk = client.gen_multi_bit_bootstrap_key(74, lwe_sk, glwe_sk, 1, N, p.pbs_base_log, p.pbs_level, g,
+                                             p.glwe_modular_std_dev, threads=THREADS)
+    rng = np.random.default_rng(75)
+    acc = rng.integers(0, 2 ** 64, 2 * N, dtype=np.uint64)
+    cts = rng.integers(0, 2 ** 64, (6, g + 1), dtype=np.uint64)
+    eng = Engine(p, 0)
+    eng.upload_bootstrap_key(bsk)
+    got = eng.programmable_bootstrap(cts, acc)
+    eng.close()
+    exact = orc.exact_mb_pbs(bsk, g, 1, N, p.pbs_base_log, p.pbs_level, g, cts, acc, threads=THREADS)
+    tol = (1 << g) * external_product_tolerance(p)
+    worst = int(modular_distance(got, exact).max())
+    print(f"multi-bit N={N} g={g}: max |GPU - exact| = 2^{np.log2(max(worst, 1)):.1f}, tolerance 2^{tol.bit_length() - 1}")
+    assert 0 < worst <= tol
+
+
 def _noise(orc, glwe_sk, out, msgs, delta):
     ph = orc.lwe_decrypt(glwe_sk, out)
     return torus_modular_diff(ph, np.asarray(msgs, dtype=np.uint64) * np.uint64(delta)), ph
