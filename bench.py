@@ -114,8 +114,10 @@ def _split_params():
         out[tag] = (name, f"shortint apply_lookup_table (keyswitch -> PBS) at {name} (shortint/parameters/mod.rs:"
                           f"{SHORTINT_SOURCE_LINE[name]}), N={p.polynomial_size}, batch per GPU; the reference publishes "
                           + ("121 ms per KS+PBS at 3_3 (benchmarks.md:42)" if tag == "3_3" else "no number for this set"),
-                    f"large_sub_kernel<{p.polynomial_size},1,{p.pbs_level}> (+ large_top_fwd/top_inv per CMUX, "
-                    "ks_mfma_kernel)")
+                    (f"large_dsub_kernel<{p.polynomial_size}> (+ split_digits/large_top_inv per CMUX, ks_mfma_kernel)"
+                     if p.pbs_level == 2 and p.polynomial_size <= 8192 else
+                     f"large_sub_kernel<{p.polynomial_size},1,{p.pbs_level}> (+ large_top_fwd/top_inv per CMUX, "
+                     "ks_mfma_kernel)"))
     # the multi-bit sets at N = 8192 (shortint/parameters/multi_bit.rs:134-153, 192-210): the split
     # CMUX with the keybundle built inside large_sub_kernel, one CMUX per group of g
     from tfhe_mi355.parameters import MULTI_BIT_ALL
@@ -132,7 +134,7 @@ def _split_params():
 
 
 PARAMS.update(_split_params())
-SPLIT_TAGS = {t for t, v in PARAMS.items() if v[2].startswith(("large_sub_kernel", "large_pair_sub_kernel"))}
+SPLIT_TAGS = {t for t, v in PARAMS.items() if v[2].startswith(("large_sub_kernel", "large_pair_sub_kernel", "large_dsub_kernel"))}
 WITH_KS = {"4_4", "2_2ks"} | SPLIT_TAGS
 
 
@@ -264,6 +266,17 @@ def split_sub_flops(p) -> float:
     return k1 * L * 5 * M * 10 + k1 * k1 * L * M * 8 + k1 * 5 * M * 10 + kb
 
 
+def split_dsub_flops(p) -> float:
+    """FP64 flop of large_dsub_kernel per ciphertext and CMUX (digits-fed split CMUX, L = 2): the
+    twist (6 M) and top radix-R stage (5 M log2 R) of the (k+1)L digit polynomials -- counted once,
+    as the algorithm needs them, although each of the R sub-block workgroups recomputes its share --
+    plus large_sub_kernel's sub-FFTs and MAC."""
+    M = p.polynomial_size // 2
+    R = M // 1024
+    k1, L = p.glwe_dimension + 1, p.pbs_level
+    return k1 * L * (6 * M + 5 * M * math.log2(R)) + split_sub_flops(p)
+
+
 def split_chunk(p, units: int) -> int:
     """Ciphertexts per pass of the split CMUX (capi.cpp large_chunk)."""
     if p.polynomial_size >= 32768:
@@ -301,7 +314,9 @@ def roofline(tag, p, units_per_launch: int, step_ms: float, kname: str, with_ks:
     else:  # one launch per step (or a replayed graph): the step's own events
         kernel_ms, timed = step_ms, None
         kernel_src = "HIP events around the whole step on the launch stream (no per-kernel timer)"
-    flop_launch = ((large_group_flops(p) if grouped else split_sub_flops(p)) * chunk) if large else steps_flop
+    dsub = large and fam == "large_dsub_kernel"
+    flop_launch = ((large_group_flops(p) if grouped else split_dsub_flops(p) if dsub else split_sub_flops(p)) * chunk
+                   if large else steps_flop)
     fp64 = flop_launch / (kernel_ms * 1e-3) / 1e12
     if tag == "mul32":
         pmc, why = None, ("the multiply DAG replays the 2_2 KS+PBS kernels in one hipGraph: their per-kernel "
@@ -318,7 +333,8 @@ def roofline(tag, p, units_per_launch: int, step_ms: float, kname: str, with_ks:
                     f"(twist, forward FFTs incl. the top radix-16 share, MAC, inverse sub-FFTs) x {chunk} ciphertexts "
                     f"per launch / its average launch duration") if grouped else
                    (f"{fam} FP64 flop per ciphertext and {'group' if p.grouping_factor else 'CMUX'} "
-                    f"{split_sub_flops(p):,.0f} (1024-point forward and inverse sub-FFTs, MAC"
+                    f"{(split_dsub_flops(p) if dsub else split_sub_flops(p)):,.0f} ("
+                    f"{'twist and top radix-R share, ' if dsub else ''}1024-point forward and inverse sub-FFTs, MAC"
                     f"{', keybundle' if p.grouping_factor else ''}) x {chunk} ciphertexts per launch / its average "
                     f"launch duration") if large else
                    (f"FP64 flop model (SURVEY.md 8d): {pbs_flops(p):,.0f} flop per PBS x {units_per_launch} PBS per "

@@ -364,33 +364,15 @@ __device__ __forceinline__ cx mono_spectrum(const double2 *__restrict__ twist, u
     }
 }
 
-// classic CMUX sub-blocks (the multi-bit sets run large_pair_sub_kernel below)
+// the sub-block CMUX of one (ciphertext, sub-block q) after this wave's input v (polynomial
+// (lvl - 1)(K+1) + r = wave, sub-block q, natural layout) is in registers and the twiddle table
+// is visible: forward sub-FFT, publish, MAC of column c = wave, inverse -> T[lvl 1][row c][q]
 template <int N, int K, int L>
-__global__ void __launch_bounds__((LargeSubCfg<K, L>::THREADS), 2) large_sub_kernel(LargePbsLaunch a, int ct0, int i) {
-    using Cfg = LargeSubCfg<K, L>;
-    using S = Split<N>;
-    constexpr int M = S::M, R = S::R;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    double2 *lds = reinterpret_cast<double2 *>(smem);
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    int q, cl;
-    sub_block_of<R>(blockIdx.x, q, cl);
-    double2 *s1 = lds + Cfg::S1;
-    // sub-block stage twiddles W_1024[lane c] = W_M[R lane c]  (oracle dif_rec tstride R)
-    for (int e = threadIdx.x; e < SubFft::Lds::s1_len; e += Cfg::THREADS) s1[e] = a.W[R * (e & 63) * ((e >> 6) + 1)];
-    const SubFft::Lds tw{s1, s1};
+__device__ __forceinline__ void sub_cmux_body(const LargePbsLaunch &a, int i, int q, double2 *T, double2 *lds, cx (&v)[16],
+                                              const SubFft::Lds &tw, int wave, int lane) {
+    constexpr int M = Split<N>::M;
     cx *xb = reinterpret_cast<cx *>(lds) + wave * SubFft::XL;
     WaveLocalSync wsync;
-    // this wave's poly (lvl - 1) (K+1) + r, sub-block q, natural layout
-    double2 *T = a.spectra + (size_t)cl * L * (K + 1) * M;
-    cx v[16];
-    {
-        const double2 *src = T + (size_t)wave * M + 1024 * q + lane;
-#pragma unroll
-        for (int b = 0; b < 16; b++) v[b] = gld(src + 64 * b);
-    }
-    __syncthreads();  // twiddle table
     SubFft::forward(v, xb, tw, lane, wsync);
     wsync();
 #pragma unroll
@@ -430,6 +412,145 @@ __global__ void __launch_bounds__((LargeSubCfg<K, L>::THREADS), 2) large_sub_ker
     double2 *dst = T + (size_t)wave * M + 1024 * q + lane;  // (lvl 1, row c) slot: read by this WG only
 #pragma unroll
     for (int b = 0; b < 16; b++) dst[64 * b] = make_double2(v[b].re, v[b].im);
+}
+
+// classic CMUX sub-blocks from large_top_fwd's spectra (the multi-bit sets run
+// large_pair_sub_kernel below)
+template <int N, int K, int L>
+__global__ void __launch_bounds__((LargeSubCfg<K, L>::THREADS), 2) large_sub_kernel(LargePbsLaunch a, int ct0, int i) {
+    using Cfg = LargeSubCfg<K, L>;
+    using S = Split<N>;
+    constexpr int M = S::M, R = S::R;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double2 *lds = reinterpret_cast<double2 *>(smem);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int q, cl;
+    sub_block_of<R>(blockIdx.x, q, cl);
+    double2 *s1 = lds + Cfg::S1;
+    // sub-block stage twiddles W_1024[lane c] = W_M[R lane c]  (oracle dif_rec tstride R)
+    for (int e = threadIdx.x; e < SubFft::Lds::s1_len; e += Cfg::THREADS) s1[e] = a.W[R * (e & 63) * ((e >> 6) + 1)];
+    const SubFft::Lds tw{s1, s1};
+    double2 *T = a.spectra + (size_t)cl * L * (K + 1) * M;
+    cx v[16];
+    {
+        const double2 *src = T + (size_t)wave * M + 1024 * q + lane;
+#pragma unroll
+        for (int b = 0; b < 16; b++) v[b] = gld(src + 64 * b);
+    }
+    __syncthreads();  // twiddle table
+    sub_cmux_body<N, K, L>(a, i, q, T, lds, v, tw, wave, lane);
+}
+
+// ---------------------------------------------------------------------------------------
+// Digits-fed split CMUX (L = 2, k = 1, N = 4096 and 8192).  As the grouped CMUX
+// at N = 32768 does, large_top_fwd's f64 spectra (4 polynomials x M x 16 B per ciphertext written,
+// then read back) are replaced by packed int16 digits (M x 16 B) and the twist + top radix-R
+// share of each sub-block is computed where it is consumed:
+//   split_digits_kernel : per (ct, j < M), both rows: ct1 = X^{a~} acc - acc at j and j + M,
+//                         decompose64<2> (the top stage's own decomposition), four int16 digits
+//                         per row word (level L at j, j + M; level L-1 at j, j + M)
+//   large_dsub_kernel   : per (ct, sub-block q): for every butterfly a < 1024 and polynomial
+//                         (level, row): twist, the top DIF radix-R (dftR_fwd, every output as the
+//                         top stage computes them), output q times W[a q] -> the wave's LDS buffer
+//                         in the WaveFft<1024> natural layout; then the sub-block CMUX as above.
+// The R workgroups of a ciphertext run on one XCD (digits from the Infinity Cache once, then L2;
+// the CMUX's GGSW, 0.25-0.5 MiB, fits that L2).  Same operations in the same order as
+// large_top_fwd + large_sub_kernel, so the outputs are bit-identical.  Digits live in the
+// ciphertext's level-2 spectra slots, which this path does not otherwise use.
+// ---------------------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ acc_pair *split_digits(const LargePbsLaunch &a, int cl) {
+    constexpr int M = Split<N>::M;
+    return reinterpret_cast<acc_pair *>(a.spectra + ((size_t)cl * 2 * 2 + 2) * M);
+}
+
+template <int N>
+__global__ void __launch_bounds__(256) split_digits_kernel(LargePbsLaunch a, int ct0, int i) {
+    using S = Split<N>;
+    constexpr int M = S::M, PER = M / 256;
+    const int x = blockIdx.x & 7, m = blockIdx.x >> 3;
+    const int cl = x + 8 * (m / PER), sub = m % PER;
+    if (cl >= a.chunk_count) return;
+    const uint64_t *in = a.lwe_in + (size_t)(ct0 + cl) * (a.n + 1);
+    const uint32_t at = pbs_modulus_switch<S::LOGN>(in[i]);
+    const bool full_odd = (at / N) & 1;
+    const int rem = at % N;
+    const int j = sub * 256 + threadIdx.x;
+    uint64_t w[2];
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        uint64_t dd[2];
+        ct1_pair_m<M>(a.acc + ((size_t)cl * 2 + r) * N, j, rem, full_odd, dd[0], dd[1]);
+        int32_t d0[2], d1[2];
+        decompose64<2>(dd[0], a.base_log, d0);
+        decompose64<2>(dd[1], a.base_log, d1);
+        w[r] = ((uint64_t)((uint32_t)d0[0] & 0xffffu)) | ((uint64_t)((uint32_t)d1[0] & 0xffffu) << 16) |
+               ((uint64_t)((uint32_t)d0[1] & 0xffffu) << 32) | ((uint64_t)((uint32_t)d1[1] & 0xffffu) << 48);
+    }
+    split_digits<N>(a, cl)[j] = acc_pair{w[0], w[1]};
+}
+
+template <int N>
+__global__ void __launch_bounds__((LargeSubCfg<1, 2>::THREADS), 2) large_dsub_kernel(LargePbsLaunch a, int ct0, int i) {
+    constexpr int K = 1, L = 2;
+    using Cfg = LargeSubCfg<K, L>;
+    using S = Split<N>;
+    constexpr int M = S::M, R = S::R;
+    static_assert(R <= 4, "N <= 8192 (the top stage's R-fold recomputation loses at R = 8)");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double2 *lds = reinterpret_cast<double2 *>(smem);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // the R sub-block workgroups of ciphertext cl: blocks 8 m + x with the same x (one XCD)
+    const int x = blockIdx.x & 7, m = blockIdx.x >> 3;
+    const int cl = x + 8 * (m / R), q = m % R;
+    if (cl >= a.chunk_count) return;  // whole workgroup
+    (void)ct0;
+    double2 *s1 = lds + Cfg::S1;
+    for (int e = threadIdx.x; e < SubFft::Lds::s1_len; e += Cfg::THREADS) s1[e] = a.W[R * (e & 63) * ((e >> 6) + 1)];
+    const SubFft::Lds tw{s1, s1};
+    const acc_pair *dig = split_digits<N>(a, cl);
+    // phase 1: butterflies a0 = tid + 256 t -> buffer of polynomial p = (lvl - 1)(K+1) + r at a0
+    for (int a0 = threadIdx.x; a0 < 1024; a0 += Cfg::THREADS) {
+        acc_pair dw[R];
+        cx tv[R];
+#pragma unroll
+        for (int b = 0; b < R; b++) {
+            dw[b] = dig[a0 + 1024 * b];
+            tv[b] = gld(a.twist + a0 + 1024 * b);
+        }
+        const cx wq = q ? gld(a.wtop + (q - 1) * 1024 + a0) : cx{1.0, 0.0};  // = W[a0 q]
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int li = 0; li < 2; li++) {  // li = 0: level L (the top stage's first pass), 1: level L-1
+                cx u[R];
+#pragma unroll
+                for (int b = 0; b < R; b++) {
+                    const uint64_t wr = r ? dw[b].y : dw[b].x;
+                    const int32_t e0 = (int32_t)(int16_t)((wr >> (32 * li)) & 0xffffu);
+                    const int32_t e1 = (int32_t)(int16_t)((wr >> (32 * li + 16)) & 0xffffu);
+                    u[b] = cmulw(cx{(double)e0, (double)e1}, tv[b].re, tv[b].im);
+                }
+                dftR_fwd<R>(u);
+                cx y = u[0];
+#pragma unroll
+                for (int c = 1; c < R; c++)
+                    if (c == q) y = cmulw(u[c], wq.re, wq.im);
+                const int p = (1 - li) * (K + 1) + r;  // level L -> polys 2, 3; level L-1 -> 0, 1
+                lds[p * SubFft::XL + a0] = make_double2(y.re, y.im);
+            }
+    }
+    __syncthreads();  // phase-1 outputs and the twiddle table
+    cx v[16];
+#pragma unroll
+    for (int b = 0; b < 16; b++) {
+        const double2 t = lds[wave * SubFft::XL + lane + 64 * b];
+        v[b] = cx{t.x, t.y};
+    }
+    double2 *T = a.spectra + (size_t)cl * L * (K + 1) * M;
+    sub_cmux_body<N, K, L>(a, i, q, T, lds, v, tw, wave, lane);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1167,6 +1288,16 @@ static bool large_grouped_enabled() {
     return v;
 }
 
+// TFHE_MI355_DSUB=0: the classic L = 2 split CMUX at N <= 8192 through large_top_fwd +
+// large_sub_kernel instead of the digits-fed path (A/B switch)
+static bool large_dsub_enabled() {
+    static const bool v = [] {
+        const char *e = std::getenv("TFHE_MI355_DSUB");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // TFHE_MI355_PAIR_SUB=1: the classic split CMUX (L <= 2) through large_pair_sub_kernel too (A/B)
 static bool large_pair_sub_classic() {
     static const bool v = [] {
@@ -1214,6 +1345,31 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
                     }
                     TimedLaunch tl(a.timer, "large_top_inv_kernel", s);
                     hipLaunchKernelGGL((large_top_inv_kernel<N, K>), dim3(top_blocks), dim3(TOPT), 0, s, a, ct0, i);
+                }
+                hipLaunchKernelGGL((large_extract_kernel<N, K>), dim3((unsigned)((out_elems + 255) / 256)), dim3(256),
+                                   0, s, a, ct0, cnt);
+                continue;
+            }
+        }
+        // N = 4096 / 8192 only: at R = 8 the R-fold recomputation of the top stage in each
+        // sub-block workgroup costs more than the spectra it saves (2_5: 2005 vs 2191 KS+PBS/s)
+        if constexpr (G == 0 && K == 1 && L == 2 && S::R <= 4) {
+            if (large_dsub_enabled()) {  // digits-fed CMUX: digits, sub-blocks from digits, top_inv
+                constexpr int DPER = S::M / 256;
+                const unsigned dig_blocks = (unsigned)((cnt + 7) / 8) * 8 * DPER;
+                const unsigned dsub_blocks = (unsigned)((cnt + 7) / 8) * 8 * S::R;
+                for (int i = 0; i < a.n; i++) {
+                    {
+                        TimedLaunch tl(a.timer, "split_digits_kernel", s);
+                        hipLaunchKernelGGL((split_digits_kernel<N>), dim3(dig_blocks), dim3(256), 0, s, a, ct0, i);
+                    }
+                    {
+                        TimedLaunch tl(a.timer, "large_dsub_kernel", s);
+                        hipLaunchKernelGGL((large_dsub_kernel<N>), dim3(dsub_blocks), dim3(Sub::THREADS), Sub::LDS, s,
+                                           a, ct0, i);
+                    }
+                    TimedLaunch tl(a.timer, "large_top_inv_kernel", s);
+                    hipLaunchKernelGGL((large_top_inv_kernel<N, K, G>), dim3(top_blocks), dim3(TOPT), 0, s, a, ct0, i);
                 }
                 hipLaunchKernelGGL((large_extract_kernel<N, K>), dim3((unsigned)((out_elems + 255) / 256)), dim3(256),
                                    0, s, a, ct0, cnt);
