@@ -114,3 +114,45 @@ def test_mixed_ops_counts_and_lut_indexes_coalesce_exactly(orc, keys_2_2, eng):
             luts = accs if idx is not None else accs[0]
             exp = keys_2_2.fbsk.pbs(small_all[j], luts, lut_idx=idx, threads=8)
         assert np.array_equal(got[j], exp), f"job {j} ({op}, {big.shape[0]} cts, idx={idx is not None}) differs"
+
+
+@pytest.mark.parametrize("name", ["PARAM_MESSAGE_3_CARRY_3_KS_PBS",                     # digits-fed split CMUX
+                                  "PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_3_KS_PBS",   # multi-bit paired kernel
+                                  "PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS"])  # multi-bit N = 2048
+def test_coalesced_single_calls_on_the_other_kernels(orc, name):
+    """8 threads x 6 one-ciphertext KS+PBS calls through the coalescer at a large-N and the
+    multi-bit shapes (reduced n): each caller's rows equal the same ciphertexts' rows from one
+    batched call (which the parity tests pin to the oracle) and decrypt to f(m)."""
+    from tfhe_mi355 import Engine, client
+    from tfhe_mi355.parameters import ALL
+
+    p = ALL[name].with_(lwe_dimension=6)
+    N, k, g = p.polynomial_size, p.glwe_dimension, p.grouping_factor
+    space = p.message_modulus * p.carry_modulus
+    lwe_sk = client.gen_binary_key(131, 1, p.lwe_dimension)
+    glwe_sk = client.gen_binary_key(131, 2, p.big_lwe_dimension)
+    if g:
+        bsk = client.gen_multi_bit_bootstrap_key(132, lwe_sk, glwe_sk, k, N, p.pbs_base_log, p.pbs_level, g,
+                                                 p.glwe_modular_std_dev, threads=8)
+    else:
+        bsk = client.gen_bootstrap_key(132, lwe_sk, glwe_sk, k, N, p.pbs_base_log, p.pbs_level, p.glwe_modular_std_dev)
+    ksk = client.gen_keyswitch_key(133, glwe_sk, lwe_sk, p.ks_base_log, p.ks_level, p.lwe_modular_std_dev)
+    e = Engine(p, 0)
+    e.upload_bootstrap_key(bsk)
+    e.upload_keyswitch_key(ksk)
+    T, C = 8, 6
+    acc = orc.fill_accumulator(N, k, p.message_modulus, p.carry_modulus, lambda x: (x + 3) % space)
+    msgs = (np.arange(T * C) * 5) % space
+    big = orc.lwe_encrypt(134, glwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta), p.glwe_modular_std_dev)
+    ref = e.keyswitch_programmable_bootstrap(big, acc)
+    out = np.zeros_like(ref)
+
+    def worker(t):
+        for c in range(C):
+            i = t * C + c
+            out[i] = e.keyswitch_programmable_bootstrap(big[i:i + 1], acc)[0]
+
+    _run_threads(T, worker)
+    e.close()
+    assert np.array_equal(out, ref)
+    assert np.array_equal(decode(orc.lwe_decrypt(glwe_sk, out), p.delta) % space, (msgs + 3) % space)
