@@ -861,14 +861,15 @@ def host_abi_rate(eng, P, cts, acc, with_ks: bool, reps: int = 3) -> dict:
 
 
 def single_ct_rates(eng, cts, acc, with_ks: bool, batched_rate: float, secs: float = 2.0,
-                    callers=(1, 16, 64, 256)) -> dict:
+                    callers=(1, 16, 64, 256), submit_windows=((1, 256), (16, 64))) -> dict:
     """The reference's own calling pattern through the synchronous host-pointer ABI: ONE ciphertext
     per call (keyswitch_programmable_bootstrap_assign, shortint/server_key/mod.rs:783-857), from T
     native threads at once (rayon workers, radix_parallel/mul.rs:347-407), each issuing its next
     call when the previous returns (lib/libtfhe_mi355_loadgen.so: std::threads, no GIL).  The
     engine coalesces concurrent small calls into batches.  Every output is compared
     with the same ciphertext's row from one batched call.  By Little's law T callers cannot exceed
-    T / latency (`little_bound`)."""
+    T / latency (`little_bound`).  `submit_wait` drives tfhe_mi355_submit / tfhe_mi355_wait
+    (count = 1 per request, W requests in flight per thread)."""
     import ctypes
 
     from tfhe_mi355 import _lib
@@ -902,6 +903,27 @@ def single_ct_rates(eng, cts, acc, with_ks: bool, batched_rate: float, secs: flo
                                   "coalescing": eng.coalesce_stats()}
     if "1" in res["callers"]:
         res["single_call_latency_ms"] = res["callers"]["1"]["mean_call_latency_ms"]
+    # the asynchronous pair (tfhe_mi355_submit / tfhe_mi355_wait): T threads, each with W count = 1
+    # requests in flight, so T * W ciphertexts can share one coalesced batch
+    lg.tfhe_mi355_loadgen_submit_run.restype = ctypes.c_int
+    res["submit_wait"] = {}
+    for T, W in submit_windows:
+        eng.coalesce_stats(reset=True)
+        calls, bad, fails = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        wall, lat = ctypes.c_double(), ctypes.c_double()
+        rc = lg.tfhe_mi355_loadgen_submit_run(
+            eng._h, ctypes.c_int(1 if with_ks else 0), x.ctypes.data_as(u64p), ctypes.c_size_t(x.shape[1]),
+            ctypes.c_size_t(n_in), exp.ctypes.data_as(u64p), ctypes.c_size_t(exp.shape[1]), a.ctypes.data_as(u64p),
+            ctypes.c_int(T), ctypes.c_int(W), ctypes.c_double(secs), ctypes.byref(calls), ctypes.byref(wall),
+            ctypes.byref(lat), ctypes.byref(bad), ctypes.byref(fails))
+        if rc != 0:
+            raise _lib.EngineError("loadgen (submit) failed")
+        rate = calls.value / wall.value
+        res["submit_wait"][f"{T}x{W}"] = {"threads": T, "in_flight_per_thread": W, "value": rate,
+                                          "frac_of_batched_device_rate": rate / batched_rate,
+                                          "mean_request_latency_ms": lat.value * 1e3, "calls": calls.value,
+                                          "mismatching_rows": bad.value, "failed_calls": fails.value,
+                                          "coalescing": eng.coalesce_stats()}
     res["note"] = ("T native threads (libtfhe_mi355_loadgen), closed loop, count = 1 per call, every output "
                    "compared with a batched call's row; T callers cannot exceed T / latency (little_bound); "
                    "the batched device rate is the headline step's")

@@ -26,7 +26,9 @@
  *     more than 64 ciphertexts are serialised by an internal mutex, smaller concurrent calls of
  *     the same entry point are coalesced into shared batches that a dispatcher thread of the
  *     context runs on its own stream, each caller blocking until its own rows are written
- *     (TFHE_MI355_COALESCE_WINDOW_US, _BATCH, _SLOTS tune it; the one-ciphertext-per-call pattern,
+ *     (a batch closes when no call has arrived for TFHE_MI355_COALESCE_GAP_US = 50, after at most
+ *     _WINDOW_US = 500, or at _BATCH = 1024 ciphertexts; _SLOTS, _OVERFLOW: a second batch runs
+ *     concurrently only when half a batch is queued; the one-ciphertext-per-call pattern,
  *     shortint/server_key/mod.rs:783-857; TFHE_MI355_COALESCE_MAX_COUNT=0 turns it off).
  *     The _async calls hold no per-context mutable state: every device scratch buffer they
  *     need comes from the caller (d_scratch, sized by the matching *_scratch query;
@@ -85,6 +87,22 @@ int tfhe_mi355_device_count(int *out_count);
 int tfhe_mi355_kernel_timing_enable(TfheMi355Context *ctx, int every);
 int tfhe_mi355_kernel_timing_entry(TfheMi355Context *ctx, size_t index, char *name, size_t name_len,
                                    double *total_ms, uint64_t *launches);
+
+/* Asynchronous form of the small host-pointer calls (the coalescer's queue):
+ * tfhe_mi355_submit enqueues 1..1024 ciphertexts of one op (0: programmable_bootstrap,
+ * 1: keyswitch_programmable_bootstrap, 2: programmable_bootstrap_keyswitch, 3: keyswitch; arguments
+ * as those entry points, luts ignored for op 3) and returns at once with a request handle;
+ * tfhe_mi355_wait blocks until the outputs are written and frees the handle (every submitted
+ * request must be waited on exactly once, before the buffers are reused or the context is
+ * destroyed).  One thread can keep many requests in flight: a rayon worker can submit every block
+ * of its share of an integer layer, then wait for them (the reference calls
+ * keyswitch_programmable_bootstrap_assign per block, shortint/server_key/mod.rs:783-857), so the
+ * coalesced batch is no longer capped by the number of threads. */
+typedef struct TfheMi355Request TfheMi355Request;
+int tfhe_mi355_submit(TfheMi355Context *ctx, int op, const uint64_t *lwe_in, uint64_t *lwe_out,
+                      const uint64_t *luts, size_t lut_count, const uint32_t *lut_indexes, size_t count,
+                      TfheMi355Request **out_req);
+int tfhe_mi355_wait(TfheMi355Request *req);
 
 /* Request-coalescing counters of this context (all ops): batches run, ciphertexts in them, the
  * most batches in flight at once, and the summed wall time of the batches (staging, copies,

@@ -33,7 +33,8 @@ for s in $STAGES; do
     bench) step bench 900 python -u bench.py ;;
     bench:*) step bench_${s#bench:} 600 python -u bench.py $(kargs ${s#bench:}) ;;
     # sct:<VAR>=<value>: the single-ciphertext calling-pattern probe under one coalescer setting
-    sct:*) kv=${s#sct:}; step sct_${kv//=/_} 300 env "$kv" python -u scripts/single_ct_probe.py ;;
+    # (several settings: VAR=v,VAR2=w; probe arguments from $SCT_ARGS)
+    sct:*) kv=${s#sct:}; step sct_${kv//[=,]/_} 300 env ${kv//,/ } python -u scripts/single_ct_probe.py $SCT_ARGS ;;
     # ab:<tag>:<VAR>=<value>: the bench of <tag> under one engine environment switch (A/B)
     ab:*) r=${s#ab:}; t=${r%%:*}; kv=${r#*:}; step ab_${t}_${kv//=/_} 600 env "$kv" python -u bench.py $(kargs $t) --no-cpu-baseline --no-host-abi ;;
     # the N = 32768, L = 2 CMUX through the split path instead of the grouped one (A/B)

@@ -1,7 +1,7 @@
 """Single-ciphertext calling pattern probe: T native callers of the count = 1
 host ABI through the request coalescer, with the coalescer's own counters (batches, rows per
 batch, batches in flight, batch wall time).  Run under different TFHE_MI355_COALESCE_* settings:
-    python scripts/single_ct_probe.py [--params 2_2] [--callers 16 64 256]"""
+    python scripts/single_ct_probe.py [--params 2_2] [--callers 16 64 256] [--windows 1x256 16x64]"""
 import argparse
 import json
 import os
@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--params", default="2_2")
     ap.add_argument("--callers", type=int, nargs="+", default=[1, 16, 64, 256])
     ap.add_argument("--seconds", type=float, default=2.0)
+    ap.add_argument("--windows", nargs="+", default=["1x256", "16x64"],
+                    help="submit/wait legs: THREADSxIN_FLIGHT_PER_THREAD")
     args = ap.parse_args()
     from tfhe_mi355 import client, fill_accumulator
     from tfhe_mi355.parameters import ALL
@@ -38,7 +40,8 @@ def main():
     cts = client.lwe_encrypt(3, key, msgs * np.uint64(P.delta), std)
     acc = fill_accumulator(P, lambda x: x)
     env = {k: v for k, v in os.environ.items() if k.startswith("TFHE_MI355_COALESCE")}
-    res = bench.single_ct_rates(eng, cts, acc, with_ks, 1.0, secs=args.seconds, callers=tuple(args.callers))
+    res = bench.single_ct_rates(eng, cts, acc, with_ks, 1.0, secs=args.seconds, callers=tuple(args.callers),
+                               submit_windows=tuple(tuple(int(v) for v in w.split("x")) for w in args.windows))
     print(json.dumps({"params": args.params, "env": env, "single_ct": res}))
 
 

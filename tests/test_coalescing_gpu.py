@@ -156,3 +156,47 @@ def test_coalesced_single_calls_on_the_other_kernels(orc, name):
     e.close()
     assert np.array_equal(out, ref)
     assert np.array_equal(decode(orc.lwe_decrypt(glwe_sk, out), p.delta) % space, (msgs + 3) % space)
+
+
+def test_submit_wait_many_in_flight_from_one_thread(orc, keys_2_2, eng):
+    """tfhe_mi355_submit / tfhe_mi355_wait: one thread keeps 256 one-ciphertext requests of the
+    four ops in flight, then waits for all of them; each result equals the oracle's result of
+    the same call made alone."""
+    p = keys_2_2.params
+    accs = np.stack([orc.fill_accumulator(2048, 1, 4, 4, lambda x: (x + 1) % 16),
+                     orc.fill_accumulator(2048, 1, 4, 4, lambda x: (3 * x) % 16)])
+    R = 256
+    msgs = (np.arange(R) * 11) % 16
+    big = orc.lwe_encrypt(977, keys_2_2.glwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta),
+                          p.glwe_modular_std_dev)
+    small = orc.keyswitch(keys_2_2.ksk, p.big_lwe_dimension, p.lwe_dimension, p.ks_base_log, p.ks_level, big)
+    ops = ("ks_pbs", "pbs", "ks", "pbs_ks")
+    reqs = []
+    for i in range(R):
+        op = ops[i % 4]
+        src = big[i:i + 1] if op in ("ks_pbs", "ks") else small[i:i + 1]
+        if op == "ks":
+            reqs.append(eng.submit(op, src))
+        else:
+            reqs.append(eng.submit(op, src, accs, np.array([i % 2], dtype=np.uint32)))
+    got = [r.wait() for r in reqs]
+    with pytest.raises(RuntimeError):
+        reqs[0].wait()
+    pbs = keys_2_2.fbsk.pbs(small, accs, lut_idx=(np.arange(R) % 2).astype(np.uint32), threads=16)
+    pbs_ks = orc.keyswitch(keys_2_2.ksk, p.big_lwe_dimension, p.lwe_dimension, p.ks_base_log, p.ks_level, pbs)
+    for i in range(R):
+        exp = {"ks_pbs": pbs, "pbs": pbs, "ks": small, "pbs_ks": pbs_ks}[ops[i % 4]][i:i + 1]
+        assert np.array_equal(got[i], exp), f"request {i} ({ops[i % 4]}) differs from the oracle"
+    dec = decode(orc.lwe_decrypt(keys_2_2.glwe_sk, pbs), p.delta) % 16
+    assert np.array_equal(dec, np.where(np.arange(R) % 2 == 0, (msgs + 1) % 16, (3 * msgs) % 16))
+    st = eng.coalesce_stats()
+    assert st["rows"] >= R
+
+
+def test_submit_rejects_bad_requests(eng):
+    from tfhe_mi355 import _lib
+
+    with pytest.raises((_lib.EngineError, ValueError)):
+        eng.submit("pbs", np.zeros((2000, eng.n + 1), dtype=np.uint64), np.zeros(eng.glwe_len, dtype=np.uint64))
+    with pytest.raises(KeyError):
+        eng.submit("nope", np.zeros((1, eng.n + 1), dtype=np.uint64))

@@ -11,6 +11,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -169,6 +170,7 @@ struct TfheMi355Context {
         std::condition_variable cv;  // dispatchers: work queued / stop
         std::vector<CoalescedReq *> queue[CO_OPS];
         size_t queued[CO_OPS] = {};
+        std::chrono::steady_clock::time_point last_arrival[CO_OPS];
         bool stop = false;
         std::vector<std::thread> workers;
         struct Slot {
@@ -671,8 +673,9 @@ void chunk_pks(TfheMi355Context *c, const uint64_t *i, uint64_t *o, const uint64
 // ---- request coalescing ---------------------------------------------------------------------------
 // Calls of at most coalesce_max_count() ciphertexts (default 64; TFHE_MI355_COALESCE_MAX_COUNT,
 // 0 = off) are coalesced: up to coalesce_batch() ciphertexts (default 1024, one ciphertext per PBS
-// slot of the chip at 2_2) gathered for at most coalesce_window() (default 200 us) from the first
-// queued call.  The window is small next to a PBS (milliseconds), and a full batch leaves at once.
+// slot of the chip at 2_2) gathered until no call has arrived for coalesce_gap() (default 50 us),
+// for at most coalesce_window() (default 500 us) from the first queued call.  Both are small next
+// to a PBS (milliseconds), and a full batch leaves at once.
 size_t env_size(const char *name, size_t dflt) {
     const char *e = std::getenv(name);
     if (!e || !*e) return dflt;
@@ -689,15 +692,32 @@ size_t coalesce_batch() {
 }
 // batch slots (dispatcher threads, up to 8): batches in flight at once, each on its own stream.
 // A PBS batch takes about one CMUX chain (6-9 ms at 2_2) whatever its size up to a chip-full, so
-// by Little's law T callers get at most T / (chain + window) calls/s, and a second slot only
-// splits the callers into two half batches that the device does not overlap (measured at 64 / 256
-// callers: 1 slot 6.8k / 25.9k calls/s, 2 slots 3.8k / 14.6k, 4 slots 2.3k / 7.4k).  Default 1.
+// by Little's law T callers get at most T / (chain + window) calls/s; a second slot that starts
+// whenever work is queued only splits the callers into half batches that the device does not
+// overlap (measured at 64 / 256 synchronous callers: 1 slot 10.4k / 37.5k calls/s, 2 slots
+// 10.3k / 30.4k, 3 slots 7.6k / 26.7k).  So a slot other than the first starts only when
+// coalesce_overflow() rows are queued (coalesce_dispatcher): synchronous callers see one slot,
+// while submit/wait callers with thousands of requests in flight overlap host staging with the
+// device (64 threads x 64 in flight: 92k calls/s with 1 slot, 108-113k with 2).  Default 2.
 size_t coalesce_slots() {
-    static const size_t v = std::min<size_t>(std::max<size_t>(env_size("TFHE_MI355_COALESCE_SLOTS", 1), 1), 8);
+    static const size_t v = std::min<size_t>(std::max<size_t>(env_size("TFHE_MI355_COALESCE_SLOTS", 2), 1), 8);
+    return v;
+}
+// queued ciphertexts of one op that start a batch on a second slot while another runs (default
+// half a batch: 16 threads x 64 submitted requests 62.6k calls/s at a full batch, 67.5k at half;
+// 256 synchronous callers never queue that many, so they keep one slot)
+size_t coalesce_overflow() {
+    static const size_t v = std::max<size_t>(env_size("TFHE_MI355_COALESCE_OVERFLOW", coalesce_batch() / 2), 1);
     return v;
 }
 std::chrono::microseconds coalesce_window() {
-    static const size_t v = env_size("TFHE_MI355_COALESCE_WINDOW_US", 200);
+    static const size_t v = env_size("TFHE_MI355_COALESCE_WINDOW_US", 500);
+    return std::chrono::microseconds(v);
+}
+// the batch also closes once no request of its op has arrived for this long: callers woken one by
+// one after a batch (or a thread submitting a burst) re-queue within microseconds of each other
+std::chrono::microseconds coalesce_gap() {
+    static const size_t v = env_size("TFHE_MI355_COALESCE_GAP_US", 50);
     return std::chrono::microseconds(v);
 }
 
@@ -806,8 +826,16 @@ void coalesce_dispatcher(TfheMi355Context *c, size_t q) {
                     if (!co.queue[o].empty()) return true;
                 return false;
             };
-            co.cv.wait(lk, [&] { return co.stop || pending(); });
+            auto full = [&] {
+                for (int o = 0; o < CO_OPS; o++)
+                    if (co.queued[o] >= coalesce_overflow()) return true;
+                return false;
+            };
+            // a batch starts when no other slot is busy, or when a full batch is waiting (overflow:
+            // callers with many requests in flight, e.g. through tfhe_mi355_submit)
+            co.cv.wait(lk, [&] { return co.stop || (pending() && (co.in_flight == 0 || full())); });
             if (co.stop && !pending()) return;
+            co.max_in_flight = std::max(co.max_in_flight, ++co.in_flight);  // claimed before the window
             for (int k = 0; k < CO_OPS; k++) {
                 const int o = (int)((rr + k) % CO_OPS);
                 if (!co.queue[o].empty()) {
@@ -816,8 +844,12 @@ void coalesce_dispatcher(TfheMi355Context *c, size_t q) {
                 }
             }
             rr = (size_t)op + 1;
-            co.cv.wait_until(lk, std::chrono::steady_clock::now() + coalesce_window(),
-                             [&] { return co.stop || co.queued[op] >= cap; });
+            const auto close = std::chrono::steady_clock::now() + coalesce_window();
+            while (!co.stop && co.queued[op] < cap) {
+                const auto t = std::min(close, co.last_arrival[op] + coalesce_gap());
+                if (std::chrono::steady_clock::now() >= t) break;
+                co.cv.wait_until(lk, t);
+            }
             auto &qu = co.queue[op];
             size_t take = 0;
             while (take < qu.size() && (batch.empty() || cts + qu[take]->count <= cap)) {
@@ -826,8 +858,11 @@ void coalesce_dispatcher(TfheMi355Context *c, size_t q) {
             }
             qu.erase(qu.begin(), qu.begin() + take);
             co.queued[op] -= cts;
-            co.max_in_flight = std::max(co.max_in_flight, ++co.in_flight);
-            if (pending()) co.cv.notify_one();  // another dispatcher can gather the rest
+            if (batch.empty()) {  // another slot took the queue during the window
+                co.in_flight--;
+                continue;
+            }
+            if (full()) co.cv.notify_one();  // another full batch: an idle slot can run it now
         }
         std::string err;
         const auto t0 = std::chrono::steady_clock::now();
@@ -837,26 +872,26 @@ void coalesce_dispatcher(TfheMi355Context *c, size_t q) {
             err = ex.what();
         }
         const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        {
+        for (auto *x : batch) {  // notified under its lock: the caller may free x as soon as it wakes
+            std::lock_guard<std::mutex> g(x->m);
+            x->err = err;
+            x->done = true;
+            x->cv.notify_one();
+        }
+        {  // the slot counts as busy until its callers are all woken, so the next batch's window
+           // (on whichever slot) starts after they have had the chance to queue again
             std::lock_guard<std::mutex> g(co.m);
             co.in_flight--;
             co.batches++;
             co.rows += cts;
             co.batch_seconds += dt;
         }
-        for (auto *x : batch) {
-            {
-                std::lock_guard<std::mutex> g(x->m);
-                x->err = err;
-                x->done = true;
-            }
-            x->cv.notify_one();
-        }
+        co.cv.notify_one();  // a slot waiting for this one to finish
     }
 }
 
-// the calling thread's request joins its op's queue and waits for its own completion
-void coalesced_call(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
+// a request joins its op's queue (the dispatchers start with the first one)
+void coalesce_enqueue(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
     auto &co = c->co;
     {
         std::lock_guard<std::mutex> g(co.m);
@@ -864,11 +899,21 @@ void coalesced_call(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
             for (size_t q = 0; q < coalesce_slots(); q++) co.workers.emplace_back(coalesce_dispatcher, c, q);
         co.queue[op].push_back(&r);
         co.queued[op] += r.count;
+        co.last_arrival[op] = std::chrono::steady_clock::now();
     }
     co.cv.notify_one();
+}
+
+void coalesce_wait(CoalescedReq &r) {
     std::unique_lock<std::mutex> lk(r.m);
     r.cv.wait(lk, [&] { return r.done; });
     if (!r.err.empty()) fail("%s", r.err.c_str());
+}
+
+// the calling thread's request joins its op's queue and waits for its own completion
+void coalesced_call(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
+    coalesce_enqueue(c, op, r);
+    coalesce_wait(r);
 }
 
 bool coalescible(size_t count) { return count > 0 && count <= coalesce_max_count(); }
@@ -915,6 +960,42 @@ int tfhe_mi355_kernel_timing_entry(TfheMi355Context *ctx, size_t index, char *na
         std::snprintf(name, name_len, "%s", it->first.c_str());
         *total_ms = it->second.first;
         *launches = it->second.second;
+    });
+}
+
+struct TfheMi355Request {
+    CoalescedReq req;
+};
+
+int tfhe_mi355_submit(TfheMi355Context *ctx, int op, const uint64_t *lwe_in, uint64_t *lwe_out, const uint64_t *luts,
+                      size_t lut_count, const uint32_t *lut_indexes, size_t count, TfheMi355Request **out_req) {
+    return guarded([&] {
+        if (!out_req) fail("null argument");
+        *out_req = nullptr;
+        if (!ctx || !lwe_in || !lwe_out) fail("null argument");
+        if (op < 0 || op >= CO_OPS) fail("unknown op %d (0 PBS, 1 KS->PBS, 2 PBS->KS, 3 KS)", op);
+        if (count == 0 || count > coalesce_batch())
+            fail("submit takes 1..%zu ciphertexts (larger batches: the batched entry points)", coalesce_batch());
+        check(hipSetDevice(ctx->device), "hipSetDevice");
+        const bool lut = op != CO_KS;
+        if (lut) {
+            require_fbsk(ctx);
+            if (!luts || lut_count == 0) fail("lut_count must be >= 1");
+            validate_lut_indexes(lut_indexes, count, lut_count);
+        }
+        if (op != CO_PBS) require_ksk(ctx);
+        auto *h = new TfheMi355Request{{lwe_in, lwe_out, lut ? luts : nullptr, lut ? lut_count : 0,
+                                        lut ? lut_indexes : nullptr, count}};
+        coalesce_enqueue(ctx, (CoalescedOp)op, h->req);
+        *out_req = h;
+    });
+}
+
+int tfhe_mi355_wait(TfheMi355Request *req) {
+    return guarded([&] {
+        if (!req) fail("null request");
+        std::unique_ptr<TfheMi355Request> own(req);
+        coalesce_wait(own->req);
     });
 }
 

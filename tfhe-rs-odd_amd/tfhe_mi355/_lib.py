@@ -131,6 +131,9 @@ SIGNATURES = [
     ("tfhe_mi355_kernel_timing_enable", ctypes.c_int, [vp, ctypes.c_int]),
     ("tfhe_mi355_kernel_timing_entry", ctypes.c_int,
      [vp, sz, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]),
+    ("tfhe_mi355_submit", ctypes.c_int,
+     [vp, ctypes.c_int, u64p, u64p, u64p, sz, u32p, sz, ctypes.POINTER(vp)]),
+    ("tfhe_mi355_wait", ctypes.c_int, [vp]),
     ("tfhe_mi355_coalesce_stats", ctypes.c_int,
      [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
       ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double)]),

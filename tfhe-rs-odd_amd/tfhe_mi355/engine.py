@@ -234,6 +234,27 @@ class Engine:
                   L.shape[0], idxp, x.shape[0])
         return out
 
+    # -- asynchronous small calls (tfhe_mi355_submit / _wait, the coalescer's queue) ----------
+    OPS = {"pbs": (0, "n", "big"), "ks_pbs": (1, "big", "big"), "pbs_ks": (2, "n", "n"), "ks": (3, "big", "n")}
+
+    def submit(self, op: str, lwe_in, luts=None, lut_indexes=None) -> "Request":
+        """Enqueue 1..1024 ciphertexts of `op` ("pbs", "ks_pbs", "pbs_ks", "ks") and return at once;
+        `Request.wait()` returns the outputs (every request must be waited on)."""
+        code, din, dout = self.OPS[op]
+        w_in = (self.n if din == "n" else self.big_dim) + 1
+        w_out = (self.n if dout == "n" else self.big_dim) + 1
+        x = np.ascontiguousarray(_u64(lwe_in).reshape(-1, w_in))
+        if code == 3:
+            L, idx, idxp = np.zeros((1, 1), dtype=np.uint64), None, None
+        else:
+            L = self._luts(luts)
+            idx, idxp = self._idx(lut_indexes, x.shape[0], L.shape[0])
+        out = np.empty((x.shape[0], w_out), dtype=np.uint64)
+        h = ctypes.c_void_p()
+        _lib.call("tfhe_mi355_submit", self._h, code, _ptr(x), _ptr(out), _ptr(L), 0 if code == 3 else L.shape[0],
+                  idxp, x.shape[0], ctypes.byref(h))
+        return Request(h, (x, L, idx, out))
+
     def programmable_bootstrap_keyswitch(self, lwe_in, luts, lut_indexes=None) -> np.ndarray:
         x = _u64(lwe_in).reshape(-1, self.n + 1)
         L = self._luts(luts)
@@ -402,3 +423,17 @@ def fill_accumulator(params: ClassicPBSParameters, f) -> np.ndarray:
     cp = c_params(params)
     _lib.call("tfhe_mi355_fill_accumulator", ctypes.byref(cp), _ptr(fv), _ptr(acc))
     return acc
+
+
+class Request:
+    """Handle of a submitted small call (Engine.submit): keeps the host buffers alive until wait()."""
+
+    def __init__(self, handle, buffers):
+        self._h, self._bufs = handle, buffers
+
+    def wait(self) -> np.ndarray:
+        if self._h is None:
+            raise RuntimeError("request already waited on")
+        h, self._h = self._h, None
+        _lib.call("tfhe_mi355_wait", h)
+        return self._bufs[3]
