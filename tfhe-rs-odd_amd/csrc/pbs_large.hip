@@ -786,6 +786,15 @@ __device__ __forceinline__ cx r4_out(cx x0, cx x1, cx x2, cx x3) {
     }
 }
 
+// Wave of (level li, sub-block k) in a group workgroup.  1: w = 2k + li -- the two waves of a
+// pair (which sync with each other in the MAC) are adjacent, so they run on different SIMDs and
+// each SIMD holds waves of two different pairs; 0: w = li KW + k (the pair on one SIMD).
+#ifndef LARGE_GRP_WMAP
+#define LARGE_GRP_WMAP 1
+#endif
+template <int KW>
+__device__ __forceinline__ constexpr int grp_wave(int li, int k) { return LARGE_GRP_WMAP ? 2 * k + li : li * KW + k; }
+
 template <int KW>
 struct LargeGroupCfg {
     static_assert(KW == 2 || KW == 4, "2 or 4 sub-blocks per level per workgroup");
@@ -940,7 +949,7 @@ __device__ __forceinline__ void group_phase1(const LargePbsLaunch &a, int cl, in
                 const int kg = KW * part + k;  // uniform: part is per workgroup
                 const cx x = KW == 4 ? y[l][k] : (part ? y[l][2 + k] : y[l][k]);
                 const cx v = (G + 4 * kg) ? cmulw(x, wt[k].re, wt[k].im) : x;
-                lds[((l * KW + k) * 2 + r) * 512 + (ap - 512 * h)] = make_double2(v.re, v.im);
+                lds[(grp_wave<KW>(l, k) * 2 + r) * 512 + (ap - 512 * h)] = make_double2(v.re, v.im);
             }
         }
     }
@@ -954,8 +963,8 @@ template <int KW, int LI>
 __device__ __forceinline__ void group_mac_pair(cx (&f)[2][16], cx (&v)[16], double2 *lds, int lane, int k,
                                                const double2 *Gb, GroupSync<2> &ps) {
     constexpr int K = 1, L = 2;
-    double2 *own = lds + (LI * KW + k) * 1024 + lane;               // this wave's block
-    const double2 *oth = lds + ((1 - LI) * KW + k) * 1024 + lane;   // the partner's block
+    double2 *own = lds + grp_wave<KW>(LI, k) * 1024 + lane;          // this wave's block
+    const double2 *oth = lds + grp_wave<KW>(1 - LI, k) * 1024 + lane;  // the partner's block
 #pragma unroll
     for (int r = 0; r < 2; r++)
 #pragma unroll
@@ -1015,7 +1024,7 @@ __device__ __forceinline__ void group_cmux_body(const LargePbsLaunch &a, int i, 
     using Cfg = LargeGroupCfg<KW>;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int li = wave / KW, k = wave % KW;
+    const int li = LARGE_GRP_WMAP ? wave & 1 : wave / KW, k = LARGE_GRP_WMAP ? wave >> 1 : wave % KW;
     const int sblk = G + 4 * (KW * part + k);
     double2 *s1 = lds + Cfg::REGION;
     // sub-block stage twiddles W_1024[lane c] = W_M[16 lane c]  (oracle dif_rec tstride 16)
