@@ -13,7 +13,8 @@ step() {  # step NAME TIMEOUT CMD...
   return 0
 }
 if [ -n "$TRY_TESTS" ]; then
-  step tests 600 python -u -m pytest $TRY_TESTS -x -q --timeout 300 --timeout-method thread
+  TFHE_MI355_LIB=${TEST_VARIANT:+$PWD/tfhe-rs-odd_amd/build/$TEST_VARIANT/libtfhe_mi355.so} \
+    step tests 600 python -u -m pytest $TRY_TESTS -x -q --timeout 300 --timeout-method thread
   tail -1 $out/tests.log
 fi
 for pass in ${PASSES:-1 2}; do

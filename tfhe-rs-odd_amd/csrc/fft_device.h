@@ -247,6 +247,15 @@ __device__ __forceinline__ double2 buffer_ld_d2(__amdgpu_buffer_rsrc_t r, uint32
     const v4u t = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
     return make_double2(__hiloint2double((int)t.y, (int)t.x), __hiloint2double((int)t.w, (int)t.z));
 }
+// 16-byte store through a buffer resource with cache-policy bits aux (gfx950: 16 = sc1, a
+// write-through store whose line leaves the XCD's L2 at once)
+template <int AUX>
+__device__ __forceinline__ void buffer_st_d2p(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double2 x) {
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    const v4u t = {(unsigned)__double2loint(x.x), (unsigned)__double2hiint(x.x), (unsigned)__double2loint(x.y),
+                   (unsigned)__double2hiint(x.y)};
+    __builtin_amdgcn_raw_buffer_store_b128(t, r, voff, soff, AUX);
+}
 __device__ __forceinline__ cx gld(const double2 *__restrict__ p) {
     double2 t = *p;
     return {t.x, t.y};

@@ -789,6 +789,15 @@ __device__ __forceinline__ cx r4_out(cx x0, cx x1, cx x2, cx x3) {
 // Wave of (level li, sub-block k) in a group workgroup.  1: w = 2k + li -- the two waves of a
 // pair (which sync with each other in the MAC) are adjacent, so they run on different SIMDs and
 // each SIMD holds waves of two different pairs; 0: w = li KW + k (the pair on one SIMD).
+#ifndef LARGE_TSKIP
+#define LARGE_TSKIP 0  // timing-only builds (wrong outputs): 1 no phase 1, 2 no GGSW loads, 4 no U stores
+#endif
+#ifndef LARGE_U_AUX
+#define LARGE_U_AUX 16  // cache policy of the group kernel's U stores: 16 = sc1 (write-through), 0 = plain
+#endif
+#ifndef LARGE_ACC_AUX
+#define LARGE_ACC_AUX 0  // cache policy of top_inv's accumulator stores (16 = sc1)
+#endif
 #ifndef LARGE_GRP_WMAP
 #define LARGE_GRP_WMAP 1
 #endif
@@ -989,10 +998,14 @@ __device__ __forceinline__ void group_mac_pair(cx (&f)[2][16], cx (&v)[16], doub
 #pragma unroll
         for (int c = 0; c < 2; c++) {
             // ggsw.rs:524-567: p = (lvl - 1)(k + 1) + r, lvl = L..1, r = 0..k; GGSW poly p (k+1) + c
+#if LARGE_TSKIP & 2  // timing only: no GGSW loads
+            const double2 g0 = make_double2(1.0 + lane, 2.0), g1 = make_double2(3.0, 1.0 + c), g2 = make_double2(sp, 0.5), g3 = g0;
+#else
             const double2 g0 = Gb[(size_t)((L - 1) * (K + 1) * (K + 1) + c) * LM + s * 64];
             const double2 g1 = Gb[(size_t)(((L - 1) * (K + 1) + 1) * (K + 1) + c) * LM + s * 64];
             const double2 g2 = Gb[(size_t)c * LM + s * 64];
             const double2 g3 = Gb[(size_t)((K + 1) + c) * LM + s * 64];
+#endif
             cx t;
             t.re = fma(g0.x, fl[0].re, -(g0.y * fl[0].im));
             t.im = fma(g0.x, fl[0].im, g0.y * fl[0].re);
@@ -1039,7 +1052,8 @@ __device__ __forceinline__ void group_cmux_body(const LargePbsLaunch &a, int i, 
     for (int h = 0; h < 2; h++) {
         if (h) __syncthreads();  // every wave has picked up half 0
 #pragma unroll
-        for (int q = 0; q < 512 / Cfg::THREADS; q++) group_phase1<KW, G>(a, cl, part, 512 * h + Cfg::THREADS * q + tid, h, lds);
+        for (int q = 0; q < 512 / Cfg::THREADS; q++)
+            if (!(LARGE_TSKIP & 1)) group_phase1<KW, G>(a, cl, part, 512 * h + Cfg::THREADS * q + tid, h, lds);
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < 2; r++)
@@ -1062,7 +1076,11 @@ __device__ __forceinline__ void group_cmux_body(const LargePbsLaunch &a, int i, 
     const int col = 1 - li;
     double2 *dst = a.spectra + ((size_t)cl * L * (K + 1) + col) * LM + 1024 * sblk + lane;
 #pragma unroll
-    for (int b = 0; b < 16; b++) dst[64 * b] = make_double2(v[b].re, v[b].im);
+    for (int b = 0; b < 16; b++) {
+        if ((LARGE_TSKIP & 4) && a.n != 12345) continue;
+        if (LARGE_U_AUX) buffer_st_d2p<LARGE_U_AUX>(make_rsrc(dst - lane), 16u * (lane + 64 * b), 0, make_double2(v[b].re, v[b].im));
+        else dst[64 * b] = make_double2(v[b].re, v[b].im);
+    }
 }
 
 // rotation + decomposition of CMUX i for the grouped path at positions j and j + M of row r
@@ -1156,9 +1174,14 @@ __device__ __forceinline__ void top_inv_body(const LargePbsLaunch &a, int cl, in
             hi = pr.y;
             backward_add(u[b], w, lo, hi, k32);  // the resident key carries the 1/M
         }
-        pr.x = lo;
-        pr.y = hi;
-        *reinterpret_cast<acc_pair *>(acc + 2 * j) = pr;
+        if (LARGE_ACC_AUX) {
+            const double2 w2 = make_double2(__longlong_as_double((long long)lo), __longlong_as_double((long long)hi));
+            buffer_st_d2p<LARGE_ACC_AUX>(make_rsrc(acc), 16u * j, 0, w2);
+        } else {
+            pr.x = lo;
+            pr.y = hi;
+            *reinterpret_cast<acc_pair *>(acc + 2 * j) = pr;
+        }
     }
 }
 
