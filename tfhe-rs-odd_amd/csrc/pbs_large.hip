@@ -108,6 +108,14 @@ __device__ __forceinline__ size_t spec_off(int wave, int h, int s, int lane) {
 
 }  // namespace
 
+// Cache policy of the stores of f64 spectra that a later launch reads, mostly on other XCDs
+// (gfx950 aux bits: 16 = sc1, write-through -- the line leaves the XCD's L2 at once instead of in
+// the end-of-kernel L2 writeback; 0 = plain): large_top_fwd's top-stage spectra here, the
+// sub-block outputs (LARGE_SUB_AUX, LARGE_U_AUX) below.
+#ifndef LARGE_TOPF_AUX
+#define LARGE_TOPF_AUX 0
+#endif
+
 // Shapes of the split CMUX (N = 4096 ... 32768, k = 1): M = N / 2 = R x 1024 -- a top radix-R
 // stage and R independent 1024-point sub-blocks ([R | 16, 16, 4], the oracle's radix_plan).
 template <int N>
@@ -285,12 +293,17 @@ __device__ __forceinline__ void top_fwd_body(const LargePbsLaunch &a, int ct0, i
     auto top_and_store = [&](int lvl) {
         dftR_fwd<R>(u);
         double2 *T = a.spectra + (((size_t)cl * L + (lvl - 1)) * (K + 1) + r) * M + t;
-        T[0] = make_double2(u[0].re, u[0].im);
+        // read by the sub-block workgroups, mostly on other XCDs
+        auto st = [&](int c, double2 x) {
+            if (LARGE_TOPF_AUX) buffer_st_d2p<LARGE_TOPF_AUX>(make_rsrc(T - t), 16u * (t + 1024 * c), 0, x);
+            else T[1024 * c] = x;
+        };
+        st(0, make_double2(u[0].re, u[0].im));
 #pragma unroll
         for (int c = 1; c < R; c++) {
             const cx w = gld(a.wtop + (c - 1) * 1024 + t);  // = W[t c]
             const cx y = cmulw(u[c], w.re, w.im);
-            T[1024 * c] = make_double2(y.re, y.im);
+            st(c, make_double2(y.re, y.im));
         }
     };
     top_and_store(L);
@@ -322,6 +335,22 @@ __global__ void __launch_bounds__(TOPT, (top_fwd_wpe<N, L>())) large_top_fwd_ker
     const int cl = x + 8 * (m / ((K + 1) * BPP));
     if (cl >= a.chunk_count) return;  // whole workgroup
     top_fwd_body<N, K, L, G>(a, ct0, i, cl, sub / BPP, (sub % BPP) * TOPT + threadIdx.x);
+}
+
+#ifndef LARGE_U_AUX
+#define LARGE_U_AUX 16  // cache policy of the group kernel's U stores: 16 = sc1 (write-through), 0 = plain
+#endif
+#ifndef LARGE_SUB_AUX
+#define LARGE_SUB_AUX 16  // the same for the split path's sub-block outputs (large_sub / dsub / pair_sub)
+#endif
+// sub-block output of one wave: 16 x 16 B per lane, cache policy AUX (16: write-through)
+template <int AUX>
+__device__ __forceinline__ void store_sub_out(double2 *dst, const cx (&v)[16], int lane) {
+#pragma unroll
+    for (int b = 0; b < 16; b++) {
+        if (AUX) buffer_st_d2p<AUX>(make_rsrc(dst - lane), 16u * (lane + 64 * b), 0, make_double2(v[b].re, v[b].im));
+        else dst[64 * b] = make_double2(v[b].re, v[b].im);
+    }
 }
 
 // (k+1) L waves; LDS: one 1024-entry buffer per wave + the sub-block twiddle table
@@ -410,8 +439,7 @@ __device__ __forceinline__ void sub_cmux_body(const LargePbsLaunch &a, int i, in
     if (!mac) return;
     SubFft::inverse(v, xb, tw, lane, wsync);
     double2 *dst = T + (size_t)wave * M + 1024 * q + lane;  // (lvl 1, row c) slot: read by this WG only
-#pragma unroll
-    for (int b = 0; b < 16; b++) dst[64 * b] = make_double2(v[b].re, v[b].im);
+    store_sub_out<LARGE_SUB_AUX>(dst, v, lane);
 }
 
 // classic CMUX sub-blocks from large_top_fwd's spectra (the multi-bit sets run
@@ -740,8 +768,7 @@ __global__ void __launch_bounds__((PairSubCfg<K, L>::THREADS), 2) large_pair_sub
     SubFft::inverse(v, xb, tw, lane, wsync);
     if (2 * cp + c >= cnt) return;
     double2 *dst = spectra(c) + (size_t)col * M + 1024 * q + lane;  // (lvl 1, row col) slot: this WG only
-#pragma unroll
-    for (int b = 0; b < 16; b++) dst[64 * b] = make_double2(v[b].re, v[b].im);
+    store_sub_out<LARGE_SUB_AUX>(dst, v, lane);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -791,9 +818,6 @@ __device__ __forceinline__ cx r4_out(cx x0, cx x1, cx x2, cx x3) {
 // each SIMD holds waves of two different pairs; 0: w = li KW + k (the pair on one SIMD).
 #ifndef LARGE_TSKIP
 #define LARGE_TSKIP 0  // timing-only builds (wrong outputs): 1 no phase 1, 2 no GGSW loads, 4 no U stores
-#endif
-#ifndef LARGE_U_AUX
-#define LARGE_U_AUX 16  // cache policy of the group kernel's U stores: 16 = sc1 (write-through), 0 = plain
 #endif
 #ifndef LARGE_ACC_AUX
 #define LARGE_ACC_AUX 0  // cache policy of top_inv's accumulator stores (16 = sc1)
@@ -1075,12 +1099,7 @@ __device__ __forceinline__ void group_cmux_body(const LargePbsLaunch &a, int i, 
     SubFft::inverse(v, xb, tw, lane, wsync);
     const int col = 1 - li;
     double2 *dst = a.spectra + ((size_t)cl * L * (K + 1) + col) * LM + 1024 * sblk + lane;
-#pragma unroll
-    for (int b = 0; b < 16; b++) {
-        if ((LARGE_TSKIP & 4) && a.n != 12345) continue;
-        if (LARGE_U_AUX) buffer_st_d2p<LARGE_U_AUX>(make_rsrc(dst - lane), 16u * (lane + 64 * b), 0, make_double2(v[b].re, v[b].im));
-        else dst[64 * b] = make_double2(v[b].re, v[b].im);
-    }
+    if (!(LARGE_TSKIP & 4) || a.n == 12345) store_sub_out<LARGE_U_AUX>(dst, v, lane);
 }
 
 // rotation + decomposition of CMUX i for the grouped path at positions j and j + M of row r
