@@ -110,10 +110,12 @@ __device__ __forceinline__ size_t spec_off(int wave, int h, int s, int lane) {
 
 // Cache policy of the stores of f64 spectra that a later launch reads, mostly on other XCDs
 // (gfx950 aux bits: 16 = sc1, write-through -- the line leaves the XCD's L2 at once instead of in
-// the end-of-kernel L2 writeback; 0 = plain): large_top_fwd's top-stage spectra here, the
-// sub-block outputs (LARGE_SUB_AUX, LARGE_U_AUX) below.
+// the end-of-kernel L2 writeback; 0 = plain): large_top_fwd's top-stage spectra here (-1:
+// write-through for the multi-bit path only -- its paired sub-block kernel reads them on other
+// XCDs: g3 8969 -> 9089 KS+PBS/s, while 2_5 lost 2260 -> 2241), the sub-block outputs
+// (LARGE_SUB_AUX, LARGE_U_AUX) below.
 #ifndef LARGE_TOPF_AUX
-#define LARGE_TOPF_AUX 0
+#define LARGE_TOPF_AUX (-1)
 #endif
 
 // Shapes of the split CMUX (N = 4096 ... 32768, k = 1): M = N / 2 = R x 1024 -- a top radix-R
@@ -295,7 +297,8 @@ __device__ __forceinline__ void top_fwd_body(const LargePbsLaunch &a, int ct0, i
         double2 *T = a.spectra + (((size_t)cl * L + (lvl - 1)) * (K + 1) + r) * M + t;
         // read by the sub-block workgroups, mostly on other XCDs
         auto st = [&](int c, double2 x) {
-            if (LARGE_TOPF_AUX) buffer_st_d2p<LARGE_TOPF_AUX>(make_rsrc(T - t), 16u * (t + 1024 * c), 0, x);
+            constexpr int AUX = LARGE_TOPF_AUX < 0 ? (G > 0 ? 16 : 0) : LARGE_TOPF_AUX;
+            if (AUX) buffer_st_d2p<AUX>(make_rsrc(T - t), 16u * (t + 1024 * c), 0, x);
             else T[1024 * c] = x;
         };
         st(0, make_double2(u[0].re, u[0].im));
