@@ -510,7 +510,16 @@ OTHER_WORKLOADS = (
     ("4_4", "4_4", {"steps": 3}),
     ("mul32", "mul32", {"steps": 2}),
     ("4_4_full", "4_4", {"steps": 1, "global_batch": 65536, "warmup_batch": 1024}),
+    ("3_3", "3_3", {"steps": 3}),
+    ("mb3_3g3", "mb3_3g3", {"steps": 3}),
 )
+# Wall-clock budget of one such workload (keys, warm-up, steps, checks).  N = 1: the child's
+# subprocess timeout; N > 1: a per-rank watchdog (below).  BENCH_WORKLOAD_BUDGET_S overrides.
+WORKLOAD_BUDGET_S = 420.0
+
+
+def workload_budget() -> float:
+    return float(os.environ.get("BENCH_WORKLOAD_BUDGET_S", WORKLOAD_BUDGET_S))
 
 
 def summarize(line: dict) -> dict:
@@ -520,7 +529,8 @@ def summarize(line: dict) -> dict:
             "scaling": line.get("scaling"), "workload": line["config"]["workload"],
             "batch": line["config"].get("global_batch", line["config"].get("global_pairs")),
             "kernel": rl.get("kernel"), "bound": rl.get("bound"), "frac": rl.get("frac"),
-            "check": line.get("check")}
+            "check": line.get("check"), "setup": line.get("setup"),
+            "single_call_latency_ms": line.get("single_call_latency_ms")}
 
 
 def _child_args(args, params, opts) -> list:
@@ -542,30 +552,39 @@ def other_workloads(args) -> dict:
     for name, params, opts in OTHER_WORKLOADS:
         cmd = [sys.executable, os.path.abspath(__file__)] + _child_args(args, params, opts)
         t = time.perf_counter()
+        budget = workload_budget()
         try:
-            cp = subprocess.run(cmd, capture_output=True, text=True, timeout=420)
+            cp = subprocess.run(cmd, capture_output=True, text=True, timeout=budget)
             lines = [l for l in cp.stdout.splitlines() if l.startswith("{")]
             if cp.returncode != 0 or not lines:
                 res[name] = {"error": f"rc={cp.returncode}: {cp.stderr.strip()[-300:]}"}
             else:
                 res[name] = summarize(json.loads(lines[-1]))
         except subprocess.TimeoutExpired:
-            res[name] = {"error": "timeout after 420 s"}
+            res[name] = {"error": f"timeout after {budget:.0f} s"}
         res[name]["wall_s"] = time.perf_counter() - t
         print(f"bench.py: {name} done in {res[name]['wall_s']:.1f} s", file=sys.stderr, flush=True)
     return res
 
 
-def other_workloads_ranks(args, R, runner) -> dict:
+def other_workloads_ranks(args, R, runner, emit=None) -> dict:
     """N > 1 (every rank of the driver's torch.distributed.run runs this): the same configurations
     in-process, one after the other on the job's process group, each a full multi-rank run
-    (keys broadcast once, contiguous shards, barrier-bracketed timing, max wall over ranks), before
+    (keys broadcast once, contiguous shards, barrier-bracketed timing, max wall over ranks), after
     the headline.  `runner(args) -> line` (rank 0) runs one workload; the CPU self-test passes a
-    stub.  Device memory of one workload is released before the next."""
+    stub.  Device memory of one workload is released before the next.
+
+    Each workload runs under a per-rank watchdog of workload_budget() seconds (no re-exec: a
+    thread).  A rank over budget (a stuck kernel, or a collective waiting on a stuck peer -- every
+    rank's watchdog then fires) marks that entry as an error; rank 0 calls `emit(res)` to print the
+    merged line with what was measured so far, and every rank exits with status 3, so the job ends
+    non-zero instead of stalling the whole multi-GPU run."""
     import copy
     import gc
+    import threading
 
     res = {}
+    budget = workload_budget()
     for name, params, opts in OTHER_WORKLOADS:
         a = copy.copy(args)
         a.params, a.steps, a.warmup = params, opts["steps"], opts.get("warmup", 1)
@@ -575,7 +594,23 @@ def other_workloads_ranks(args, R, runner) -> dict:
         a.batch = args.batch if args.launch_selftest else 0
         a.other = None
         t = time.perf_counter()
-        line = runner(a)
+
+        def over_budget(name=name, t=t):
+            res[name] = {"error": f"over its {budget:.0f} s budget on rank {R.rank} (watchdog)",
+                         "wall_s": time.perf_counter() - t}
+            print(f"bench.py: rank {R.rank}: {name} exceeded {budget:.0f} s; exiting", file=sys.stderr, flush=True)
+            if R.rank == 0 and emit is not None:
+                emit(res)
+            sys.stdout.flush()
+            os._exit(3)
+
+        dog = threading.Timer(budget, over_budget)
+        dog.daemon = True
+        dog.start()
+        try:
+            line = runner(a)
+        finally:
+            dog.cancel()
         if R.rank == 0:
             res[name] = summarize(line)
             res[name]["wall_s"] = time.perf_counter() - t
@@ -668,13 +703,12 @@ def run_selftest(args) -> int:
     import torch
 
     R = Ranks(torch.device("cpu"), os.environ.get("BENCH_DIST_BACKEND", "gloo"))
-    other = None
-    if args.params is None and not args.no_other_workloads and R.world > 1:
-        other = other_workloads_ranks(args, R, lambda a: selftest_line(a, R))
     line = selftest_line(args, R)
+    if args.params is None and not args.no_other_workloads and R.world > 1:
+        line = merge_other(line, other_workloads_ranks(args, R, lambda a: selftest_line(a, R),
+                                                       emit=lambda res: print(json.dumps(merge_other(line, res)),
+                                                                              flush=True)))
     if R.rank == 0:
-        if other is not None:
-            line["other_workloads"] = other
         print(json.dumps(line), flush=True)
     R.finish()
     return 0
@@ -689,6 +723,8 @@ def selftest_line(args, R) -> dict | None:
     lo, hi = shard_range(G, R.rank, R.world)
     msgs = np.random.default_rng(args.seed).integers(0, 16, G).astype(np.uint64)[lo:hi]
     per_step = 0.02 * (R.rank + 1)   # ranks run at different speeds: the max must win
+    if args.params and args.params == os.environ.get("BENCH_SELFTEST_STALL"):
+        time.sleep(3600)             # a stuck workload (tests the per-workload watchdog)
 
     def step():
         time.sleep(per_step)
@@ -766,12 +802,30 @@ def main():
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     R = Ranks(device, os.environ.get("BENCH_DIST_BACKEND", "nccl"))  # nccl = RCCL over xGMI
-    if default_run and ws > 1:
-        args.other = other_workloads_ranks(args, R, lambda a: run_workload(a, R))
     line = run_workload(args, R)
+    if args.other is not None:  # N = 1: measured by the child runs above
+        line = merge_other(line, args.other)
+    if default_run and ws > 1:
+        # after the headline, so that a workload over its budget still leaves a complete line
+        line = merge_other(line, other_workloads_ranks(args, R, lambda a: run_workload(a, R),
+                                                       emit=lambda res: print(json.dumps(merge_other(line, res)),
+                                                                              flush=True)))
     if R.rank == 0:
         print(json.dumps(line), flush=True)
     R.finish()
+
+
+def merge_other(line, res):
+    """The headline line (rank 0) with the other configurations' entries; an entry that failed
+    makes the line say so (`other_workloads_errors`)."""
+    if line is None:
+        return None
+    out = dict(line)
+    out["other_workloads"] = dict(res)
+    bad = sorted(k for k, v in res.items() if "error" in v)
+    if bad:
+        out["other_workloads_errors"] = bad
+    return out
 
 
 def run_workload(args, R) -> dict | None:
@@ -820,11 +874,17 @@ def make_keys(args, P, R, with_ks):
         if R.rank == 0:
             ksk = client.gen_keyswitch_key(args.seed + 200, glwe_sk, lwe_sk, P.ks_base_log, P.ks_level,
                                            P.lwe_modular_std_dev)
+        t = time.perf_counter()
         d_ksk = broadcast_u64(ksk, ksk_len, 0, R.device if R.backend != "gloo" else torch.device("cpu"))
+        torch.cuda.synchronize()
+        t_bc_ksk = time.perf_counter() - t
         eng.upload_keyswitch_key_device(d_ksk.to(R.device), ksk_len)
         del d_ksk
     torch.cuda.synchronize()
-    return eng, lwe_sk, glwe_sk, bsk, ksk, {"bsk_keygen_s": t_gen, "bsk_broadcast_s": t_bc}
+    setup = {"bsk_keygen_s": t_gen, "bsk_broadcast_s": t_bc}
+    if with_ks:
+        setup["ksk_broadcast_s"] = t_bc_ksk
+    return eng, lwe_sk, glwe_sk, bsk, ksk, setup
 
 
 def host_abi_rate(eng, P, cts, acc, with_ks: bool, reps: int = 3) -> dict:
@@ -1029,8 +1089,6 @@ def run_pbs(args, P, pname, workload, kname, R):
         }
         if host_abi:
             line["host_abi"] = host_abi
-        if args.other:
-            line["other_workloads"] = args.other
         if R.world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or cpu_share()
             line["cpu_baseline"] = cpu_baseline(P, bsk, cts, acc, threads, ksk)
@@ -1053,16 +1111,24 @@ def run_mul32(args, P, workload, kname, R):
     bsk_len = ggsw_count(P) * P.pbs_level * (P.glwe_dimension + 1) ** 2 * P.polynomial_size
     ksk_len = P.big_lwe_dimension * P.ks_level * (P.lwe_dimension + 1)
     bsk = ksk = None
+    t = time.perf_counter()
     if R.rank == 0:
         bsk = client.gen_bootstrap_key(args.seed + 100, ck.small_lwe_secret_key, ck.glwe_secret_key,
                                        P.glwe_dimension, P.polynomial_size, P.pbs_base_log, P.pbs_level,
                                        P.glwe_modular_std_dev)
         ksk = client.gen_keyswitch_key(args.seed + 200, ck.large_lwe_secret_key, ck.small_lwe_secret_key,
                                        P.ks_base_log, P.ks_level, P.lwe_modular_std_dev)
+    t_gen = time.perf_counter() - t
     bdev = R.device if R.backend != "gloo" else torch.device("cpu")
+    t = time.perf_counter()
     d = broadcast_u64(bsk, bsk_len, 0, bdev)
+    torch.cuda.synchronize()
+    t_bc = time.perf_counter() - t
     eng.convert_bootstrap_key_device(d.to(R.device), bsk_len)
+    t = time.perf_counter()
     d = broadcast_u64(ksk, ksk_len, 0, bdev)
+    torch.cuda.synchronize()
+    t_bc_ksk = time.perf_counter() - t
     eng.upload_keyswitch_key_device(d.to(R.device), ksk_len)
     torch.cuda.synchronize()
     del d
@@ -1126,6 +1192,7 @@ def run_mul32(args, P, workload, kname, R):
             "pbs_per_sec": pbs_rate,
             "roofline": rl,
             "check": {"decrypted_ok": agg["ok"], "of": agg["of"]},
+            "setup": {"keygen_s": t_gen, "bsk_broadcast_s": t_bc, "ksk_broadcast_s": t_bc_ksk},
         }
         if R.world == 1 and not args.no_cpu_baseline:
             sys.path.insert(0, ROOT)

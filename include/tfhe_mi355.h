@@ -31,10 +31,14 @@
  *     concurrently only when half a batch is queued; the one-ciphertext-per-call pattern,
  *     shortint/server_key/mod.rs:783-857; TFHE_MI355_COALESCE_MAX_COUNT=0 turns it off).
  *     The _async calls hold no per-context mutable state: every device scratch buffer they
- *     need comes from the caller (d_scratch, sized by the matching *_scratch query;
- *     a query returning 0 means d_scratch may be NULL), so concurrent callers on different
- *     streams only need scratch buffers of their own, and the calls can be captured into a
- *     hipGraph (no allocation or synchronisation inside);
+ *     need comes from the caller (d_scratch, sized by the matching *_scratch query; a call
+ *     given less than its query fails with an error, and only a query returning 0 allows
+ *     d_scratch = NULL), so concurrent callers on different streams only need scratch buffers
+ *     of their own, and the calls can be captured into a hipGraph (no allocation or
+ *     synchronisation inside);
+ *   - keys: a key upload (any *_key_upload*, *_set_ready) waits for the coalesced batches in
+ *     flight and blocks new ones until it is done; _async calls are not ordered with uploads:
+ *     do not re-upload a key while _async work that reads it may still run;
  *   - _async lut index arrays are not checked on the host (they live on the device): an entry
  *     >= lut_count is clamped to lut_count - 1 by the kernels (no out-of-bounds read); the
  *     host-pointer forms reject such an entry with an error;
@@ -68,7 +72,8 @@ typedef struct {
     uint32_t ks_level;
     uint32_t message_modulus;
     uint32_t carry_modulus;
-    uint32_t grouping_factor; /* 0 = classic; 2, 3 = multi-bit (N=2048, L=1)  */
+    uint32_t grouping_factor; /* 0 = classic; 2, 3 = multi-bit: N = 2048 (k = 1, L = 1),
+                                 N = 512 (k = 3, L = 1), N = 8192 (k = 1, L = 2)  */
 } TfheMi355Parameters;
 
 /* Thread-local text of the last failure ("" if none). */
@@ -94,7 +99,8 @@ int tfhe_mi355_kernel_timing_entry(TfheMi355Context *ctx, size_t index, char *na
  * as those entry points, luts ignored for op 3) and returns at once with a request handle;
  * tfhe_mi355_wait blocks until the outputs are written and frees the handle (every submitted
  * request must be waited on exactly once, before the buffers are reused or the context is
- * destroyed).  One thread can keep many requests in flight: a rayon worker can submit every block
+ * destroyed; a request still queued when tfhe_mi355_context_destroy runs is not run: destroy
+ * returns 1, and that request's wait returns 1 with a message).  One thread can keep many requests in flight: a rayon worker can submit every block
  * of its share of an integer layer, then wait for them (the reference calls
  * keyswitch_programmable_bootstrap_assign per block, shortint/server_key/mod.rs:783-857), so the
  * coalesced batch is no longer capped by the number of threads. */
@@ -120,10 +126,16 @@ int tfhe_mi355_host_alloc(size_t bytes, void **out_ptr);
 int tfhe_mi355_host_free(void *ptr);
 
 /* Create / destroy an engine context on `device`.
+ * Accepted decompositions: 2 <= pbs_base_log and pbs_base_log * pbs_level <= 30 for N <= 2048 and
+ * multi-bit; <= 63 for classic N >= 4096, with pbs_base_log <= 15 when pbs_level > 1 (the split
+ * CMUX packs signed digits into int16).  Every reference parameter set is inside these bounds.
  * Replaces Fft::new + the shortint engine's thread-local buffers
  * (fft64/math/fft/mod.rs:146-193, shortint/engine/mod.rs:23-70,163-235). */
 int tfhe_mi355_context_create(const TfheMi355Parameters *params, int device,
                               TfheMi355Context **out_ctx);
+/* Destroy stops the request coalescer first (a batch already running completes), then frees the
+ * device state.  Requests still queued are failed, not run: their tfhe_mi355_wait returns 1, and
+ * destroy itself returns 1 saying how many there were (the context is destroyed all the same). */
 int tfhe_mi355_context_destroy(TfheMi355Context *ctx);
 
 /* Upload a standard-domain (u64) bootstrapping key and convert it to the engine's Fourier
@@ -168,9 +180,17 @@ int tfhe_mi355_programmable_bootstrap_async(TfheMi355Context *ctx, const uint64_
                                             size_t lut_count, const uint32_t *d_lut_indexes,
                                             size_t count, void *d_scratch, size_t scratch_bytes,
                                             void *stream);
-/* Device scratch (bytes) of the async PBS for `count` ciphertexts: 0 for N <= 2048 and multi-bit;
- * at N = 32768 the accumulators + spectra of one pass (1.5 MiB per ciphertext, passes of <= 128;
- * less scratch = smaller passes, at least one ciphertext's worth). */
+/* Device scratch (bytes) of the async PBS for `count` ciphertexts (count >= 1):
+ *   - classic N <= 2048: 256 bytes (the persistent grid's ciphertext ticket) at the shapes that
+ *     run it -- N = 2048 k = 1 L = 1 (every 2_2-like shortint set), N = 1024 k = 1 L = 2,
+ *     N = 1024 k = 2 L = 3, N = 256 k = 5 L = 1 -- and 0 at the other classic shapes;
+ *   - multi-bit N = 2048 / 512: 0;
+ *   - N >= 4096, classic and multi-bit (N = 8192): the accumulators + spectra of one pass of
+ *     min(count, chunk) ciphertexts (chunk = 128 at N = 32768, ~160 MiB worth below; e.g.
+ *     1.5 MiB per ciphertext at 4_4).  Less scratch runs smaller passes; the call fails below one
+ *     ciphertext's worth.
+ * tfhe_mi355_programmable_bootstrap_async fails when given less than this (N <= 2048) -- it never
+ * falls back silently.  tfhe_mi355_blind_rotate_async takes no scratch and runs the one-pass grid. */
 int tfhe_mi355_programmable_bootstrap_scratch(TfheMi355Context *ctx, size_t count, size_t *bytes);
 
 /* Batched blind rotation WITHOUT sample extraction: glwe_out[c] = the rotated accumulator
@@ -197,7 +217,7 @@ int tfhe_mi355_context_parameters(TfheMi355Context *ctx, TfheMi355Parameters *ou
  *   ServerKey (shortint/server_key/mod.rs:283-297): standard LWE keyswitching key +
  *     Fourier bootstrapping key in concrete-fft's serialized form (FourierPolynomialList,
  *     fft64/math/fft/mod.rs:588-717: natural DFT order), mapped into the engine layout
- *     (N = 2048 and 32768).  Replaces the ServerKey deserialisation feeding the CPU PBS.
+ *     (every N = 256 ... 32768).  Replaces the ServerKey deserialisation feeding the CPU PBS.
  * Only native (2^64) ciphertext moduli.  *_inspect parses and validates without a GPU and
  * reports the parameter set the key implies (create the context from info.params); *_upload
  * requires a context with exactly that parameter set.  Truncated or inconsistent input fails
@@ -215,8 +235,8 @@ int tfhe_mi355_compressed_server_key_inspect(const uint8_t *bytes, size_t len, T
 int tfhe_mi355_compressed_server_key_upload(TfheMi355Context *ctx, const uint8_t *bytes, size_t len);
 int tfhe_mi355_server_key_inspect(const uint8_t *bytes, size_t len, TfheMi355ServerKeyInfo *info);
 int tfhe_mi355_server_key_upload(TfheMi355Context *ctx, const uint8_t *bytes, size_t len);
-/* engine Fourier layout: freq[e] = natural DFT index held by element e of a polynomial
- * (N = 2048: M = 1024 entries; N = 32768: 16384) -- host-only, no GPU needed */
+/* engine Fourier layout: freq[e] = natural DFT index held by element e of a polynomial, M = N/2
+ * entries, for every N = 256 ... 32768 -- host-only, no GPU needed */
 int tfhe_mi355_fourier_engine_frequency(uint32_t N, uint32_t *freq);
 
 /* Seeded (compressed) keys: the reference's SeededLweBootstrapKey / SeededLweKeyswitchKey

@@ -98,3 +98,22 @@ def test_multi_rank_default_run_merges_every_configuration():
             assert e["batch"] == 16 and e["scaling"] == "weak"
         assert e["check"]["decrypted_ok"] == e["check"]["of"] == e["batch"]
     assert d["world_size"] == 2 and d["check"]["decrypted_ok"] == 16
+
+
+@pytest.mark.timeout(240)
+def test_multi_rank_workload_over_budget_still_prints_the_line():
+    """N > 1: one configuration stalls (stub sleeping far past BENCH_WORKLOAD_BUDGET_S): every
+    rank's watchdog fires, rank 0 prints the merged line -- the headline (measured first), the
+    configurations measured before the stall, and that entry marked as an error -- and the job
+    exits non-zero instead of hanging the multi-GPU run."""
+    p, lines = _run(["--gpus", "2", "--launch-selftest", "--steps", "2", "--warmup", "1", "--batch", "8"],
+                    extra_env={"BENCH_SELFTEST_STALL": "mb2", "BENCH_WORKLOAD_BUDGET_S": "4"})
+    assert p.returncode != 0
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["check"]["decrypted_ok"] == 16            # the headline
+    ow = d["other_workloads"]
+    assert "error" in ow["mb2"] and "budget" in ow["mb2"]["error"]
+    assert d["other_workloads_errors"] == ["mb2"]
+    assert ow["mb3"]["world_size"] == 2 and "error" not in ow["mb3"]   # ran before the stall
+    assert "4_4" not in ow                               # never started

@@ -173,4 +173,21 @@ def test_engine_frequency_matches_oracle_position_order(orc, N):
     pos = 1024 * blk + 64 * (lane & 15) + 16 * (lane >> 4) + s
     assert np.array_equal(S.engine_frequency(N).astype(np.int64), orc.pos_freq(N)[pos])
     with pytest.raises(Exception, match="supports"):
-        S.engine_frequency(1024)
+        S.engine_frequency(128)
+
+
+@pytest.mark.parametrize("N", [256, 512, 1024])
+def test_small_n_engine_frequency_matches_oracle_position_order(orc, N):
+    """N <= 1024 (WaveFft<128> / <256> / <512>, fft_device.h): element e of the engine layout holds
+    FFT position P(e), whose frequency is the oracle's digit reversal of the plan."""
+    e = np.arange(N // 2)
+    lane, s = e % 64, e // 64
+    if N == 1024:    # [8, 8, 8]: lane L, slot s <-> 64 (L & 7) + 8 (L >> 3) + s
+        pos = 64 * (lane & 7) + 8 * (lane >> 3) + s
+    elif N == 512:   # [16, 16]: lane L, slot q <-> 16 (L & 15) + (L >> 4) + 4 q
+        pos = 16 * (lane & 15) + (lane >> 4) + 4 * s
+    else:            # [16, 8]: natural = Fourier layout
+        pos = e
+    f = S.engine_frequency(N).astype(np.int64)
+    assert np.array_equal(np.sort(f), e)
+    assert np.array_equal(f, orc.pos_freq(N)[pos])

@@ -84,15 +84,25 @@ def test_compressed_server_key_wrong_context_is_rejected():
         eng.upload_compressed_server_key(data)
 
 
-@pytest.mark.parametrize("which", ["2_2", "mb_g3"])
+@pytest.mark.parametrize("which", ["2_2", "mb_g3", "1_1", "1_0", "1_2"])
 def test_server_key_fourier_ingestion_bit_exact_vs_oracle(orc, keys_2_2, keys_mb, which):
     """The oracle's Fourier BSK, serialized in natural DFT order (position P -> frequency
     pos_freq(P)), ingested through tfhe_mi355_server_key_upload: every bootstrap equals the
-    oracle's bit for bit, and the resident key equals the GPU's own conversion of the standard key."""
+    oracle's bit for bit, and the resident key equals the GPU's own conversion of the standard key.
+    1_1 (N = 512, k = 3), 1_0 (N = 256, k = 5) and 1_2 (N = 1024, k = 2) cover the small-N
+    layouts of WaveFft<256> / <128> / <512>."""
+    from conftest import KeySet
     from tfhe_mi355 import Engine, fill_accumulator, serialization, shortint
+    from tfhe_mi355 import parameters as PS
 
-    k = keys_2_2 if which == "2_2" else keys_mb
+    small = {"1_1": (PS.PARAM_MESSAGE_1_CARRY_1_KS_PBS, 31), "1_0": (PS.PARAM_MESSAGE_1_CARRY_0_KS_PBS, 32),
+             "1_2": (PS.PARAM_MESSAGE_1_CARRY_2_KS_PBS, 33)}
+    if which in small:
+        k = KeySet(orc, small[which][0], seed=small[which][1])
+    else:
+        k = keys_2_2 if which == "2_2" else keys_mb
     P = k.params
+    p = P.message_modulus * P.carry_modulus
     M = P.polynomial_size // 2
     four = k.fbsk.fourier().reshape(-1, M)                  # position order, reference scale
     natural = np.empty_like(four)
@@ -104,9 +114,10 @@ def test_server_key_fourier_ingestion_bit_exact_vs_oracle(orc, keys_2_2, keys_mb
     assert np.array_equal(_device_words(*sks.engine.fourier_bootstrap_key()), _device_words(*ref.fourier_bootstrap_key()))
 
     rng = np.random.default_rng(3)
-    msgs = rng.integers(0, 16, 24).astype(np.uint64)
+    msgs = rng.integers(0, p, 24).astype(np.uint64)
     cts = orc.lwe_encrypt(9, k.lwe_sk, msgs * np.uint64(P.delta), P.lwe_modular_std_dev)
-    acc = orc.fill_accumulator(P.polynomial_size, 1, 4, 4, lambda x: (x * x) % 16)
+    acc = orc.fill_accumulator(P.polynomial_size, P.glwe_dimension, P.message_modulus, P.carry_modulus,
+                               lambda x: (x * x) % p)
     got = sks.engine.programmable_bootstrap(cts, acc)
     assert np.array_equal(got, k.fbsk.pbs(cts, acc, threads=16))
-    assert np.array_equal(decode(orc.lwe_decrypt(k.glwe_sk, got), P.delta) % 16, (msgs * msgs) % 16)
+    assert np.array_equal(decode(orc.lwe_decrypt(k.glwe_sk, got), P.delta) % p, (msgs * msgs) % p)

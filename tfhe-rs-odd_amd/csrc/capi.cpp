@@ -13,6 +13,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -133,6 +134,10 @@ struct TfheMi355Context {
     TfheMi355Parameters p{};
     int device = 0;
     std::mutex mu;
+    // Key material vs the coalescer's batches: every key upload holds it exclusively, every
+    // dispatcher batch shared, so a re-upload waits for the batches in flight and no batch starts
+    // on a half-written key (the large host-pointer calls are ordered with uploads by `mu`).
+    std::shared_mutex keys_mu;
     hipStream_t stream = nullptr;
     FftTables tables;
     DeviceBuffer fbsk, ksk, std_staging;
@@ -682,12 +687,14 @@ size_t env_size(const char *name, size_t dflt) {
     const long x = std::atol(e);
     return x >= 0 ? (size_t)x : dflt;
 }
-size_t coalesce_max_count() {
-    static const size_t v = env_size("TFHE_MI355_COALESCE_MAX_COUNT", 64);
-    return v;
-}
 size_t coalesce_batch() {
     static const size_t v = std::max<size_t>(env_size("TFHE_MI355_COALESCE_BATCH", 1024), 1);
+    return v;
+}
+// never above the batch size: a dispatcher always takes its queue's first request whole, and the
+// slot staging is sized for one batch
+size_t coalesce_max_count() {
+    static const size_t v = std::min(env_size("TFHE_MI355_COALESCE_MAX_COUNT", 64), coalesce_batch());
     return v;
 }
 // batch slots (dispatcher threads, up to 8): batches in flight at once, each on its own stream.
@@ -743,11 +750,13 @@ void run_coalesced_batch(TfheMi355Context *c, TfheMi355Context::Coalescer::Slot 
                          const std::vector<CoalescedReq *> &batch) {
     check(hipSetDevice(c->device), "hipSetDevice");
     const CoalescedOpDesc d = coalesced_op(c, op);
-    const size_t cap = coalesce_batch(), glwe = c->glwe_len();
     if (!sl.stream) check(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking), "hipStreamCreate(slot)");
     size_t total = 0;
     for (auto *r : batch) total += r->count;
-    // sized for a full batch once (no hipFree between batches: it would wait for the device)
+    // sized for a full batch once (no hipFree between batches: it would wait for the device); a
+    // batch is at most `cap` rows (coalesce_max_count() <= cap, submit counts <= cap), the max()
+    // keeps the copies below in bounds whatever the settings
+    const size_t cap = std::max(coalesce_batch(), total), glwe = c->glwe_len();
     sl.h_in.reserve(cap * d.in_words * 8);
     sl.h_out.reserve(cap * d.out_words * 8);
     sl.d_in.reserve(cap * d.in_words * 8);
@@ -867,6 +876,7 @@ void coalesce_dispatcher(TfheMi355Context *c, size_t q) {
         std::string err;
         const auto t0 = std::chrono::steady_clock::now();
         try {
+            std::shared_lock<std::shared_mutex> keys(c->keys_mu);  // no key upload mid-batch
             run_coalesced_batch(c, sl, op, batch);
         } catch (const std::exception &ex) {
             err = ex.what();
@@ -1061,9 +1071,12 @@ int tfhe_mi355_context_create(const TfheMi355Parameters *params, int device, Tfh
         if (p.pbs_base_log < 2 || p.pbs_base_log * p.pbs_level > max_bits)
             fail("pbs decomposition base_log*level must be in [2, %u] (got %u x %u)", max_bits, p.pbs_base_log,
                  p.pbs_level);
-        // the split CMUX keeps the lower levels' digits as int16 between passes
-        if (split && p.pbs_level > 1 && p.pbs_base_log > 16)
-            fail("pbs base_log %u > 16 with %u levels at N = %u", p.pbs_base_log, p.pbs_level, p.polynomial_size);
+        // the split CMUX keeps the lower levels' digits as int16 between passes: a signed digit lies
+        // in [-2^(beta-1), 2^(beta-1)], so beta <= 15 (beta = 16 would wrap +2^15 to -2^15); this
+        // also keeps the grouped N = 32768, L = 2 path's 32-bit decomposition at beta * L <= 30
+        if (split && p.pbs_level > 1 && p.pbs_base_log > 15)
+            fail("pbs base_log %u > 15 with %u levels at N = %u (digits are packed as int16)", p.pbs_base_log,
+                 p.pbs_level, p.polynomial_size);
         if (p.ks_level && (p.ks_base_log == 0 || p.ks_base_log * p.ks_level >= 64)) fail("invalid ks decomposition");
         if (p.lwe_dimension == 0) fail("lwe_dimension must be > 0");
         check(hipSetDevice(device), "hipSetDevice");
@@ -1090,6 +1103,36 @@ int tfhe_mi355_context_destroy(TfheMi355Context *ctx) {
     return guarded([&] {
         if (!ctx) return;
         (void)hipSetDevice(ctx->device);
+        // 1. The coalescer first: take every still-queued request out of the queues and stop the
+        //    dispatchers (a batch already running completes; its callers get their rows), join
+        //    them, then fail the taken requests with rc = 1 -- they never launch a kernel on the
+        //    tables and streams freed below (c_api/utils.rs:3-11 error convention).
+        std::vector<CoalescedReq *> orphans;
+        {
+            std::lock_guard<std::mutex> g(ctx->co.m);
+            ctx->co.stop = true;
+            for (int o = 0; o < CO_OPS; o++) {
+                orphans.insert(orphans.end(), ctx->co.queue[o].begin(), ctx->co.queue[o].end());
+                ctx->co.queue[o].clear();
+                ctx->co.queued[o] = 0;
+            }
+        }
+        ctx->co.cv.notify_all();
+        for (auto &t : ctx->co.workers) t.join();
+        ctx->co.workers.clear();
+        for (auto *x : orphans) {
+            std::lock_guard<std::mutex> g(x->m);
+            x->err = "the context was destroyed before this request ran (wait on every request first)";
+            x->done = true;
+            x->cv.notify_one();
+        }
+        for (auto &sl : ctx->co.slots)
+            if (sl.stream) {
+                (void)hipStreamSynchronize(sl.stream);
+                (void)hipStreamDestroy(sl.stream);
+                sl.stream = nullptr;
+            }
+        // 2. then the device work of the synchronous paths, the tables and the streams
         if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
         for (auto &L : ctx->lanes)
             if (L.stream) (void)hipStreamSynchronize(L.stream);
@@ -1102,18 +1145,10 @@ int tfhe_mi355_context_destroy(TfheMi355Context *ctx) {
             if (L.stream) (void)hipStreamDestroy(L.stream);
         }
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-        {  // the coalescer's dispatchers drain their queues and exit
-            std::lock_guard<std::mutex> g(ctx->co.m);
-            ctx->co.stop = true;
-        }
-        ctx->co.cv.notify_all();
-        for (auto &t : ctx->co.workers) t.join();
-        for (auto &sl : ctx->co.slots)
-            if (sl.stream) {
-                (void)hipStreamSynchronize(sl.stream);
-                (void)hipStreamDestroy(sl.stream);
-            }
         delete ctx;  // device and pinned buffers free themselves
+        if (!orphans.empty())
+            fail("context destroyed with %zu request(s) still queued: they were not run and their wait returns 1",
+                 orphans.size());
     });
 }
 
@@ -1121,6 +1156,7 @@ int tfhe_mi355_bootstrap_key_upload(TfheMi355Context *ctx, const uint64_t *bsk, 
     return guarded([&] {
         if (!ctx || !bsk) fail("null argument");
         std::lock_guard<std::mutex> g(ctx->mu);
+        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
         check(hipSetDevice(ctx->device), "hipSetDevice");
         if (len != ctx->std_bsk_len()) fail("bootstrapping key has %zu words, expected %zu", len, ctx->std_bsk_len());
         ctx->std_staging.reserve(len * sizeof(uint64_t));
@@ -1151,6 +1187,7 @@ int tfhe_mi355_bootstrap_key_upload_seeded(TfheMi355Context *ctx, const uint64_t
     return guarded([&] {
         if (!ctx || !bodies) fail("null argument");
         std::lock_guard<std::mutex> g(ctx->mu);
+        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
         check(hipSetDevice(ctx->device), "hipSetDevice");
         const size_t rows = ctx->ggsw_count() * ctx->p.pbs_level * (ctx->k() + 1);
         if (len != rows * ctx->N()) fail("seeded bootstrapping key has %zu body words, expected %zu", len, rows * ctx->N());
@@ -1180,6 +1217,7 @@ int tfhe_mi355_keyswitch_key_upload_seeded(TfheMi355Context *ctx, const uint64_t
     return guarded([&] {
         if (!ctx || !bodies) fail("null argument");
         std::lock_guard<std::mutex> g(ctx->mu);
+        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
         check(hipSetDevice(ctx->device), "hipSetDevice");
         const size_t rows = ctx->big_dim() * ctx->p.ks_level;
         if (len != rows) fail("seeded keyswitching key has %zu body words, expected %zu", len, rows);
@@ -1227,6 +1265,7 @@ int tfhe_mi355_bootstrap_key_convert_async(TfheMi355Context *ctx, const uint64_t
     return guarded([&] {
         if (!ctx || !d_bsk) fail("null argument");
         std::lock_guard<std::mutex> g(ctx->mu);
+        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
         check(hipSetDevice(ctx->device), "hipSetDevice");
         if (len != ctx->std_bsk_len()) fail("bootstrapping key has %zu words, expected %zu", len, ctx->std_bsk_len());
         ctx->fbsk_ready = false;
@@ -1252,6 +1291,7 @@ int tfhe_mi355_bootstrap_key_fourier(TfheMi355Context *ctx, void **d_ptr, size_t
         *d_ptr = nullptr;
         *bytes = 0;
         std::lock_guard<std::mutex> g(ctx->mu);
+        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
         check(hipSetDevice(ctx->device), "hipSetDevice");
         ctx->fbsk.reserve(ctx->fourier_bsk_bytes());
         *d_ptr = ctx->fbsk.ptr;
@@ -1263,6 +1303,7 @@ int tfhe_mi355_bootstrap_key_fourier_set_ready(TfheMi355Context *ctx) {
     return guarded([&] {
         if (!ctx) fail("null ctx");
         std::lock_guard<std::mutex> g(ctx->mu);
+        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
         if (!ctx->fbsk.ptr) fail("no Fourier key buffer");
         ctx->fbsk_ready = true;
     });
@@ -1272,6 +1313,7 @@ int tfhe_mi355_keyswitch_key_upload(TfheMi355Context *ctx, const uint64_t *ksk, 
     return guarded([&] {
         if (!ctx || !ksk) fail("null argument");
         std::lock_guard<std::mutex> g(ctx->mu);
+        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
         check(hipSetDevice(ctx->device), "hipSetDevice");
         if (len != ctx->ksk_len()) fail("keyswitching key has %zu words, expected %zu", len, ctx->ksk_len());
         ctx->ksk.reserve(len * sizeof(uint64_t));
@@ -1287,6 +1329,7 @@ int tfhe_mi355_keyswitch_key_upload_async(TfheMi355Context *ctx, const uint64_t 
     return guarded([&] {
         if (!ctx || !d_ksk) fail("null argument");
         std::lock_guard<std::mutex> g(ctx->mu);
+        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
         check(hipSetDevice(ctx->device), "hipSetDevice");
         if (len != ctx->ksk_len()) fail("keyswitching key has %zu words, expected %zu", len, ctx->ksk_len());
         ctx->ksk.reserve(len * sizeof(uint64_t));
@@ -1305,6 +1348,7 @@ int tfhe_mi355_keyswitch_key_device(TfheMi355Context *ctx, void **d_ptr, size_t 
         *d_ptr = nullptr;
         *bytes = 0;
         std::lock_guard<std::mutex> g(ctx->mu);
+        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
         check(hipSetDevice(ctx->device), "hipSetDevice");
         ctx->ksk.reserve(ctx->ksk_len() * sizeof(uint64_t));
         *d_ptr = ctx->ksk.ptr;
@@ -1316,6 +1360,7 @@ int tfhe_mi355_keyswitch_key_set_ready(TfheMi355Context *ctx) {
     return guarded([&] {
         if (!ctx) fail("null ctx");
         std::lock_guard<std::mutex> g(ctx->mu);
+        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
         if (!ctx->ksk.ptr) fail("no keyswitching key buffer");
         check(hipSetDevice(ctx->device), "hipSetDevice");
         repack_ksk(ctx, ctx->stream);
@@ -1356,6 +1401,10 @@ int tfhe_mi355_programmable_bootstrap_async(TfheMi355Context *ctx, const uint64_
     return guarded([&] {
         if (!ctx || (!d_in && count) || (!d_out && count) || !d_luts) fail("null argument");
         check(hipSetDevice(ctx->device), "hipSetDevice");
+        // the scratch query is the contract: the persistent grid's ticket word at the classic
+        // shapes that use one (a NULL scratch there would silently run the slower one-pass grid);
+        // at N >= 4096 at least one ciphertext's worth (smaller passes below the query's size)
+        if (count && !is_large(ctx)) require_scratch(d_scratch ? scratch_bytes : 0, pbs_scratch_bytes(ctx, count));
         launch_pbs_dev(ctx, d_in, d_out, d_luts, lut_count, d_idx, count, d_scratch, scratch_bytes,
                        (hipStream_t)stream);
     });

@@ -48,6 +48,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <initializer_list>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -361,15 +362,41 @@ int tfhe_mi355_fourier_engine_frequency(uint32_t N, uint32_t *freq) {
             const uint32_t lane = e & 63, s = e >> 6;
             return (lane & 15) + 64 * (lane >> 4) + 16 * (s >> 2) + 256 * (s & 3);
         };
+        // DIF output position P = sum_i c_i M / (R_0 ... R_i) holds frequency sum_i c_i R_0 ... R_{i-1}
+        // (the plan's digit reversal, oracle pos_freq)
+        auto digit_reverse = [](uint32_t M, std::initializer_list<uint32_t> plan, uint32_t P) {
+            uint32_t f = 0, stride = M, weight = 1;
+            for (uint32_t R : plan) {
+                stride /= R;
+                f += (P / stride % R) * weight;
+                weight *= R;
+            }
+            return f;
+        };
         if (N == 2048) {
             for (uint32_t e = 0; e < 1024; e++) freq[e] = f1024(e);
+        } else if (N == 1024) {
+            // WaveFft<512>, plan [8, 8, 8]: element s*64 + lane holds P = 64 (lane & 7) + 8 (lane >> 3) + s
+            for (uint32_t e = 0; e < 512; e++) {
+                const uint32_t lane = e & 63, s = e >> 6;
+                freq[e] = digit_reverse(512, {8, 8, 8}, 64 * (lane & 7) + 8 * (lane >> 3) + s);
+            }
+        } else if (N == 512) {
+            // WaveFft<256>, plan [16, 16]: element q*64 + lane holds P = 16 (lane & 15) + (lane >> 4) + 4 q
+            for (uint32_t e = 0; e < 256; e++) {
+                const uint32_t lane = e & 63, q = e >> 6;
+                freq[e] = digit_reverse(256, {16, 16}, 16 * (lane & 15) + (lane >> 4) + 4 * q);
+            }
+        } else if (N == 256) {
+            // WaveFft<128>, plan [16, 8]: element e holds P = e (natural = Fourier layout)
+            for (uint32_t e = 0; e < 128; e++) freq[e] = digit_reverse(128, {16, 8}, e);
         } else if (N == 4096 || N == 8192 || N == 16384 || N == 32768) {
             // element ((q 16 + s) 64 + lane): sub-block q (top DIF radix-R output digit, R = N/2048)
             // of the [R | 16, 16, 4] plan, then the 1024-point layout inside it
             const uint32_t R = N / 2048;
             for (uint32_t e = 0; e < N / 2; e++) freq[e] = (e >> 10) + R * f1024(e & 1023);
         } else {
-            fail("Fourier key ingestion supports N = 2048 ... 32768 (got %u)", N);
+            fail("Fourier key ingestion supports N = 256 ... 32768 (got %u)", N);
         }
     });
 }

@@ -437,3 +437,14 @@ class Request:
         h, self._h = self._h, None
         _lib.call("tfhe_mi355_wait", h)
         return self._bufs[3]
+
+    def __del__(self):
+        # Dropped without wait() (e.g. an exception between a loop of submits and the waits): the
+        # dispatcher may still copy from / into the numpy buffers this object keeps alive, so block
+        # until the request is done (this also frees its native handle); errors are ignored here.
+        h, self._h = getattr(self, "_h", None), None
+        if h is not None:
+            try:
+                _lib.load().tfhe_mi355_wait(h)
+            except Exception:  # interpreter shutdown
+                pass
