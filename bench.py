@@ -920,6 +920,35 @@ def host_abi_rate(eng, P, cts, acc, with_ks: bool, reps: int = 3) -> dict:
                      "directly, same outputs); PCIe-inclusive, rank 0's GPU, not the headline value")}
 
 
+# the reference's published single-thread KS+PBS latencies (tfhe/docs/getting_started/benchmarks.md:42)
+REFERENCE_KS_PBS_MS = {"PARAM_MESSAGE_2_CARRY_2_KS_PBS": 16.6, "PARAM_MESSAGE_3_CARRY_3_KS_PBS": 121.0,
+                       "PARAM_MESSAGE_4_CARRY_4_KS_PBS": 811.0}
+
+
+def single_call_latency(eng, pname, cts, acc, with_ks: bool, secs: float = 1.5, max_reps: int = 50) -> dict:
+    """Wall time of ONE synchronous count = 1 call through the host-pointer ABI, the reference's
+    calling pattern (keyswitch_programmable_bootstrap_assign bootstraps one ciphertext,
+    shortint/server_key/mod.rs:783-857), on an otherwise idle GPU: median over repeated calls,
+    PCIe copies included.  Beside the reference's published single-thread latency where one exists."""
+    f = eng.keyswitch_programmable_bootstrap if with_ks else eng.programmable_bootstrap
+    x = np.ascontiguousarray(cts[:1])
+    f(x, acc)
+    times = []
+    t_end = time.perf_counter() + secs
+    while len(times) < max_reps and (len(times) < 3 or time.perf_counter() < t_end):
+        t = time.perf_counter()
+        f(x, acc)
+        times.append(time.perf_counter() - t)
+    ref = REFERENCE_KS_PBS_MS.get(pname) if with_ks else None
+    return {"ms": 1e3 * float(np.median(times)), "min_ms": 1e3 * min(times), "calls": len(times),
+            "op": "KS+PBS" if with_ks else "PBS",
+            "entry_point": ("tfhe_mi355_keyswitch_programmable_bootstrap" if with_ks
+                            else "tfhe_mi355_programmable_bootstrap"),
+            "reference_single_thread_ms": ref,
+            "note": "one count = 1 synchronous host-pointer call at a time (median), PCIe-inclusive"
+                    + ("; reference: benchmarks.md:42, one Xeon thread" if ref else "")}
+
+
 def single_ct_rates(eng, cts, acc, with_ks: bool, batched_rate: float, secs: float = 2.0,
                     callers=(1, 16, 64, 256), submit_windows=((1, 256), (16, 64))) -> dict:
     """The reference's own calling pattern through the synchronous host-pointer ABI: ONE ciphertext
@@ -1045,6 +1074,7 @@ def run_pbs(args, P, pname, workload, kname, R):
     ok = int(np.count_nonzero(dec == msgs))
     agg = aggregate(R, nb * args.steps, wall, ok, nb, lo, hi)
 
+    latency = single_call_latency(eng, pname, cts, acc, with_ks) if R.rank == 0 else None
     host_abi = None
     if not args.no_host_abi and R.rank == 0 and P.polynomial_size <= 2048:
         host_abi = host_abi_rate(eng, P, cts, acc, with_ks)
@@ -1089,6 +1119,8 @@ def run_pbs(args, P, pname, workload, kname, R):
         }
         if host_abi:
             line["host_abi"] = host_abi
+        line["single_call_latency_ms"] = latency["ms"]
+        line["single_call_latency"] = latency
         if R.world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or cpu_share()
             line["cpu_baseline"] = cpu_baseline(P, bsk, cts, acc, threads, ksk)

@@ -1,0 +1,56 @@
+"""Device time of one async PBS launch at 2_2 for a range of batch sizes (HIP events on the launch
+stream), to place the latency/throughput kernel switch (TFHE_MI355_LATENCY_MAX, capi.cpp).
+Run it twice, with TFHE_MI355_LATENCY_MAX=0 (throughput kernel only) and =4096 (latency kernel
+for every count), and compare.  Prints one JSON line."""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tfhe-rs-odd_amd")]
+
+
+def main():
+    import torch
+
+    from tfhe_mi355 import Engine, client, fill_accumulator
+    from tfhe_mi355.parameters import PARAM_MESSAGE_2_CARRY_2_KS_PBS as P
+
+    counts = [int(c) for c in (sys.argv[1] if len(sys.argv) > 1 else "1,16,64,128,256,384,512,768,1024").split(",")]
+    lwe_sk = client.gen_binary_key(3, 1, P.lwe_dimension)
+    glwe_sk = client.gen_binary_key(3, 2, P.big_lwe_dimension)
+    bsk = client.gen_bootstrap_key(4, lwe_sk, glwe_sk, 1, P.polynomial_size, P.pbs_base_log, P.pbs_level,
+                                   P.glwe_modular_std_dev)
+    eng = Engine(P, 0)
+    eng.upload_bootstrap_key(bsk)
+    C = max(counts)
+    msgs = np.arange(C, dtype=np.uint64) % 16
+    cts = client.lwe_encrypt(5, lwe_sk, msgs * np.uint64(P.delta), P.lwe_modular_std_dev)
+    acc = fill_accumulator(P, lambda x: x)
+    d_in = torch.from_numpy(cts.view(np.int64)).cuda()
+    d_out = torch.zeros((C, P.big_lwe_dimension + 1), dtype=torch.int64, device="cuda")
+    d_lut = torch.from_numpy(acc.view(np.int64)).cuda()
+    scratch = torch.empty(max(eng.pbs_scratch_bytes(C), 1), dtype=torch.uint8, device="cuda")
+    res = {"latency_max_env": os.environ.get("TFHE_MI355_LATENCY_MAX"), "ms": {}}
+    for c in counts:
+        eng.programmable_bootstrap_async(d_in, d_out, d_lut, 1, c, d_scratch=scratch)
+        torch.cuda.synchronize()
+        reps = 3 if c > 256 else 5
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for s, e in evs:
+            s.record()
+            eng.programmable_bootstrap_async(d_in, d_out, d_lut, 1, c, d_scratch=scratch)
+            e.record()
+        torch.cuda.synchronize()
+        ms = float(np.median([s.elapsed_time(e) for s, e in evs]))
+        out = d_out[:c].cpu().numpy().view(np.uint64)
+        dec = client.decode(client.lwe_decrypt(glwe_sk, out), P.delta) % np.uint64(16)
+        res["ms"][c] = {"ms": ms, "pbs_per_s": c / ms * 1e3, "decrypt_ok": int(np.count_nonzero(dec == msgs[:c]))}
+        print(c, res["ms"][c], file=sys.stderr, flush=True)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -294,6 +294,16 @@ size_t pbs_scratch_bytes(const TfheMi355Context *c, size_t count) {
     return per_ct * std::min(count, large_chunk(c));
 }
 
+// Batches of at most this many ciphertexts run the latency kernel at the shapes it supports
+// (TFHE_MI355_LATENCY_MAX; 0 = never).
+size_t latency_max() {
+    static const size_t v = [] {
+        const char *e = std::getenv("TFHE_MI355_LATENCY_MAX");
+        return e && *e ? (size_t)std::max(0L, std::atol(e)) : (size_t)256;
+    }();
+    return v;
+}
+
 bool ks_use_mfma(const TfheMi355Context *c) {
     static const bool disabled = env_flag("TFHE_MI355_KS_NO_MFMA");
     return !disabled && ks_mfma_supported((int)c->big_dim(), (int)c->p.ks_level, (int)c->p.ks_base_log);
@@ -399,6 +409,12 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
     a.base_log = (int)c->p.pbs_base_log;
     a.count = (int)count;
     a.glwe_out = glwe_out;
+    // small batches: the latency kernel (one ciphertext per CU, all 8 waves on it; same outputs)
+    if (count <= latency_max() && latency_pbs_supported((int)c->N(), (int)c->k(), (int)c->p.pbs_level)) {
+        TimedLaunch tl(c->timer_or_null(), "pbs_latency_kernel", s);
+        check(launch_latency_pbs(a, s), "launch latency pbs");
+        return;
+    }
     // persistent grid: a zeroed ticket word from the caller's scratch (none given: one pass)
     if (classic_pbs_ticket_bytes((int)c->N(), (int)c->k(), (int)c->p.pbs_level) && scratch && scratch_bytes >= 4) {
         a.ticket = reinterpret_cast<uint32_t *>(scratch);

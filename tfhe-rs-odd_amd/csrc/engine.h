@@ -130,6 +130,10 @@ bool classic_pbs_supported(int N, int k, int L);
 // device scratch (zeroed by the caller before each launch) for the persistent grid's ticket
 size_t classic_pbs_ticket_bytes(int N, int k, int L);
 hipError_t launch_classic_pbs(int N, int k, int L, const ClassicPbsLaunch &a, hipStream_t s);
+// latency form (pbs_latency.hip): one ciphertext per workgroup of 8 waves, same outputs; for small
+// batches (the one-ciphertext-per-call pattern).  N = 2048, k = 1, L = 1 only; no ticket, no scratch.
+bool latency_pbs_supported(int N, int k, int L);
+hipError_t launch_latency_pbs(const ClassicPbsLaunch &a, hipStream_t s);
 
 struct MultiBitPbsLaunch {
     const uint64_t *lwe_in;      // [count][n+1]
