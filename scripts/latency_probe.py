@@ -32,7 +32,8 @@ def main():
     d_in = torch.from_numpy(cts.view(np.int64)).cuda()
     d_out = torch.zeros((C, P.big_lwe_dimension + 1), dtype=torch.int64, device="cuda")
     d_lut = torch.from_numpy(acc.view(np.int64)).cuda()
-    scratch = torch.empty(max(eng.pbs_scratch_bytes(C), 1), dtype=torch.uint8, device="cuda")
+    stamps = os.environ.get("LAT_STAMPS") == "1"   # a LAT_STAMPS=1 build (TFHE_MI355_LIB)
+    scratch = torch.zeros(max(eng.pbs_scratch_bytes(C), 1 << 16), dtype=torch.uint8, device="cuda")
     res = {"latency_max_env": os.environ.get("TFHE_MI355_LATENCY_MAX"), "ms": {}}
     for c in counts:
         eng.programmable_bootstrap_async(d_in, d_out, d_lut, 1, c, d_scratch=scratch)
@@ -48,6 +49,12 @@ def main():
         out = d_out[:c].cpu().numpy().view(np.uint64)
         dec = client.decode(client.lwe_decrypt(glwe_sk, out), P.delta) % np.uint64(16)
         res["ms"][c] = {"ms": ms, "pbs_per_s": c / ms * 1e3, "decrypt_ok": int(np.count_nonzero(dec == msgs[:c]))}
+        if stamps and c <= 256:
+            st = scratch[: 2 * 8 * 12 * 8].cpu().numpy().view(np.uint64).reshape(2, 8, 12).astype(np.int64)
+            d = np.diff(st[:, :, :11], axis=2)            # per phase, cycles
+            res["ms"][c]["phase_cycles_row0"] = np.median(d[0], axis=0).tolist()
+            res["ms"][c]["phase_cycles_row1"] = np.median(d[1], axis=0).tolist()
+            res["ms"][c]["cmux_cycles"] = float(np.median(st[0, 1:, 0] - st[0, :-1, 0]))
         print(c, res["ms"][c], file=sys.stderr, flush=True)
     print(json.dumps(res), flush=True)
 

@@ -411,6 +411,9 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
     a.glwe_out = glwe_out;
     // small batches: the latency kernel (one ciphertext per CU, all 8 waves on it; same outputs)
     if (count <= latency_max() && latency_pbs_supported((int)c->N(), (int)c->k(), (int)c->p.pbs_level)) {
+#if LAT_STAMPS
+        a.ticket = reinterpret_cast<uint32_t *>(scratch);  // diagnostic builds: the stamp buffer
+#endif
         TimedLaunch tl(c->timer_or_null(), "pbs_latency_kernel", s);
         check(launch_latency_pbs(a, s), "launch latency pbs");
         return;

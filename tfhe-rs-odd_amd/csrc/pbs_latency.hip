@@ -37,14 +37,11 @@ namespace tfhe_mi355 {
 namespace {
 
 constexpr int LAT_N = 2048, LAT_M = 1024;
-// LDS layout in double2 units: stage-1 twiddles W[a C] as [C][a] (C, a < 16 x 64), stage-2
-// twiddles W[16 a1 C2] as [C2][a1], the twist, per GLWE row an exchange buffer X (stages 1/2) and
-// a buffer Y (stage-2 outputs, and the accumulator pairs of the rotation).
+// LDS layout in double2 units: per GLWE row an exchange buffer X (stages 1/2) and a buffer Y
+// (stage-2 outputs, and the accumulator pairs of the rotation).  The twiddles and the twist a lane
+// needs are 12 constants per lane, kept in registers (read once from the global tables).
 struct LatLds {
-    static constexpr int twf = 0;
-    static constexpr int tw2 = twf + 16 * 64;
-    static constexpr int twist = tw2 + 16 * 4;
-    static constexpr int X = twist + LAT_M;
+    static constexpr int X = 0;
     static constexpr int Y = X + 2 * LAT_M;
     static constexpr int end = Y + 2 * LAT_M;
     static constexpr size_t bytes = sizeof(double2) * end;
@@ -56,23 +53,100 @@ __device__ __forceinline__ cx ld2(const double2 *p) {
     return {t.x, t.y};
 }
 __device__ __forceinline__ void st2(double2 *p, cx v) { *p = make_double2(v.re, v.im); }
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations (lgkmcnt), not
+// for its global loads, so the GGSW prefetch stays in flight across it (__syncthreads' fence
+// would wait for vmcnt(0) too and expose the prefetch's latency at the first barrier).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 }  // namespace
 
-__global__ void __launch_bounds__(512, 2) pbs_latency_kernel(ClassicPbsLaunch a) {
+#ifndef LAT_BF
+#define LAT_BF 1  // branch-free row twiddles (per-lane constants + selects) instead of row branches
+#endif
+
+// Row-split 16-point DFTs of dft16_fwd_rows / dft16_inv_rows (fft_device.h) with the internal
+// twiddles omega16^(A k) (A = the lane's row, k = 1, 2, 3) computed without lane-divergent
+// branches: every exponent E = A k is either a cmulw with a constant (E = 0: (1, 0), E = 4:
+// (0, -1), value-identical to skipping / swapping; E = 1, 3, 9: the tw16 constants) or one of the
+// two sqrt(1/2) forms (E = 2, 6); each lane computes both candidate forms and selects its own.
+// Operation for operation the same as tw16_fwd<E> / tw16_inv<E> for the selected E.
+struct RowTw {
+    double cr[3], ci[3];  // cmulw constants of k = 1, 2, 3 (forward; the inverse conjugates)
+    bool sp[3], e6[3];    // sqrt(1/2) form (E = 2 or 6) and which one
+    __device__ explicit RowTw(int A) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const int E = A * (k + 1);
+            sp[k] = E == 2 || E == 6;
+            e6[k] = E == 6;
+            cr[k] = E == 0 ? 1.0 : E == 1 ? TM_C16_1 : E == 3 ? TM_S16_1 : E == 4 ? 0.0 : E == 9 ? -TM_C16_1 : 0.0;
+            ci[k] = E == 0 ? 0.0 : E == 1 ? -TM_S16_1 : E == 3 ? -TM_C16_1 : E == 4 ? -1.0 : E == 9 ? TM_S16_1 : 0.0;
+        }
+    }
+    template <bool INV>
+    __device__ __forceinline__ cx apply(int k, cx x) const {
+        const cx c = cmulw(x, cr[k], INV ? -ci[k] : ci[k]);
+        // forward E = 2: ((r + i) h, (i - r) h), E = 6: ((i - r) h, -((r + i) h));
+        // inverse E = 2: ((r - i) h, (r + i) h), E = 6: (-((r + i) h), (r - i) h)
+        const double sh = (x.re + x.im) * TM_SQH;
+        const double dh = (INV ? x.re - x.im : x.im - x.re) * TM_SQH;
+        cx sq;
+        if (INV) sq = e6[k] ? cx{-sh, dh} : cx{dh, sh};
+        else sq = e6[k] ? cx{dh, -sh} : cx{sh, dh};
+        return sp[k] ? sq : c;
+    }
+};
+__device__ __forceinline__ void dft16_fwd_rows_bf(cx *v, const RowTw &t) {
+    r4_fwd(v[0], v[1], v[2], v[3]);
+    v[1] = t.apply<false>(0, v[1]);
+    v[2] = t.apply<false>(1, v[2]);
+    v[3] = t.apply<false>(2, v[3]);
+    transpose_rows4(v[0], v[1], v[2], v[3]);
+    r4_fwd(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void dft16_inv_rows_bf(cx *v, const RowTw &t) {
+    r4_inv(v[0], v[1], v[2], v[3]);
+    transpose_rows4(v[0], v[1], v[2], v[3]);
+    v[1] = t.apply<true>(0, v[1]);
+    v[2] = t.apply<true>(1, v[2]);
+    v[3] = t.apply<true>(2, v[3]);
+    r4_inv(v[0], v[1], v[2], v[3]);
+}
+
+#ifndef LAT_STAMPS
+#define LAT_STAMPS 0  // diagnostic builds: s_memtime per CMUX phase of block 0 into the ticket buffer
+#endif
+
+// RPW = GLWE rows per wave: 1 -> 8 waves (wave (row, w), 2 per SIMD); 2 -> 4 waves, each doing
+// quarter w of both rows (twice the independent work per lane, one wave per SIMD; the stage-2 ->
+// MAC hand-off is then wave-private, so one workgroup barrier fewer per CMUX).
+template <int RPW>
+__global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(ClassicPbsLaunch a) {
     constexpr int N = LAT_N, M = LAT_M, K = 1, LOG2N = 11;
+    static_assert(RPW == 1 || RPW == 2, "one or both GLWE rows per wave");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double2 *lds = reinterpret_cast<double2 *>(smem);
     const int tid = threadIdx.x;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int row = wid >> 2;     // GLWE polynomial this wave transforms (and MAC output column)
-    const int w = wid & 3;        // quarter of that polynomial's transform
+    const int row0 = (wid >> 2) * RPW;  // first GLWE row this wave transforms (rows row0 .. row0 + RPW - 1)
+    const int w = wid & 3;              // quarter of the rows' transforms
     const int lane0 = tid & 63;
 
-    // tables: W[a C] (C = 0 row = W[0] = (1, -0): value-identical to the oracle's skipped multiply)
-    for (int e = tid; e < 16 * 64; e += 512) lds[LatLds::twf + e] = a.W[(e & 63) * (e >> 6)];
-    if (tid < 64) lds[LatLds::tw2 + tid] = a.W[16 * (tid & 3) * (tid >> 2)];
-    for (int e = tid; e < M; e += 512) lds[LatLds::twist + e] = a.twist[e];
+    // per-lane constants: stage-1 twiddles W[a1 C] (a1 = 16 w + col, C = lrow + 4 q; C = 0 gives
+    // W[0] = (1, -0): value-identical to the oracle's skipped multiply), stage-2 twiddles
+    // W[16 a2 C2] (a2 = col & 3), the twist of the lane's positions j_q = a1 + 64 (lrow + 4 q)
+    cx tw1[4], tw2[4], tws[4];
+    const RowTw rtw(lane0 >> 4);
+    {
+        const int lrow = lane0 >> 4, col = lane0 & 15, a1 = 16 * w + col, a2 = col & 3;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int C = lrow + 4 * q;
+            tw1[q] = ld2(a.W + a1 * C);
+            tw2[q] = ld2(a.W + 16 * a2 * C);
+            tws[q] = ld2(a.twist + a1 + 64 * C);
+        }
+    }
 
     const int ct = blockIdx.x;
     const int n = a.n;
@@ -81,211 +155,279 @@ __global__ void __launch_bounds__(512, 2) pbs_latency_kernel(ClassicPbsLaunch a)
         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)in >> 32)) << 32) |
         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)in));
     const uint32_t li = a.lut_indexes ? min(a.lut_indexes[ct], a.lut_count - 1u) : 0u;
-    const uint64_t *lut = a.luts + (size_t)li * (K + 1) * N + (size_t)row * N;
     const DigitL1 digit_l1(a.base_log);
 
-    // this lane's accumulator coefficients: j_q = a1 + 64 (lrow + 4 q) (a1 = 16 w + col) and j_q + M
-    // (the stage-1 input positions and the backward conversion's output positions)
-    uint64_t lo[4], hi[4];
+    // this lane's accumulator coefficients of row row0 + r: j_q = a1 + 64 (lrow + 4 q) (a1 = 16 w +
+    // col) and j_q + M (the stage-1 input positions and the backward conversion's output positions)
+    uint64_t lo[RPW][4], hi[RPW][4];
     {
         const uint32_t bt = pbs_modulus_switch<LOG2N>(in[n]);
         const int full = bt / N, rem = bt % N;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int j = 16 * w + (lane0 & 15) + 64 * (lane0 >> 4) + 256 * q;
+        for (int r = 0; r < RPW; r++) {
+            const uint64_t *lut = a.luts + (size_t)li * (K + 1) * N + (size_t)(row0 + r) * N;
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int src = j + h * M + rem;
-                const bool wrap = src >= N;
-                const uint64_t v = lut[wrap ? src - N : src];
-                const uint64_t c = (wrap != (bool)(full & 1)) ? 0 - v : v;
-                (h ? hi : lo)[q] = c;
+            for (int q = 0; q < 4; q++) {
+                const int j = 16 * w + (lane0 & 15) + 64 * (lane0 >> 4) + 256 * q;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int src = j + h * M + rem;
+                    const bool wrap = src >= N;
+                    const uint64_t v = lut[wrap ? src - N : src];
+                    const uint64_t c = (wrap != (bool)(full & 1)) ? 0 - v : v;
+                    (h ? hi : lo)[r][q] = c;
+                }
             }
         }
     }
-    __syncthreads();  // tables
-
-    const double2 *twf = lds + LatLds::twf;
-    const double2 *tw2 = lds + LatLds::tw2;
-    const double2 *s_twist = lds + LatLds::twist;
-    double2 *X = lds + LatLds::X + row * M;
-    double2 *Y = lds + LatLds::Y + row * M;
-    // accumulator pairs (acc[p], acc[p + M]) in Y between CMUXes (Y's stage-2 outputs are dead then)
-    uint64_t *A64 = reinterpret_cast<uint64_t *>(Y);
+    // per row: X = exchange buffer of stages 1 / 2, Y = stage-2 outputs; the accumulator pairs
+    // (acc[p], acc[p + M]) live in Y between CMUXes (its stage-2 outputs are dead then)
+    auto Xr = [&](int r) { return lds + LatLds::X + (row0 + r) * M; };
+    auto Yr = [&](int r) { return lds + LatLds::Y + (row0 + r) * M; };
+    auto Ar = [&](int r) { return reinterpret_cast<uint64_t *>(Yr(r)); };
     constexpr size_t ggsw_stride = (size_t)(K + 1) * (K + 1) * M;
     const double k32 = torus_k32();
 
+    // diagnostic stamps (LAT_STAMPS builds only; written to a buffer nothing else reads): wave 0 and
+    // (RPW = 1) wave 4 of workgroup 0, CMUX 200 .. 207, 12 stamps each
+    uint64_t *stamp_buf = LAT_STAMPS ? reinterpret_cast<uint64_t *>(a.ticket) : nullptr;
+    auto stamp = [&](int i, int k) {
+        if constexpr (LAT_STAMPS) {
+            if (blockIdx.x == 0 && (wid & 3) == 0 && lane0 == 0 && i >= 200 && i < 208) {
+                int vo = lane0;  // a VGPR offset (0 here): the stamp goes out through a vector store
+                asm volatile("" : "+v"(vo));
+                stamp_buf[((wid >> 2) * 8 + (i - 200)) * 12 + k + vo] = __builtin_amdgcn_s_memtime();
+            }
+        }
+    };
     for (int i = 0; i < n; i++) {
         int lane = lane0;  // opaque per-iteration copy: lane-derived addresses are not hoisted
         asm volatile("" : "+v"(lane));
+        stamp(i, 0);
         const int lrow = lane >> 4, col = lane & 15;
+        // this CMUX's GGSW operands of the MAC lane's block (see the MAC below) for each output
+        // column of this wave, loaded first so that their L2/MALL latency hides behind the rotation
+        // and the forward FFT
+        const int ccm = 4 * w + (col & 3), xm = col >> 2;
+        double2 gpre[RPW][K + 1][4];
+        {
+            // engine layout: element s*64 + L <-> position 64 (L & 15) + 16 (L >> 4) + s, so position
+            // 64 ccm + 4 (lrow + 4 xm) + e is element (4 lrow + e) 64 + 16 xm + ccm
+            const double2 *g = a.fbsk + (size_t)i * ggsw_stride + 256 * lrow + 16 * xm + ccm;
+#pragma unroll
+            for (int c = 0; c < RPW; c++)
+#pragma unroll
+                for (int rr = 0; rr <= K; rr++)
+#pragma unroll
+                    for (int e = 0; e < 4; e++)
+                        gpre[c][rr][e] = g[(size_t)(rr * (K + 1) + row0 + c) * M + 64 * e];
+        }
+        __builtin_amdgcn_sched_barrier(0);
         const uint32_t at = pbs_modulus_switch<LOG2N>(in_s[i]);
         const bool full_odd = (at / N) & 1;
         const int rem = at % N;
 
         // ---- accumulator -> LDS pairs, rotation gather, ct1 = X^at acc - acc, digits, twist ----
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int j = 16 * w + col + 64 * lrow + 256 * q;
-            A64[2 * j] = lo[q];
-            A64[2 * j + 1] = hi[q];
-        }
-        __syncthreads();  // (A) every wave's pairs written
-        cx v[4];
+        for (int r = 0; r < RPW; r++)
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int j = 16 * w + col + 64 * lrow + 256 * q;
-            // (X^rem p) at j and j + M from ONE pair: u = j - rem, s = u mod M; u >= 0: (lo, hi);
-            // -M <= u < 0: (-hi, lo) (X^M acts as i on the fold); u < -M: (-lo, -hi)
-            const int u = j - rem;
-            const int s = u & (M - 1);
-            const uint64_t plo = A64[2 * s], phi = A64[2 * s + 1];
-            const bool swap = u < 0 && u >= -M;
-            const bool n0 = (u < 0) != full_odd, n1 = (u < -M) != full_odd;
-            const uint64_t x0 = swap ? phi : plo, x1 = swap ? plo : phi;
-            const uint64_t r0 = n0 ? 0 - x0 : x0, r1 = n1 ? 0 - x1 : x1;
-            const int32_t d0 = digit_l1((uint32_t)((r0 - lo[q]) >> 32));
-            const int32_t d1 = digit_l1((uint32_t)((r1 - hi[q]) >> 32));
-            const double2 tw = s_twist[j];
-            v[q] = cmulw(cx{(double)d0, (double)d1}, tw.x, tw.y);  // convert_forward_integer (x86.rs:505-596)
-        }
+            for (int q = 0; q < 4; q++) {
+                const int j = 16 * w + col + 64 * lrow + 256 * q;
+                Ar(r)[2 * j] = lo[r][q];
+                Ar(r)[2 * j + 1] = hi[r][q];
+            }
+        lds_barrier();  // (A) every wave's pairs written
+        stamp(i, 1);
+        cx v[RPW][4];
+#pragma unroll
+        for (int r = 0; r < RPW; r++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int j = 16 * w + col + 64 * lrow + 256 * q;
+                // (X^rem p) at j and j + M from ONE pair: u = j - rem, s = u mod M; u >= 0: (lo, hi);
+                // -M <= u < 0: (-hi, lo) (X^M acts as i on the fold); u < -M: (-lo, -hi)
+                const int u = j - rem;
+                const int s = u & (M - 1);
+                const uint64_t plo = Ar(r)[2 * s], phi = Ar(r)[2 * s + 1];
+                const bool swap = u < 0 && u >= -M;
+                const bool n0 = (u < 0) != full_odd, n1 = (u < -M) != full_odd;
+                const uint64_t x0 = swap ? phi : plo, x1 = swap ? plo : phi;
+                const uint64_t r0 = n0 ? 0 - x0 : x0, r1 = n1 ? 0 - x1 : x1;
+                const int32_t d0 = digit_l1((uint32_t)((r0 - lo[r][q]) >> 32));
+                const int32_t d1 = digit_l1((uint32_t)((r1 - hi[r][q]) >> 32));
+                v[r][q] = cmulw(cx{(double)d0, (double)d1}, tws[q].re, tws[q].im);  // convert_forward_integer (x86.rs:505-596)
+            }
 
+        stamp(i, 2);
         // ---- forward stage 1: butterfly a1 = 16 w + col, column lrow ----
-        dft16_fwd_rows(v, lrow);
-        {
+#pragma unroll
+        for (int r = 0; r < RPW; r++) {
+            if (LAT_BF) dft16_fwd_rows_bf(v[r], rtw);
+            else dft16_fwd_rows(v[r], lrow);
             const int a1 = 16 * w + col;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const int C = lrow + 4 * q;
-                const double2 t = twf[C * 64 + a1];
-                st2(X + a1 + 64 * C, cmulw(v[q], t.x, t.y));
+                st2(Xr(r) + a1 + 64 * C, cmulw(v[r][q], tw1[q].re, tw1[q].im));
             }
         }
-        __syncthreads();  // (B)
+        stamp(i, 3);
+        lds_barrier();  // (B)
+        stamp(i, 4);
         // ---- forward stage 2: block cc = 4 w + (col >> 2), butterfly a2 = col & 3 ----
         {
             const int cc = 4 * w + (col >> 2), a2 = col & 3;
 #pragma unroll
-            for (int q = 0; q < 4; q++) v[q] = ld2(X + 64 * cc + a2 + 4 * (lrow + 4 * q));
-            dft16_fwd_rows(v, lrow);
+            for (int r = 0; r < RPW; r++) {
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int C2 = lrow + 4 * q;
-                const double2 t = tw2[C2 * 4 + a2];
-                st2(Y + 64 * cc + a2 + 4 * C2, cmulw(v[q], t.x, t.y));
-            }
-        }
-        __syncthreads();  // (C) both rows' stage-2 outputs
-        // ---- stage 3 of both rows + MAC of output column `row` on block t ----
-        const int ccm = 4 * w + (col & 3), xm = col >> 2;
-        const int tb = 64 * ccm + 4 * (lrow + 4 * xm);  // first position of block t
-        cx o[4];
-        {
-            // GGSW elements of positions tb + e in the engine layout (element s*64 + L <-> position
-            // 64 (L & 15) + 16 (L >> 4) + s): (4 lrow + e) 64 + 16 xm + ccm
-            const double2 *g = a.fbsk + (size_t)i * ggsw_stride + (size_t)row * M + 256 * lrow + 16 * xm + ccm;
+                for (int q = 0; q < 4; q++) v[r][q] = ld2(Xr(r) + 64 * cc + a2 + 4 * (lrow + 4 * q));
+                if (LAT_BF) dft16_fwd_rows_bf(v[r], rtw);
+                else dft16_fwd_rows(v[r], lrow);
 #pragma unroll
-            for (int rr = 0; rr <= K; rr++) {
-                const double2 *Yr = lds + LatLds::Y + rr * M + tb;
-                cx f0 = ld2(Yr), f1 = ld2(Yr + 1), f2 = ld2(Yr + 2), f3 = ld2(Yr + 3);
-                r4_fwd(f0, f1, f2, f3);
-                const cx f[4] = {f0, f1, f2, f3};
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    const double2 gg = g[(size_t)rr * (K + 1) * M + 64 * e];
-                    const double2 ff = make_double2(f[e].re, f[e].im);
-                    if (rr == 0) {  // update_with_fmadd (ggsw.rs:524-567), the throughput kernel's form
-                        o[e].re = fma(gg.x, ff.x, -(gg.y * ff.y));
-                        o[e].im = fma(gg.x, ff.y, gg.y * ff.x);
-                    } else {
-                        o[e].re = fma(gg.x, ff.x, fma(-gg.y, ff.y, o[e].re));
-                        o[e].im = fma(gg.x, ff.y, fma(gg.y, ff.x, o[e].im));
-                    }
+                for (int q = 0; q < 4; q++) {
+                    const int C2 = lrow + 4 * q;
+                    st2(Yr(r) + 64 * cc + a2 + 4 * C2, cmulw(v[r][q], tw2[q].re, tw2[q].im));
                 }
             }
         }
+        stamp(i, 5);
+        // (C) both rows' stage-2 outputs of this wave's blocks: written by the other row's wave
+        // (RPW = 1), or by this wave itself (RPW = 2: wave-private)
+        if constexpr (RPW == 1) lds_barrier();
+        else WaveLocalSync{}();
+        stamp(i, 6);
+        // ---- stage 3 of both rows + MAC of this wave's output columns on block t ----
+        const int tb = 64 * ccm + 4 * (lrow + 4 * xm);  // first position of block t
+        cx o[RPW][4];
+        {
+            cx f[K + 1][4];
+#pragma unroll
+            for (int rr = 0; rr <= K; rr++) {
+                const double2 *y = lds + LatLds::Y + rr * M + tb;
+                f[rr][0] = ld2(y);
+                f[rr][1] = ld2(y + 1);
+                f[rr][2] = ld2(y + 2);
+                f[rr][3] = ld2(y + 3);
+                r4_fwd(f[rr][0], f[rr][1], f[rr][2], f[rr][3]);
+            }
+#pragma unroll
+            for (int c = 0; c < RPW; c++)
+#pragma unroll
+                for (int rr = 0; rr <= K; rr++)
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        const double2 gg = gpre[c][rr][e];
+                        const double2 ff = make_double2(f[rr][e].re, f[rr][e].im);
+                        if (rr == 0) {  // update_with_fmadd (ggsw.rs:524-567), the throughput kernel's form
+                            o[c][e].re = fma(gg.x, ff.x, -(gg.y * ff.y));
+                            o[c][e].im = fma(gg.x, ff.y, gg.y * ff.x);
+                        } else {
+                            o[c][e].re = fma(gg.x, ff.x, fma(-gg.y, ff.y, o[c][e].re));
+                            o[c][e].im = fma(gg.x, ff.y, fma(gg.y, ff.x, o[c][e].im));
+                        }
+                    }
+        }
         // ---- inverse stage 3 (R4 on the block), back to the stage-2 lanes through this wave's
         //      own quarter of X (positions 256 w .. 256 w + 255: written and read by this wave only)
-        r4_inv(o[0], o[1], o[2], o[3]);
+        stamp(i, 7);
 #pragma unroll
-        for (int e = 0; e < 4; e++) st2(X + tb + e, o[e]);
+        for (int c = 0; c < RPW; c++) {
+            r4_inv(o[c][0], o[c][1], o[c][2], o[c][3]);
+#pragma unroll
+            for (int e = 0; e < 4; e++) st2(Xr(c) + tb + e, o[c][e]);
+        }
         WaveLocalSync{}();
         {
             const int cc = 4 * w + (col >> 2), a2 = col & 3;
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int C2 = lrow + 4 * q;
-                const double2 t = tw2[C2 * 4 + a2];
-                v[q] = cmulw(ld2(X + 64 * cc + a2 + 4 * C2), t.x, -t.y);
+            for (int r = 0; r < RPW; r++) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int C2 = lrow + 4 * q;
+                    v[r][q] = cmulw(ld2(Xr(r) + 64 * cc + a2 + 4 * C2), tw2[q].re, -tw2[q].im);
+                }
+                if (LAT_BF) dft16_inv_rows_bf(v[r], rtw);
+                else dft16_inv_rows(v[r], lrow);
             }
-            dft16_inv_rows(v, lrow);
             WaveLocalSync{}();
 #pragma unroll
-            for (int q = 0; q < 4; q++) st2(X + 64 * cc + a2 + 4 * (lrow + 4 * q), v[q]);
+            for (int r = 0; r < RPW; r++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) st2(Xr(r) + 64 * cc + a2 + 4 * (lrow + 4 * q), v[r][q]);
         }
-        __syncthreads();  // (D)
+        stamp(i, 8);
+        lds_barrier();  // (D)
+        stamp(i, 9);
         // ---- inverse stage 1 + backward conversion into the accumulator ----
         {
             const int a1 = 16 * w + col;
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int C = lrow + 4 * q;
-                const double2 t = twf[C * 64 + a1];
-                v[q] = cmulw(ld2(X + a1 + 64 * C), t.x, -t.y);
-            }
-            dft16_inv_rows(v, lrow);
+            for (int r = 0; r < RPW; r++) {
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int j = a1 + 64 * lrow + 256 * q;
-                const double2 tw = s_twist[j];  // the resident key carries the 1/M
-                backward_add(v[q], cx{tw.x, tw.y}, lo[q], hi[q], k32);
+                for (int q = 0; q < 4; q++) {
+                    const int C = lrow + 4 * q;
+                    v[r][q] = cmulw(ld2(Xr(r) + a1 + 64 * C), tw1[q].re, -tw1[q].im);
+                }
+                if (LAT_BF) dft16_inv_rows_bf(v[r], rtw);
+                else dft16_inv_rows(v[r], lrow);
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    backward_add(v[r][q], tws[q], lo[r][q], hi[r][q], k32);  // the resident key carries the 1/M
             }
         }
+        stamp(i, 10);
     }
 
     // ---- output ----
     const int lrow = lane0 >> 4, col = lane0 & 15;
     if (a.glwe_out) {  // bootstrap_without_sample_extract (fork, bootstrap.rs:383-412)
-        uint64_t *g = a.lwe_out + ((size_t)ct * (K + 1) + row) * N;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int j = 16 * w + col + 64 * lrow + 256 * q;
-            g[j] = lo[q];
-            g[j + M] = hi[q];
+        for (int r = 0; r < RPW; r++) {
+            uint64_t *g = a.lwe_out + ((size_t)ct * (K + 1) + row0 + r) * N;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int j = 16 * w + col + 64 * lrow + 256 * q;
+                g[j] = lo[r][q];
+                g[j + M] = hi[r][q];
+            }
         }
         return;
     }
-    // sample extract at degree 0 (glwe_sample_extraction.rs:91-147): mask j = -acc0[N - j] (j > 0)
+    // sample extract at degree 0 (glwe_sample_extraction.rs:91-147): mask j = -acc0[N - j] (j > 0),
+    // body = acc_k[0]
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int j = 16 * w + col + 64 * lrow + 256 * q;
-        A64[2 * j] = lo[q];
-        A64[2 * j + 1] = hi[q];
-    }
+    for (int r = 0; r < RPW; r++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int j = 16 * w + col + 64 * lrow + 256 * q;
+            Ar(r)[2 * j] = lo[r][q];
+            Ar(r)[2 * j + 1] = hi[r][q];
+        }
     __syncthreads();
     uint64_t *out = a.lwe_out + (size_t)ct * (K * N + 1);
-    if (row < K) {
-        const uint64_t *A0 = reinterpret_cast<const uint64_t *>(lds + LatLds::Y + row * M);
-        for (int j = tid & 255; j < N; j += 256) {
-            uint64_t x;
-            if (j == 0) {
-                x = A0[0];
-            } else {
-                const int src = N - j;  // acc0[src]: pair (src mod M), lo below M, hi above
-                x = 0 - A0[2 * (src & (M - 1)) + (src >= M)];
-            }
-            out[(size_t)row * N + j] = x;
+    const uint64_t *A0 = reinterpret_cast<const uint64_t *>(lds + LatLds::Y);  // row 0 (K = 1)
+    for (int j = tid; j < N; j += (int)blockDim.x) {
+        uint64_t x;
+        if (j == 0) {
+            x = A0[0];
+        } else {
+            const int src = N - j;  // acc0[src]: pair (src mod M), lo below M, hi above
+            x = 0 - A0[2 * (src & (M - 1)) + (src >= M)];
         }
-    } else if (tid == 256 * K) {
-        out[K * N] = lo[0];  // body = acc_k[0]: j = 0 lives in lane 0 of wave 0 of row k (q = 0)
+        out[j] = x;
     }
+    if (tid == 0) out[K * N] = reinterpret_cast<const uint64_t *>(lds + LatLds::Y + K * M)[0];
 }
 
 bool latency_pbs_supported(int N, int k, int L) { return N == 2048 && k == 1 && L == 1; }
 
+#ifndef LAT_RPW
+#define LAT_RPW 1  // GLWE rows per wave (1: 8 waves per ciphertext, 2: 4 waves)
+#endif
+
 hipError_t launch_latency_pbs(const ClassicPbsLaunch &a, hipStream_t s) {
     if (a.count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(pbs_latency_kernel, dim3(a.count), dim3(512), LatLds::bytes, s, a);
+    hipLaunchKernelGGL(pbs_latency_kernel<LAT_RPW>, dim3(a.count), dim3(512 / LAT_RPW), LatLds::bytes, s, a);
     return hipGetLastError();
 }
 
