@@ -127,3 +127,31 @@ def test_unsupported_multi_bit_parameters_are_rejected():
     with pytest.raises(EngineError, match="multiple of grouping_factor"):
         Engine(mb.with_(lwe_dimension=889), 0)
 
+
+
+@pytest.mark.parametrize("N,base_log,level,ok", [
+    (8192, 15, 2, True),     # PARAM_MESSAGE_3_CARRY_3 (split CMUX, int16 digit packing)
+    (8192, 16, 2, False),    # a digit of +2^15 would wrap in int16
+    (32768, 16, 2, False),   # grouped N = 32768 path: 32-bit decomposition needs beta * L <= 30
+    (32768, 11, 3, True),    # PARAM_MESSAGE_1_CARRY_7 (64-bit decomposition, 33 bits)
+    (4096, 22, 1, True),     # one level: no packing
+])
+def test_context_create_validates_split_decomposition(N, base_log, level, ok):
+    """tfhe_mi355_context_create checks the decomposition before touching the GPU (capi.cpp):
+    base_log > 15 with more than one level is rejected at N >= 4096."""
+    from tfhe_mi355 import _lib
+    from tfhe_mi355._lib import TfheMi355Parameters, vp
+
+    p = TfheMi355Parameters(800, 1, N, base_log, level, 3, 6, 4, 4, 0)
+    h = vp()
+    lib = _lib.load()
+    rc = lib.tfhe_mi355_context_create(ctypes.byref(p), 0, ctypes.byref(h))
+    msg = lib.tfhe_mi355_last_error().decode()
+    if ok:
+        # valid parameters get past validation: on a CPU box the first HIP call then fails
+        if rc == 0:
+            lib.tfhe_mi355_context_destroy(h)
+        else:
+            assert "decomposition" not in msg and "base_log" not in msg, msg
+    else:
+        assert rc == 1 and not h.value and "base_log" in msg, msg

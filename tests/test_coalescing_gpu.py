@@ -200,3 +200,48 @@ def test_submit_rejects_bad_requests(eng):
         eng.submit("pbs", np.zeros((2000, eng.n + 1), dtype=np.uint64), np.zeros(eng.glwe_len, dtype=np.uint64))
     with pytest.raises(KeyError):
         eng.submit("nope", np.zeros((1, eng.n + 1), dtype=np.uint64))
+
+
+_SMALL_BATCH_CHILD = r'''
+import sys, threading
+import numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[1] + "/tfhe-rs-odd_amd"]
+from tfhe_mi355 import Engine, client, fill_accumulator
+from tfhe_mi355.parameters import PARAM_MESSAGE_2_CARRY_2_KS_PBS as P0
+P = P0.with_(lwe_dimension=32)
+lsk = client.gen_binary_key(1, 1, P.lwe_dimension)
+gsk = client.gen_binary_key(1, 2, P.big_lwe_dimension)
+eng = Engine(P, 0)
+eng.upload_bootstrap_key(client.gen_bootstrap_key(2, lsk, gsk, 1, P.polynomial_size, P.pbs_base_log,
+                                                  P.pbs_level, P.glwe_modular_std_dev))
+acc = fill_accumulator(P, lambda x: (x + 1) % 16)
+msgs = np.arange(64, dtype=np.uint64) % 16
+cts = client.lwe_encrypt(3, lsk, msgs * np.uint64(P.delta), P.lwe_modular_std_dev)
+ref = eng.programmable_bootstrap(cts, acc)            # 64 rows: above the clamped max count
+outs = [None] * 8
+def call(i):
+    outs[i] = eng.programmable_bootstrap(cts[8 * i: 8 * i + 8], acc)   # coalesced, 8 per call
+ts = [threading.Thread(target=call, args=(i,)) for i in range(8)]
+[t.start() for t in ts]; [t.join() for t in ts]
+assert np.array_equal(np.concatenate(outs), ref), "coalesced rows differ"
+dec = client.decode(client.lwe_decrypt(gsk, ref), P.delta) % np.uint64(16)
+assert np.array_equal(dec, (msgs + 1) % 16), dec
+st = eng.coalesce_stats()
+assert st["rows"] == 64 and max(1, st["batches"]) >= 4, st   # batches of <= 16 rows
+print("OK", st)
+'''
+
+
+def test_coalesce_batch_smaller_than_max_count_is_safe():
+    """TFHE_MI355_COALESCE_BATCH (16) below TFHE_MI355_COALESCE_MAX_COUNT (64): the max count is
+    clamped to the batch, so a 64-row call takes the pipelined path instead of overflowing the
+    batch staging (ADVICE r03), and 8-row calls are coalesced into batches of at most 16 rows."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, TFHE_MI355_COALESCE_BATCH="16", TFHE_MI355_COALESCE_MAX_COUNT="64")
+    r = subprocess.run([sys.executable, "-c", _SMALL_BATCH_CHILD, root], capture_output=True, text=True,
+                       timeout=240, env=env)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr[-2000:]

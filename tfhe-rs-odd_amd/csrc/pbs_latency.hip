@@ -53,6 +53,17 @@ __device__ __forceinline__ cx ld2(const double2 *p) {
     return {t.x, t.y};
 }
 __device__ __forceinline__ void st2(double2 *p, cx v) { *p = make_double2(v.re, v.im); }
+// X / Y slot of FFT position P: an XOR swizzle of the 16-byte slot's bank bits (0-3) by bits 4, 6
+// and 7, found by exhaustive search over the linear swizzles of bits 4-7 to make all three access
+// patterns of a wave (stage-1 a1 + 64 C, stage-2 64 cc + a2 + 4 C2, the MAC's blocks 4 t + e) free
+// of bank conflicts for both ds_read_b128 lane groups and ds_write_b128's (the plain layout puts
+// up to 4 lanes of a group on one bank).  LAT_SWZ=0: plain.
+#ifndef LAT_SWZ
+#define LAT_SWZ 1
+#endif
+__device__ __forceinline__ int lswz(int P) {
+    return LAT_SWZ ? P ^ (((P >> 4) & 1) | ((P >> 6) & 2) | ((P >> 4) & 4) | ((P >> 3) & 8)) : P;
+}
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations (lgkmcnt), not
 // for its global loads, so the GGSW prefetch stays in flight across it (__syncthreads' fence
 // would wait for vmcnt(0) too and expose the prefetch's latency at the first barrier).
@@ -112,6 +123,13 @@ __device__ __forceinline__ void dft16_inv_rows_bf(cx *v, const RowTw &t) {
     v[3] = t.apply<true>(2, v[3]);
     r4_inv(v[0], v[1], v[2], v[3]);
 }
+
+#ifndef LAT_PRIO
+#define LAT_PRIO 0  // s_setprio for the second-dispatched half of the waves (the arbitration losers)
+#endif
+#ifndef LAT_PREF2
+#define LAT_PREF2 0  // GGSW of CMUX i + 1 loaded during CMUX i (two register sets) instead of at its top
+#endif
 
 #ifndef LAT_STAMPS
 #define LAT_STAMPS 0  // diagnostic builds: s_memtime per CMUX phase of block 0 into the ticket buffer
@@ -200,27 +218,41 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
             }
         }
     };
+    // GGSW operands of the MAC lane's block (see the MAC below) for each output column of this
+    // wave; engine layout: element s*64 + L <-> position 64 (L & 15) + 16 (L >> 4) + s, so position
+    // 64 ccm + 4 (lrow + 4 xm) + e is element (4 lrow + e) 64 + 16 xm + ccm
+    auto load_ggsw = [&](double2 (&gp)[RPW][K + 1][4], int ii, int lrow, int col) {
+        const int ccm = 4 * w + (col & 3), xm = col >> 2;
+        const double2 *g = a.fbsk + (size_t)ii * ggsw_stride + 256 * lrow + 16 * xm + ccm;
+#pragma unroll
+        for (int c = 0; c < RPW; c++)
+#pragma unroll
+            for (int rr = 0; rr <= K; rr++)
+#pragma unroll
+                for (int e = 0; e < 4; e++) gp[c][rr][e] = g[(size_t)(rr * (K + 1) + row0 + c) * M + 64 * e];
+    };
+    double2 gnext[RPW][K + 1][4];
+    if (LAT_PREF2) load_ggsw(gnext, 0, lane0 >> 4, lane0 & 15);
+    if (LAT_PRIO && wid >= (int)(blockDim.x >> 7)) __builtin_amdgcn_s_setprio(1);
     for (int i = 0; i < n; i++) {
         int lane = lane0;  // opaque per-iteration copy: lane-derived addresses are not hoisted
         asm volatile("" : "+v"(lane));
         stamp(i, 0);
         const int lrow = lane >> 4, col = lane & 15;
-        // this CMUX's GGSW operands of the MAC lane's block (see the MAC below) for each output
-        // column of this wave, loaded first so that their L2/MALL latency hides behind the rotation
-        // and the forward FFT
         const int ccm = 4 * w + (col & 3), xm = col >> 2;
+        // this CMUX's GGSW operands: loaded at its top, so that their L2/MALL latency hides behind
+        // the rotation and the forward FFT (LAT_PREF2: during the previous CMUX)
         double2 gpre[RPW][K + 1][4];
-        {
-            // engine layout: element s*64 + L <-> position 64 (L & 15) + 16 (L >> 4) + s, so position
-            // 64 ccm + 4 (lrow + 4 xm) + e is element (4 lrow + e) 64 + 16 xm + ccm
-            const double2 *g = a.fbsk + (size_t)i * ggsw_stride + 256 * lrow + 16 * xm + ccm;
+        if (LAT_PREF2) {
 #pragma unroll
             for (int c = 0; c < RPW; c++)
 #pragma unroll
                 for (int rr = 0; rr <= K; rr++)
 #pragma unroll
-                    for (int e = 0; e < 4; e++)
-                        gpre[c][rr][e] = g[(size_t)(rr * (K + 1) + row0 + c) * M + 64 * e];
+                    for (int e = 0; e < 4; e++) gpre[c][rr][e] = gnext[c][rr][e];
+            if (i + 1 < n) load_ggsw(gnext, i + 1, lrow, col);
+        } else {
+            load_ggsw(gpre, i, lrow, col);
         }
         __builtin_amdgcn_sched_barrier(0);
         const uint32_t at = pbs_modulus_switch<LOG2N>(in_s[i]);
@@ -268,7 +300,7 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const int C = lrow + 4 * q;
-                st2(Xr(r) + a1 + 64 * C, cmulw(v[r][q], tw1[q].re, tw1[q].im));
+                st2(Xr(r) + lswz(a1 + 64 * C), cmulw(v[r][q], tw1[q].re, tw1[q].im));
             }
         }
         stamp(i, 3);
@@ -280,13 +312,13 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
 #pragma unroll
             for (int r = 0; r < RPW; r++) {
 #pragma unroll
-                for (int q = 0; q < 4; q++) v[r][q] = ld2(Xr(r) + 64 * cc + a2 + 4 * (lrow + 4 * q));
+                for (int q = 0; q < 4; q++) v[r][q] = ld2(Xr(r) + lswz(64 * cc + a2 + 4 * (lrow + 4 * q)));
                 if (LAT_BF) dft16_fwd_rows_bf(v[r], rtw);
                 else dft16_fwd_rows(v[r], lrow);
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const int C2 = lrow + 4 * q;
-                    st2(Yr(r) + 64 * cc + a2 + 4 * C2, cmulw(v[r][q], tw2[q].re, tw2[q].im));
+                    st2(Yr(r) + lswz(64 * cc + a2 + 4 * C2), cmulw(v[r][q], tw2[q].re, tw2[q].im));
                 }
             }
         }
@@ -303,11 +335,11 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
             cx f[K + 1][4];
 #pragma unroll
             for (int rr = 0; rr <= K; rr++) {
-                const double2 *y = lds + LatLds::Y + rr * M + tb;
-                f[rr][0] = ld2(y);
-                f[rr][1] = ld2(y + 1);
-                f[rr][2] = ld2(y + 2);
-                f[rr][3] = ld2(y + 3);
+                const double2 *y = lds + LatLds::Y + rr * M;
+                f[rr][0] = ld2(y + lswz(tb));
+                f[rr][1] = ld2(y + lswz(tb + 1));
+                f[rr][2] = ld2(y + lswz(tb + 2));
+                f[rr][3] = ld2(y + lswz(tb + 3));
                 r4_fwd(f[rr][0], f[rr][1], f[rr][2], f[rr][3]);
             }
 #pragma unroll
@@ -334,7 +366,7 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
         for (int c = 0; c < RPW; c++) {
             r4_inv(o[c][0], o[c][1], o[c][2], o[c][3]);
 #pragma unroll
-            for (int e = 0; e < 4; e++) st2(Xr(c) + tb + e, o[c][e]);
+            for (int e = 0; e < 4; e++) st2(Xr(c) + lswz(tb + e), o[c][e]);
         }
         WaveLocalSync{}();
         {
@@ -344,7 +376,7 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const int C2 = lrow + 4 * q;
-                    v[r][q] = cmulw(ld2(Xr(r) + 64 * cc + a2 + 4 * C2), tw2[q].re, -tw2[q].im);
+                    v[r][q] = cmulw(ld2(Xr(r) + lswz(64 * cc + a2 + 4 * C2)), tw2[q].re, -tw2[q].im);
                 }
                 if (LAT_BF) dft16_inv_rows_bf(v[r], rtw);
                 else dft16_inv_rows(v[r], lrow);
@@ -353,7 +385,7 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
 #pragma unroll
             for (int r = 0; r < RPW; r++)
 #pragma unroll
-                for (int q = 0; q < 4; q++) st2(Xr(r) + 64 * cc + a2 + 4 * (lrow + 4 * q), v[r][q]);
+                for (int q = 0; q < 4; q++) st2(Xr(r) + lswz(64 * cc + a2 + 4 * (lrow + 4 * q)), v[r][q]);
         }
         stamp(i, 8);
         lds_barrier();  // (D)
@@ -366,7 +398,7 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const int C = lrow + 4 * q;
-                    v[r][q] = cmulw(ld2(Xr(r) + a1 + 64 * C), tw1[q].re, -tw1[q].im);
+                    v[r][q] = cmulw(ld2(Xr(r) + lswz(a1 + 64 * C)), tw1[q].re, -tw1[q].im);
                 }
                 if (LAT_BF) dft16_inv_rows_bf(v[r], rtw);
                 else dft16_inv_rows(v[r], lrow);
