@@ -187,7 +187,7 @@ def pbs_flops(p) -> float:
 
 
 PMC_ALIAS = {"mul32": "2_2ks"}  # the multiply DAG runs the 2_2 KS+PBS kernels: per-PBS traffic of that workload
-PMC_ROUND = "r03"
+PMC_ROUNDS = ("r04", "r03")  # newest committed PMC summary first (kernels unchanged since are still described by it)
 
 # dominant kernel of each workload: (kernel-timer family, rocprofv3 name normalised as
 # scripts/pmc_workload.py does).  Its average duration comes from the engine's HIP-event timer
@@ -223,13 +223,16 @@ def pmc_entry(by_kernel: dict, kernel: str):
 
 def load_pmc(tag: str, kernel: str):
     """The committed rocprofv3 PMC summary of this workload (scripts/pmc_workload.sh ->
-    profiles/r03_pmc_<tag>.json) and its entry for `kernel`.  A file without an entry for the
+    profiles/r04_pmc_<tag>.json, else r03) and its entry for `kernel`.  A file without an entry for the
     kernel the bench times is refused (returns the reason instead): counters of another kernel
     are not evidence for this one."""
-    name = f"{PMC_ROUND}_pmc_{PMC_ALIAS.get(tag, tag)}.json"
-    path = os.path.join(ROOT, "profiles", name)
-    if not os.path.exists(path):
-        return None, f"no PMC summary profiles/{name}"
+    for rnd in PMC_ROUNDS:
+        name = f"{rnd}_pmc_{PMC_ALIAS.get(tag, tag)}.json"
+        path = os.path.join(ROOT, "profiles", name)
+        if os.path.exists(path):
+            break
+    else:
+        return None, f"no PMC summary profiles/{PMC_ROUNDS[0]}_pmc_{PMC_ALIAS.get(tag, tag)}.json"
     d = json.load(open(path))
     e = pmc_entry(d.get("by_kernel") or {}, kernel)
     if e is None:

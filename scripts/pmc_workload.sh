@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 PMC passes (one counter group per run, each under its own time limit) of one bench
-# workload, summarised per kernel into gpurun_out/r03_pmc_<tag>.json (copied to profiles/).
+# workload, summarised per kernel into gpurun_out/<round>_pmc_<tag>.json (copied to profiles/).
 #   usage: pmc_workload.sh <tag>
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
@@ -29,4 +29,4 @@ run sq SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_IN
 run lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS TCC_HIT_sum TCC_MISS_sum && \
 python3 scripts/pmc_workload.py --fetch gpurun_out/pmc_$tag/fetch --write gpurun_out/pmc_$tag/write \
   --sq gpurun_out/pmc_$tag/sq --extra gpurun_out/pmc_$tag/lds --tag $tag --kernels "$K" --unit-kernel "$U" \
-  --units-per-dispatch $UPD --main-kernel "$M" --out gpurun_out/r03_pmc_$tag.json
+  --units-per-dispatch $UPD --main-kernel "$M" --out gpurun_out/${ROUND:-r04}_pmc_$tag.json
