@@ -32,7 +32,7 @@ def test_committed_pmc_names_the_timed_kernel(tag):
 def test_pmc_of_another_kernel_is_refused(tmp_path, monkeypatch):
     prof = tmp_path / "profiles"
     prof.mkdir()
-    (prof / f"{bench.PMC_ROUND}_pmc_2_2.json").write_text(json.dumps(
+    (prof / f"{bench.PMC_ROUNDS[0]}_pmc_2_2.json").write_text(json.dumps(
         {"by_kernel": {"pbs_multibit_kernel<2048,1,1,3>": {"hbm_bytes_per_dispatch": 1.0}}}))
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
     e, why = bench.load_pmc("2_2", "pbs_classic_kernel<2048,1,1>")
