@@ -72,7 +72,7 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 }  // namespace
 
 #ifndef LAT_BF
-#define LAT_BF 1  // branch-free row twiddles (per-lane constants + selects) instead of row branches
+#define LAT_BF 2  // row twiddles: 2 select-free fused products (RowTwF), 1 per-lane constants + selects, 0 row branches
 #endif
 
 // Row-split 16-point DFTs of dft16_fwd_rows / dft16_inv_rows (fft_device.h) with the internal
@@ -107,6 +107,59 @@ struct RowTw {
         return sp[k] ? sq : c;
     }
 };
+// Select-free form (LAT_BF = 2): every E as the same three fused products,
+//   U = fma(im, be, re),  U2 = fma(im, be2, re),  out = (fma(U, c1, im s1), fma(U2, c2, im s2))
+// with per-lane constants.  cmulw lanes (E = 0, 1, 3, 4, 9): be = be2 = 0, so U = U2 = re exactly,
+// and (c1, s1, c2, s2) = (wr, -wi, wi, wr): cmulw's (fma(re, wr, -(im wi)), fma(re, wi, im wr)).
+// sqrt(1/2) lanes: U, U2 = re + im or re - im with one rounding (the oracle's x.re + x.im etc.; its
+// x.im - x.re is the negation of re - im, folded into the sign of c), s1 = s2 = 0, c1, c2 = +-h, so
+// each output is the oracle's single rounding of (sum) * h.  Only the sign of a zero can differ from
+// the branchy form (a +-0 addend), which no later rounding observes.
+struct RowTwF {
+    double be[3], be2[3], c1[3], s1[3], c2[3], s2[3];
+    __device__ RowTwF(int A, bool inv) {
+        // every member by a conditional expression (no if/else over members: those leave the
+        // object in private memory instead of registers)
+        const double h = TM_SQH;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const int E = A * (k + 1);
+            const bool sq = E == 2 || E == 6, six = E == 6;
+            const double wr = E == 0 ? 1.0 : E == 1 ? TM_C16_1 : E == 3 ? TM_S16_1 : E == 4 ? 0.0 : -TM_C16_1;
+            const double wf = E == 0 ? 0.0 : E == 1 ? -TM_S16_1 : E == 3 ? -TM_C16_1 : E == 4 ? -1.0 : TM_S16_1;
+            const double wi = inv ? -wf : wf;
+            // fwd E=2: ((r+i)h, -((r-i)h))   fwd E=6: (-((r-i)h), -((r+i)h))
+            // inv E=2: ((r-i)h, (r+i)h)      inv E=6: (-((r+i)h), (r-i)h)
+            be[k] = !sq ? 0.0 : (inv ? six : !six) ? 1.0 : -1.0;
+            be2[k] = !sq ? 0.0 : (inv ? !six : six) ? 1.0 : -1.0;
+            c1[k] = !sq ? wr : six ? -h : h;
+            s1[k] = sq ? 0.0 : -wi;
+            c2[k] = !sq ? wi : inv ? h : -h;
+            s2[k] = sq ? 0.0 : wr;
+        }
+    }
+    __device__ __forceinline__ cx apply(int k, cx x) const {
+        const double u = fma(x.im, be[k], x.re);
+        const double u2 = fma(x.im, be2[k], x.re);
+        return {fma(u, c1[k], x.im * s1[k]), fma(u2, c2[k], x.im * s2[k])};
+    }
+};
+__device__ __forceinline__ void dft16_fwd_rows_sf(cx *v, const RowTwF &t) {
+    r4_fwd(v[0], v[1], v[2], v[3]);
+    v[1] = t.apply(0, v[1]);
+    v[2] = t.apply(1, v[2]);
+    v[3] = t.apply(2, v[3]);
+    transpose_rows4(v[0], v[1], v[2], v[3]);
+    r4_fwd(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void dft16_inv_rows_sf(cx *v, const RowTwF &t) {
+    r4_inv(v[0], v[1], v[2], v[3]);
+    transpose_rows4(v[0], v[1], v[2], v[3]);
+    v[1] = t.apply(0, v[1]);
+    v[2] = t.apply(1, v[2]);
+    v[3] = t.apply(2, v[3]);
+    r4_inv(v[0], v[1], v[2], v[3]);
+}
 __device__ __forceinline__ void dft16_fwd_rows_bf(cx *v, const RowTw &t) {
     r4_fwd(v[0], v[1], v[2], v[3]);
     v[1] = t.apply<false>(0, v[1]);
@@ -129,6 +182,10 @@ __device__ __forceinline__ void dft16_inv_rows_bf(cx *v, const RowTw &t) {
 #endif
 #ifndef LAT_PREF2
 #define LAT_PREF2 0  // GGSW of CMUX i + 1 loaded during CMUX i (two register sets) instead of at its top
+#endif
+
+#ifndef LAT_HOIST
+#define LAT_HOIST 1  // 1: the per-lane LDS / GGSW addresses are loop invariants (kept in VGPRs); 0: recomputed per CMUX
 #endif
 
 #ifndef LAT_STAMPS
@@ -155,6 +212,7 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
     // W[16 a2 C2] (a2 = col & 3), the twist of the lane's positions j_q = a1 + 64 (lrow + 4 q)
     cx tw1[4], tw2[4], tws[4];
     const RowTw rtw(lane0 >> 4);
+    const RowTwF rtf(lane0 >> 4, false), rti(lane0 >> 4, true);  // LAT_BF = 2
     {
         const int lrow = lane0 >> 4, col = lane0 & 15, a1 = 16 * w + col, a2 = col & 3;
 #pragma unroll
@@ -235,8 +293,8 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
     if (LAT_PREF2) load_ggsw(gnext, 0, lane0 >> 4, lane0 & 15);
     if (LAT_PRIO && wid >= (int)(blockDim.x >> 7)) __builtin_amdgcn_s_setprio(1);
     for (int i = 0; i < n; i++) {
-        int lane = lane0;  // opaque per-iteration copy: lane-derived addresses are not hoisted
-        asm volatile("" : "+v"(lane));
+        int lane = lane0;  // LAT_HOIST = 0: opaque per-iteration copy, lane-derived addresses not hoisted
+        if (!LAT_HOIST) asm volatile("" : "+v"(lane));
         stamp(i, 0);
         const int lrow = lane >> 4, col = lane & 15;
         const int ccm = 4 * w + (col & 3), xm = col >> 2;
@@ -294,7 +352,8 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
         // ---- forward stage 1: butterfly a1 = 16 w + col, column lrow ----
 #pragma unroll
         for (int r = 0; r < RPW; r++) {
-            if (LAT_BF) dft16_fwd_rows_bf(v[r], rtw);
+            if constexpr (LAT_BF == 2) dft16_fwd_rows_sf(v[r], rtf);
+            else if (LAT_BF) dft16_fwd_rows_bf(v[r], rtw);
             else dft16_fwd_rows(v[r], lrow);
             const int a1 = 16 * w + col;
 #pragma unroll
@@ -313,7 +372,8 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
             for (int r = 0; r < RPW; r++) {
 #pragma unroll
                 for (int q = 0; q < 4; q++) v[r][q] = ld2(Xr(r) + lswz(64 * cc + a2 + 4 * (lrow + 4 * q)));
-                if (LAT_BF) dft16_fwd_rows_bf(v[r], rtw);
+                if constexpr (LAT_BF == 2) dft16_fwd_rows_sf(v[r], rtf);
+                else if (LAT_BF) dft16_fwd_rows_bf(v[r], rtw);
                 else dft16_fwd_rows(v[r], lrow);
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
@@ -378,7 +438,8 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
                     const int C2 = lrow + 4 * q;
                     v[r][q] = cmulw(ld2(Xr(r) + lswz(64 * cc + a2 + 4 * C2)), tw2[q].re, -tw2[q].im);
                 }
-                if (LAT_BF) dft16_inv_rows_bf(v[r], rtw);
+                if constexpr (LAT_BF == 2) dft16_inv_rows_sf(v[r], rti);
+                else if (LAT_BF) dft16_inv_rows_bf(v[r], rtw);
                 else dft16_inv_rows(v[r], lrow);
             }
             WaveLocalSync{}();
@@ -400,7 +461,8 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
                     const int C = lrow + 4 * q;
                     v[r][q] = cmulw(ld2(Xr(r) + lswz(a1 + 64 * C)), tw1[q].re, -tw1[q].im);
                 }
-                if (LAT_BF) dft16_inv_rows_bf(v[r], rtw);
+                if constexpr (LAT_BF == 2) dft16_inv_rows_sf(v[r], rti);
+                else if (LAT_BF) dft16_inv_rows_bf(v[r], rtw);
                 else dft16_inv_rows(v[r], lrow);
 #pragma unroll
                 for (int q = 0; q < 4; q++)
