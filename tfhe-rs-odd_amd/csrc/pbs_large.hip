@@ -1214,6 +1214,77 @@ __global__ void __launch_bounds__(TOPT) large_top_inv_kernel(LargePbsLaunch a, i
     top_inv_body<N, K, G>(a, blockIdx.x / (BPP * (K + 1)), col, (blockIdx.x % BPP) * TOPT + threadIdx.x);
 }
 
+// Digits-fed CMUX (N = 4096 / 8192, L = 2): large_top_inv of CMUX i fused with split_digits of
+// CMUX i + 1.  One 1024-thread workgroup per (ciphertext, row): thread t runs top_inv_body's
+// butterfly t of column `row` (positions j = t + 1024 b), keeps the updated accumulator pairs in
+// registers, writes them to HBM (the extraction and the final CMUX read them there) and to LDS (one
+// row is M pairs, 32 / 64 KiB); after one barrier it gathers X^{a~_(i+1)} acc - acc at its own
+// positions from LDS and writes the row's half of the next CMUX's digit words.  Saves
+// split_digits' re-read of the accumulator from HBM (self + rotated pair per position) and one
+// launch per CMUX.  Same operations as top_inv_body + split_digits_kernel, so bit-identical.
+template <int N>
+__global__ void __launch_bounds__(1024) split_inv_digits_kernel(LargePbsLaunch a, int ct0, int i) {
+    using S = Split<N>;
+    constexpr int K = 1, R = S::R, M = S::M;
+    static_assert(M == 1024 * R, "one butterfly per thread");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    acc_pair *row_acc = reinterpret_cast<acc_pair *>(smem);
+    // XCD-aware as split_digits / large_dsub: ciphertext cl on XCD cl % 8
+    const int x = blockIdx.x & 7, m = blockIdx.x >> 3;
+    const int cl = x + 8 * (m >> 1), row = m & 1;
+    if (cl >= a.chunk_count) return;  // whole workgroup
+    const int t = threadIdx.x;
+    // ---- top DIT radix-R of butterfly t of column `row`, backward conversion, acc += ----
+    const double2 *U = a.spectra + ((size_t)cl * a.levels * (K + 1) + row) * M + t;
+    cx u[R];
+    u[0] = gld(U);
+#pragma unroll
+    for (int c = 1; c < R; c++) {
+        const cx w = gld(a.wtop + (c - 1) * 1024 + t);  // = W[t c]
+        u[c] = cmulw(gld(U + 1024 * c), w.re, -w.im);
+    }
+    dftR_inv<R>(u);
+    uint64_t *acc = a.acc + ((size_t)cl * (K + 1) + row) * N;
+    const double k32 = torus_k32();
+    uint64_t lo[R], hi[R];
+#pragma unroll
+    for (int b = 0; b < R; b++) {
+        const int j = t + 1024 * b;
+        const cx w = gld(a.twist + j);
+        const acc_pair pr = *reinterpret_cast<const acc_pair *>(acc + 2 * j);
+        lo[b] = pr.x;
+        hi[b] = pr.y;
+        backward_add(u[b], w, lo[b], hi[b], k32);  // the resident key carries the 1/M
+        const acc_pair nw = {lo[b], hi[b]};
+        *reinterpret_cast<acc_pair *>(acc + 2 * j) = nw;
+        row_acc[j] = nw;
+    }
+    __syncthreads();
+    // ---- split_digits of CMUX i + 1 for this row ----
+    const uint64_t *in = a.lwe_in + (size_t)(ct0 + cl) * (a.n + 1);
+    const uint32_t at = pbs_modulus_switch<S::LOGN>(in[i + 1]);
+    const bool full_odd = (at / N) & 1;
+    const int rem = at % N;
+    uint64_t *dig = reinterpret_cast<uint64_t *>(split_digits<N>(a, cl));
+#pragma unroll
+    for (int b = 0; b < R; b++) {
+        const int j = t + 1024 * b;
+        // ct1_pair_m with the self pair from registers and the rotated one from LDS
+        const int jj0 = j - rem;  // in (-N, M)
+        const acc_pair rot = row_acc[jj0 & (M - 1)];
+        const bool swap = jj0 < 0 && jj0 >= -M;
+        const uint64_t x0 = swap ? rot.y : rot.x, x1 = swap ? rot.x : rot.y;
+        const bool neg0 = (jj0 < 0) != full_odd, neg1 = (jj0 + M < 0) != full_odd;
+        const uint64_t d0 = (neg0 ? 0 - x0 : x0) - lo[b];
+        const uint64_t d1 = (neg1 ? 0 - x1 : x1) - hi[b];
+        int32_t e0[2], e1[2];
+        decompose64<2>(d0, a.base_log, e0);
+        decompose64<2>(d1, a.base_log, e1);
+        dig[2 * j + row] = ((uint64_t)((uint32_t)e0[0] & 0xffffu)) | ((uint64_t)((uint32_t)e1[0] & 0xffffu) << 16) |
+                           ((uint64_t)((uint32_t)e0[1] & 0xffffu) << 32) | ((uint64_t)((uint32_t)e1[1] & 0xffffu) << 48);
+    }
+}
+
 // sample extract at degree 0 (glwe_sample_extraction.rs:91-147)
 template <int N, int K>
 __global__ void __launch_bounds__(256) large_extract_kernel(LargePbsLaunch a, int ct0, int cnt) {
@@ -1352,6 +1423,16 @@ static bool large_dsub_enabled() {
     return v;
 }
 
+// TFHE_MI355_SPLIT_FUSED=0: the digits-fed CMUX with separate large_top_inv and split_digits
+// launches instead of split_inv_digits_kernel (A/B switch)
+static bool split_fused_enabled() {
+    static const bool v = [] {
+        const char *e = std::getenv("TFHE_MI355_SPLIT_FUSED");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // TFHE_MI355_PAIR_SUB=1: the classic split CMUX (L <= 2) through large_pair_sub_kernel too (A/B)
 static bool large_pair_sub_classic() {
     static const bool v = [] {
@@ -1412,8 +1493,10 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
                 constexpr int DPER = S::M / 256;
                 const unsigned dig_blocks = (unsigned)((cnt + 7) / 8) * 8 * DPER;
                 const unsigned dsub_blocks = (unsigned)((cnt + 7) / 8) * 8 * S::R;
+                const unsigned fused_blocks = (unsigned)((cnt + 7) / 8) * 8 * 2;  // (ct, row)
+                const bool fused = split_fused_enabled();
                 for (int i = 0; i < a.n; i++) {
-                    {
+                    if (i == 0 || !fused) {
                         TimedLaunch tl(a.timer, "split_digits_kernel", s);
                         hipLaunchKernelGGL((split_digits_kernel<N>), dim3(dig_blocks), dim3(256), 0, s, a, ct0, i);
                     }
@@ -1421,6 +1504,12 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
                         TimedLaunch tl(a.timer, "large_dsub_kernel", s);
                         hipLaunchKernelGGL((large_dsub_kernel<N>), dim3(dsub_blocks), dim3(Sub::THREADS), Sub::LDS, s,
                                            a, ct0, i);
+                    }
+                    if (fused && i + 1 < a.n) {  // top_inv of CMUX i + digits of CMUX i + 1
+                        TimedLaunch tl(a.timer, "split_inv_digits_kernel", s);
+                        hipLaunchKernelGGL((split_inv_digits_kernel<N>), dim3(fused_blocks), dim3(1024),
+                                           sizeof(acc_pair) * S::M, s, a, ct0, i);
+                        continue;
                     }
                     TimedLaunch tl(a.timer, "large_top_inv_kernel", s);
                     hipLaunchKernelGGL((large_top_inv_kernel<N, K, G>), dim3(top_blocks), dim3(TOPT), 0, s, a, ct0, i);
