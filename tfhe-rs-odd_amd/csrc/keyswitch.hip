@@ -161,7 +161,11 @@ __global__ void __launch_bounds__(256) ks_mfma_kernel(KeyswitchLaunch a, const i
     for (int b = 0; b < 8; b++)
 #pragma unroll
         for (int q = 0; q < 16; q++) acc[b][q] = 0;
-    for (size_t k = 0; k < mpad; k += 32) {
+    // split K (gridDim.z > 1, small batches): slice z of the rows, the partial products combined by
+    // 64-bit atomic adds into an output zeroed beforehand (sums mod 2^64: order-independent, exact)
+    const size_t kslice = mpad / gridDim.z / 32 * 32;  // whole 32-row steps; the last slice takes the rest
+    const size_t kbeg = kslice * blockIdx.z, kend = blockIdx.z + 1 == gridDim.z ? mpad : kbeg + kslice;
+    for (size_t k = kbeg; k < kend; k += 32) {
         const ks_v4i av = *reinterpret_cast<const ks_v4i *>(pa + k);
 #pragma unroll
         for (int b = 0; b < 8; b++) {
@@ -178,11 +182,14 @@ __global__ void __launch_bounds__(256) ks_mfma_kernel(KeyswitchLaunch a, const i
     for (int q = 0; q < 16; q++) {
         const int c = c0 + (q & 3) + 8 * (q >> 2) + 4 * h;
         if (c >= a.count) continue;
-        uint64_t v = (uint64_t)(int64_t)rowsum[c] * kOffset;
+        const bool first = blockIdx.z == 0;
+        uint64_t v = first ? (uint64_t)(int64_t)rowsum[c] * kOffset : 0;
 #pragma unroll
         for (int b = 0; b < 8; b++) v += (uint64_t)(int64_t)acc[b][q] << (8 * b);
-        const uint64_t body = (j == a.body()) ? a.lwe_in[(size_t)c * in_stride + a.in_dim] : 0;
-        a.lwe_out[(size_t)c * out_stride + j] = body - v;
+        const uint64_t body = (first && j == a.body()) ? a.lwe_in[(size_t)c * in_stride + a.in_dim] : 0;
+        uint64_t *o = a.lwe_out + (size_t)c * out_stride + j;
+        if (gridDim.z == 1) *o = body - v;
+        else atomicAdd(reinterpret_cast<unsigned long long *>(o), (unsigned long long)(body - v));
     }
     (void)cpad;
 }
@@ -222,8 +229,18 @@ hipError_t launch_keyswitch_mfma(const KeyswitchLaunch &a, const int8_t *kt, voi
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(ks_digits_kernel, dim3(a.count), dim3(256), 0, s, a, dig, rowsum, mpad);
-    hipLaunchKernelGGL(ks_mfma_kernel, dim3((unsigned)(jpad / 64), (unsigned)(cpad / 64)), dim3(256), 0, s, a, dig,
-                       rowsum, kt, mpad, jpad, cpad);
+    // few output tiles (small batches: 12 at 2_2 for up to 64 ciphertexts, each streaming 5 MiB of
+    // KSK planes through one CU): split K over up to ~256 workgroups, >= 8 k-steps each
+    const unsigned tiles = (unsigned)(jpad / 64) * (unsigned)(cpad / 64);
+    unsigned split = 1;
+    if (tiles < 128) split = (unsigned)std::min<size_t>((256 + tiles - 1) / tiles, mpad / 256);
+    if (split < 2) split = 1;
+    if (split > 1) {  // atomics accumulate into a zeroed output
+        hipError_t e = hipMemsetAsync(a.lwe_out, 0, (size_t)a.count * (a.out_dim + 1) * sizeof(uint64_t), s);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(ks_mfma_kernel, dim3((unsigned)(jpad / 64), (unsigned)(cpad / 64), split), dim3(256), 0, s, a,
+                       dig, rowsum, kt, mpad, jpad, cpad);
     return hipGetLastError();
 }
 
