@@ -4,8 +4,10 @@ set -e
 cd "$(dirname "$0")/../tfhe-rs-odd_amd"
 d=build/$1; mkdir -p $d
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $2"
-hipcc $F ${MB_SCHED--mllvm -amdgpu-sched-strategy=max-ilp} -c -o $d/pbs_multibit.o csrc/pbs_multibit.hip &  # as the Makefile
-for f in pbs_classic.hip pbs_latency.hip pbs_large.hip keyswitch.hip lwe_ops.hip glwe_ops.hip csprng.hip; do hipcc $F -c -o $d/${f%.hip}.o csrc/$f & done
+for f in pbs_multibit.hip pbs_latency.hip; do  # as the Makefile
+  hipcc $F ${MB_SCHED--mllvm -amdgpu-sched-strategy=max-ilp} -c -o $d/${f%.hip}.o csrc/$f &
+done
+for f in pbs_classic.hip pbs_large.hip keyswitch.hip lwe_ops.hip glwe_ops.hip csprng.hip; do hipcc $F -c -o $d/${f%.hip}.o csrc/$f & done
 for f in capi.cpp client.cpp serde.cpp; do hipcc $F -c -o $d/${f%.cpp}.o csrc/$f & done
 wait
 hipcc $F -shared -o $d/libtfhe_mi355.so $d/*.o
