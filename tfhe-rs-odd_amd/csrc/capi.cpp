@@ -175,6 +175,7 @@ struct TfheMi355Context {
         std::condition_variable cv;  // dispatchers: work queued / stop
         std::vector<CoalescedReq *> queue[CO_OPS];
         size_t queued[CO_OPS] = {};
+        size_t last_rows[CO_OPS] = {};  // rows of the op's previous batch (the window's early close)
         std::chrono::steady_clock::time_point last_arrival[CO_OPS];
         bool stop = false;
         std::vector<std::thread> workers;
@@ -873,8 +874,10 @@ void coalesce_dispatcher(TfheMi355Context *c, size_t q) {
                 }
             }
             rr = (size_t)op + 1;
+            // the window also closes as soon as as many rows are queued as the op's previous batch
+            // had: closed-loop callers (each waiting for its last call) are then all back
             const auto close = std::chrono::steady_clock::now() + coalesce_window();
-            while (!co.stop && co.queued[op] < cap) {
+            while (!co.stop && co.queued[op] < cap && !(co.last_rows[op] && co.queued[op] >= co.last_rows[op])) {
                 const auto t = std::min(close, co.last_arrival[op] + coalesce_gap());
                 if (std::chrono::steady_clock::now() >= t) break;
                 co.cv.wait_until(lk, t);
@@ -887,6 +890,7 @@ void coalesce_dispatcher(TfheMi355Context *c, size_t q) {
             }
             qu.erase(qu.begin(), qu.begin() + take);
             co.queued[op] -= cts;
+            co.last_rows[op] = cts;
             if (batch.empty()) {  // another slot took the queue during the window
                 co.in_flight--;
                 continue;
