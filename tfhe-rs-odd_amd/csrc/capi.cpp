@@ -122,6 +122,7 @@ struct CoalescedReq {
     size_t lut_count;
     const uint32_t *idx;
     size_t count;
+    bool sync = false;  // a blocking caller (coalesced_call), not a submitted request
     // completion: set by the dispatcher, waited on by the caller alone (no shared mutex, so a
     // finished batch wakes its callers without a thundering herd on the queue lock)
     std::mutex m;
@@ -175,7 +176,8 @@ struct TfheMi355Context {
         std::condition_variable cv;  // dispatchers: work queued / stop
         std::vector<CoalescedReq *> queue[CO_OPS];
         size_t queued[CO_OPS] = {};
-        size_t last_rows[CO_OPS] = {};  // rows of the op's previous batch (the window's early close)
+        size_t queued_sync[CO_OPS] = {};  // of queued[]: rows from blocking callers
+        size_t last_sync_rows[CO_OPS] = {};  // rows of the op's previous batch if all were blocking calls
         std::chrono::steady_clock::time_point last_arrival[CO_OPS];
         bool stop = false;
         std::vector<std::thread> workers;
@@ -874,23 +876,29 @@ void coalesce_dispatcher(TfheMi355Context *c, size_t q) {
                 }
             }
             rr = (size_t)op + 1;
-            // the window also closes as soon as as many rows are queued as the op's previous batch
-            // had: closed-loop callers (each waiting for its last call) are then all back
+            // the window also closes as soon as the blocking callers of the op's previous batch can
+            // all be back (as many blocking rows queued as it had; each such caller has one call
+            // outstanding).  Submitted requests keep the gap rule: a burst from one thread says
+            // nothing about how many more are coming.
             const auto close = std::chrono::steady_clock::now() + coalesce_window();
-            while (!co.stop && co.queued[op] < cap && !(co.last_rows[op] && co.queued[op] >= co.last_rows[op])) {
+            while (!co.stop && co.queued[op] < cap &&
+                   !(co.last_sync_rows[op] && co.queued_sync[op] >= co.last_sync_rows[op])) {
                 const auto t = std::min(close, co.last_arrival[op] + coalesce_gap());
                 if (std::chrono::steady_clock::now() >= t) break;
                 co.cv.wait_until(lk, t);
             }
             auto &qu = co.queue[op];
             size_t take = 0;
+            size_t sync_rows = 0;
             while (take < qu.size() && (batch.empty() || cts + qu[take]->count <= cap)) {
                 cts += qu[take]->count;
+                if (qu[take]->sync) sync_rows += qu[take]->count;
                 batch.push_back(qu[take++]);
             }
             qu.erase(qu.begin(), qu.begin() + take);
             co.queued[op] -= cts;
-            co.last_rows[op] = cts;
+            co.queued_sync[op] -= sync_rows;
+            co.last_sync_rows[op] = sync_rows == cts ? cts : 0;
             if (batch.empty()) {  // another slot took the queue during the window
                 co.in_flight--;
                 continue;
@@ -933,6 +941,7 @@ void coalesce_enqueue(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
             for (size_t q = 0; q < coalesce_slots(); q++) co.workers.emplace_back(coalesce_dispatcher, c, q);
         co.queue[op].push_back(&r);
         co.queued[op] += r.count;
+        if (r.sync) co.queued_sync[op] += r.count;
         co.last_arrival[op] = std::chrono::steady_clock::now();
     }
     co.cv.notify_one();
@@ -965,6 +974,7 @@ void coalesced_call(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
         if (idle) co.direct_busy = direct = true;
     }
     if (!direct) {
+        r.sync = true;
         coalesce_enqueue(c, op, r);
         coalesce_wait(r);
         return;
@@ -1177,6 +1187,7 @@ int tfhe_mi355_context_destroy(TfheMi355Context *ctx) {
                 orphans.insert(orphans.end(), ctx->co.queue[o].begin(), ctx->co.queue[o].end());
                 ctx->co.queue[o].clear();
                 ctx->co.queued[o] = 0;
+                ctx->co.queued_sync[o] = 0;
             }
         }
         ctx->co.cv.notify_all();
