@@ -522,6 +522,41 @@ __global__ void __launch_bounds__(256) split_digits_kernel(LargePbsLaunch a, int
     split_digits<N>(a, cl)[j] = acc_pair{w[0], w[1]};
 }
 
+// phase 1 of large_dsub_kernel for sub-block Q: butterflies a0 = tid + 256 t -> the LDS buffer of
+// polynomial p = (lvl - 1)(K+1) + r at a0 (twist, top DIF radix-R, output Q times W[a0 Q])
+template <int N, int Q>
+__device__ __forceinline__ void dsub_phase1(const LargePbsLaunch &a, const acc_pair *dig, double2 *lds) {
+    constexpr int K = 1, R = Split<N>::R;
+    using Cfg = LargeSubCfg<K, 2>;
+    for (int a0 = threadIdx.x; a0 < 1024; a0 += Cfg::THREADS) {
+        acc_pair dw[R];
+        cx tv[R];
+#pragma unroll
+        for (int b = 0; b < R; b++) {
+            dw[b] = dig[a0 + 1024 * b];
+            tv[b] = gld(a.twist + a0 + 1024 * b);
+        }
+        const cx wq = Q ? gld(a.wtop + (Q - 1) * 1024 + a0) : cx{1.0, 0.0};  // = W[a0 Q]
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int li = 0; li < 2; li++) {  // li = 0: level L (the top stage's first pass), 1: level L-1
+                cx u[R];
+#pragma unroll
+                for (int b = 0; b < R; b++) {
+                    const uint64_t wr = r ? dw[b].y : dw[b].x;
+                    const int32_t e0 = (int32_t)(int16_t)((wr >> (32 * li)) & 0xffffu);
+                    const int32_t e1 = (int32_t)(int16_t)((wr >> (32 * li + 16)) & 0xffffu);
+                    u[b] = cmulw(cx{(double)e0, (double)e1}, tv[b].re, tv[b].im);
+                }
+                dftR_fwd<R>(u);
+                const cx y = Q ? cmulw(u[Q], wq.re, wq.im) : u[0];
+                const int p = (1 - li) * (K + 1) + r;  // level L -> polys 2, 3; level L-1 -> 0, 1
+                lds[p * SubFft::XL + a0] = make_double2(y.re, y.im);
+            }
+    }
+}
+
 template <int N>
 __global__ void __launch_bounds__((LargeSubCfg<1, 2>::THREADS), 2) large_dsub_kernel(LargePbsLaunch a, int ct0, int i) {
     constexpr int K = 1, L = 2;
@@ -542,36 +577,13 @@ __global__ void __launch_bounds__((LargeSubCfg<1, 2>::THREADS), 2) large_dsub_ke
     for (int e = threadIdx.x; e < SubFft::Lds::s1_len; e += Cfg::THREADS) s1[e] = a.W[R * (e & 63) * ((e >> 6) + 1)];
     const SubFft::Lds tw{s1, s1};
     const acc_pair *dig = split_digits<N>(a, cl);
-    // phase 1: butterflies a0 = tid + 256 t -> buffer of polynomial p = (lvl - 1)(K+1) + r at a0
-    for (int a0 = threadIdx.x; a0 < 1024; a0 += Cfg::THREADS) {
-        acc_pair dw[R];
-        cx tv[R];
-#pragma unroll
-        for (int b = 0; b < R; b++) {
-            dw[b] = dig[a0 + 1024 * b];
-            tv[b] = gld(a.twist + a0 + 1024 * b);
-        }
-        const cx wq = q ? gld(a.wtop + (q - 1) * 1024 + a0) : cx{1.0, 0.0};  // = W[a0 q]
-#pragma unroll
-        for (int r = 0; r < 2; r++)
-#pragma unroll
-            for (int li = 0; li < 2; li++) {  // li = 0: level L (the top stage's first pass), 1: level L-1
-                cx u[R];
-#pragma unroll
-                for (int b = 0; b < R; b++) {
-                    const uint64_t wr = r ? dw[b].y : dw[b].x;
-                    const int32_t e0 = (int32_t)(int16_t)((wr >> (32 * li)) & 0xffffu);
-                    const int32_t e1 = (int32_t)(int16_t)((wr >> (32 * li + 16)) & 0xffffu);
-                    u[b] = cmulw(cx{(double)e0, (double)e1}, tv[b].re, tv[b].im);
-                }
-                dftR_fwd<R>(u);
-                cx y = u[0];
-#pragma unroll
-                for (int c = 1; c < R; c++)
-                    if (c == q) y = cmulw(u[c], wq.re, wq.im);
-                const int p = (1 - li) * (K + 1) + r;  // level L -> polys 2, 3; level L-1 -> 0, 1
-                lds[p * SubFft::XL + a0] = make_double2(y.re, y.im);
-            }
+    // phase 1 with the sub-block index a compile-time constant, so that only output q of each top
+    // radix-R butterfly is computed (the compiler drops the other outputs' adds)
+    switch (q) {
+        case 0: dsub_phase1<N, 0>(a, dig, lds); break;
+        case 1: dsub_phase1<N, 1>(a, dig, lds); break;
+        case 2: if constexpr (R > 2) dsub_phase1<N, 2>(a, dig, lds); break;
+        default: if constexpr (R > 3) dsub_phase1<N, 3>(a, dig, lds); break;
     }
     __syncthreads();  // phase-1 outputs and the twiddle table
     cx v[16];
