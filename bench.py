@@ -767,6 +767,8 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="ciphertexts per GPU per step (default 4096; 1024 at 4_4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-abi", action="store_true", help="skip the host-pointer ABI rate")
+    ap.add_argument("--no-single-call", action="store_true",
+                    help="skip the one-ciphertext call latency (kernel traces / PMC runs of the batch)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-other-workloads", action="store_true",
@@ -1077,7 +1079,8 @@ def run_pbs(args, P, pname, workload, kname, R):
     ok = int(np.count_nonzero(dec == msgs))
     agg = aggregate(R, nb * args.steps, wall, ok, nb, lo, hi)
 
-    latency = single_call_latency(eng, pname, cts, acc, with_ks) if R.rank == 0 else None
+    # (profiling runs skip it: its count = 1 launches would mix into the per-kernel averages)
+    latency = single_call_latency(eng, pname, cts, acc, with_ks) if R.rank == 0 and not args.no_single_call else None
     host_abi = None
     if not args.no_host_abi and R.rank == 0 and P.polynomial_size <= 2048:
         host_abi = host_abi_rate(eng, P, cts, acc, with_ks)
@@ -1122,8 +1125,9 @@ def run_pbs(args, P, pname, workload, kname, R):
         }
         if host_abi:
             line["host_abi"] = host_abi
-        line["single_call_latency_ms"] = latency["ms"]
-        line["single_call_latency"] = latency
+        if latency:
+            line["single_call_latency_ms"] = latency["ms"]
+            line["single_call_latency"] = latency
         if R.world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or cpu_share()
             line["cpu_baseline"] = cpu_baseline(P, bsk, cts, acc, threads, ksk)

@@ -24,7 +24,7 @@ for s in ${STAGES:-tests smoke bench}; do
               python3 scripts/latency_probe.py 1,64,256
           else
             step r04_kt_$t 400 rocprofv3 --kernel-trace --stats -d gpurun_out/kt_$t -o run --output-format csv -- \
-              python3 bench.py --params $t --steps 3 --warmup 1 --no-cpu-baseline --no-host-abi --no-other-workloads
+              python3 bench.py --params $t --steps 3 --warmup 1 --no-cpu-baseline --no-host-abi --no-single-call --no-other-workloads
           fi
           find gpurun_out/kt_$t -name '*kernel_trace.csv' -delete
         done ;;

@@ -16,7 +16,7 @@ case $tag in
   mb3_3g2|mb3_3g3) K='large_|split_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=384; M='large_pair_sub_kernel|large_sub_kernel'; ARGS="--params $tag --batch 384" ;;
   *) echo "unknown tag $tag"; exit 2 ;;
 esac
-B="$ARGS --steps 2 --warmup 1 --no-cpu-baseline --no-host-abi"
+B="$ARGS --steps 2 --warmup 1 --no-cpu-baseline --no-host-abi --no-single-call"
 run() {  # run NAME COUNTERS...
   local n=$1; shift
   # counters only for the workload's own kernels (copy / fill kernels of the runtime excluded)
