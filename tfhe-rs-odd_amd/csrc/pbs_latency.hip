@@ -188,6 +188,10 @@ __device__ __forceinline__ void dft16_inv_rows_bf(cx *v, const RowTw &t) {
 #define LAT_HOIST 1  // 1: the per-lane LDS / GGSW addresses are loop invariants (kept in VGPRs); 0: recomputed per CMUX
 #endif
 
+#ifndef LAT_TSKIP
+#define LAT_TSKIP 0  // timing-only builds (wrong outputs): 1 = skip the inverse's wave-private exchange
+#endif
+
 #ifndef LAT_STAMPS
 #define LAT_STAMPS 0  // diagnostic builds: s_memtime per CMUX phase of block 0 into the ticket buffer
 #endif
@@ -426,9 +430,10 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
         for (int c = 0; c < RPW; c++) {
             r4_inv(o[c][0], o[c][1], o[c][2], o[c][3]);
 #pragma unroll
-            for (int e = 0; e < 4; e++) st2(Xr(c) + lswz(tb + e), o[c][e]);
+            for (int e = 0; e < 4; e++)
+                if (!(LAT_TSKIP & 1)) st2(Xr(c) + lswz(tb + e), o[c][e]);
         }
-        WaveLocalSync{}();
+        if (!(LAT_TSKIP & 1)) WaveLocalSync{}();
         {
             const int cc = 4 * w + (col >> 2), a2 = col & 3;
 #pragma unroll
@@ -436,7 +441,9 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const int C2 = lrow + 4 * q;
-                    v[r][q] = cmulw(ld2(Xr(r) + lswz(64 * cc + a2 + 4 * C2)), tw2[q].re, -tw2[q].im);
+                    // LAT_TSKIP & 1 (timing only, wrong outputs): no wave-private exchange
+                    const cx x = (LAT_TSKIP & 1) ? o[r][q] : ld2(Xr(r) + lswz(64 * cc + a2 + 4 * C2));
+                    v[r][q] = cmulw(x, tw2[q].re, -tw2[q].im);
                 }
                 if constexpr (LAT_BF == 2) dft16_inv_rows_sf(v[r], rti);
                 else if (LAT_BF) dft16_inv_rows_bf(v[r], rtw);
