@@ -1193,6 +1193,15 @@ int tfhe_mi355_context_destroy(TfheMi355Context *ctx) {
         ctx->co.cv.notify_all();
         for (auto &t : ctx->co.workers) t.join();
         ctx->co.workers.clear();
+        // a direct call (coalesced_call on an idle coalescer) still running on another thread
+        // finishes on slot 8 before the slots' streams and the tables go (none starts after stop)
+        for (;;) {
+            {
+                std::lock_guard<std::mutex> g(ctx->co.m);
+                if (!ctx->co.direct_busy) break;
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(100));
+        }
         for (auto *x : orphans) {
             std::lock_guard<std::mutex> g(x->m);
             x->err = "the context was destroyed before this request ran (wait on every request first)";
