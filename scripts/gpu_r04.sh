@@ -17,6 +17,7 @@ for s in ${STAGES:-tests smoke bench}; do
     tests) step r04_gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) step r04_smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step r04_bench_default 900 python bench.py --steps 10 --warmup 2 ;;
+    rehearse2) step r04_rehearse2_gloo_1gpu 1100 env BENCH_DIST_BACKEND=gloo python -u bench.py --gpus 2 --steps 5 --warmup 1 ;;
     bench22) step r04_bench_2_2 400 python bench.py --params 2_2 --steps 10 --warmup 2 --no-other-workloads ;;
     kt) for t in ${KT_TAGS:-2_2}; do
           if [ "$t" = lat ]; then

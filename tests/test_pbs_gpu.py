@@ -91,6 +91,14 @@ def test_keyswitch_bit_exact_vs_oracle(orc, keys_2_2, engine_2_2):
     assert np.array_equal(engine_2_2.keyswitch(rnd), orc.keyswitch(keys_2_2.ksk, 2048, 742, 3, 5, rnd))
 
 
+@pytest.mark.parametrize("count", [1, 2, 63, 64, 65, 200])
+def test_keyswitch_split_k_counts_bit_exact(orc, keys_2_2, engine_2_2, count):
+    """Small batches split the MFMA keyswitch's K over workgroups and sum the partial products
+    with 64-bit atomics (keyswitch.hip): every count around the 64-row tile, random rows."""
+    rnd = np.random.default_rng(40 + count).integers(0, 2 ** 64, (count, 2049), dtype=np.uint64)
+    assert np.array_equal(engine_2_2.keyswitch(rnd), orc.keyswitch(keys_2_2.ksk, 2048, 742, 3, 5, rnd))
+
+
 def test_keyswitch_programmable_bootstrap_shortint_order(orc, keys_2_2, engine_2_2):
     """PBSOrder::KeyswitchBootstrap (server_key/mod.rs:783-857): big-key in, big-key out."""
     p = keys_2_2.params
