@@ -27,9 +27,14 @@
  *     the same entry point are coalesced into shared batches that a dispatcher thread of the
  *     context runs on its own stream, each caller blocking until its own rows are written
  *     (a batch closes when no call has arrived for TFHE_MI355_COALESCE_GAP_US = 50, after at most
- *     _WINDOW_US = 500, or at _BATCH = 1024 ciphertexts; _SLOTS, _OVERFLOW: a second batch runs
- *     concurrently only when half a batch is queued; the one-ciphertext-per-call pattern,
- *     shortint/server_key/mod.rs:783-857; TFHE_MI355_COALESCE_MAX_COUNT=0 turns it off).
+ *     _WINDOW_US = 500, at _BATCH = 1024 ciphertexts, or -- blocking callers only -- as soon as
+ *     as many rows are queued as the previous batch of the entry point had; _SLOTS, _OVERFLOW: a
+ *     second batch runs concurrently only when half a batch is queued; a call that finds the
+ *     coalescer idle runs at once on the calling thread, TFHE_MI355_COALESCE_DIRECT=0 turns that
+ *     off; the one-ciphertext-per-call pattern, shortint/server_key/mod.rs:783-857;
+ *     TFHE_MI355_COALESCE_MAX_COUNT=0 turns coalescing off).  Batches of at most
+ *     TFHE_MI355_LATENCY_MAX = 256 ciphertexts at N = 2048, k = 1, L = 1 run a one-ciphertext-
+ *     per-CU latency kernel (same outputs; 0 = never).
  *     The _async calls hold no per-context mutable state: every device scratch buffer they
  *     need comes from the caller (d_scratch, sized by the matching *_scratch query; a call
  *     given less than its query fails with an error, and only a query returning 0 allows
