@@ -188,6 +188,10 @@ __device__ __forceinline__ void dft16_inv_rows_bf(cx *v, const RowTw &t) {
 #define LAT_HOIST 1  // 1: the per-lane LDS / GGSW addresses are loop invariants (kept in VGPRs); 0: recomputed per CMUX
 #endif
 
+#ifndef LAT_EARLYACC
+#define LAT_EARLYACC 1  // 1: each accumulator pair goes to LDS right after its backward conversion (0: at the CMUX top)
+#endif
+
 #ifndef LAT_TSKIP
 #define LAT_TSKIP 0  // timing-only builds (wrong outputs): 1 = skip the inverse's wave-private exchange
 #endif
@@ -322,14 +326,18 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
         const int rem = at % N;
 
         // ---- accumulator -> LDS pairs, rotation gather, ct1 = X^at acc - acc, digits, twist ----
+        // (LAT_EARLYACC: the pairs were stored by the previous CMUX's backward conversion, or before
+        // the loop; Y is free then -- its last reads were the MAC's, before barrier D)
+        if (!LAT_EARLYACC || i == 0) {
 #pragma unroll
-        for (int r = 0; r < RPW; r++)
+            for (int r = 0; r < RPW; r++)
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int j = 16 * w + col + 64 * lrow + 256 * q;
-                Ar(r)[2 * j] = lo[r][q];
-                Ar(r)[2 * j + 1] = hi[r][q];
-            }
+                for (int q = 0; q < 4; q++) {
+                    const int j = 16 * w + col + 64 * lrow + 256 * q;
+                    Ar(r)[2 * j] = lo[r][q];
+                    Ar(r)[2 * j + 1] = hi[r][q];
+                }
+        }
         lds_barrier();  // (A) every wave's pairs written
         stamp(i, 1);
         cx v[RPW][4];
@@ -472,8 +480,14 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
                 else if (LAT_BF) dft16_inv_rows_bf(v[r], rtw);
                 else dft16_inv_rows(v[r], lrow);
 #pragma unroll
-                for (int q = 0; q < 4; q++)
+                for (int q = 0; q < 4; q++) {
                     backward_add(v[r][q], tws[q], lo[r][q], hi[r][q], k32);  // the resident key carries the 1/M
+                    if constexpr (LAT_EARLYACC) {  // the next rotation's pair, stored as soon as it is final
+                        const int j = 16 * w + col + 64 * lrow + 256 * q;
+                        Ar(r)[2 * j] = lo[r][q];
+                        Ar(r)[2 * j + 1] = hi[r][q];
+                    }
+                }
             }
         }
         stamp(i, 10);
