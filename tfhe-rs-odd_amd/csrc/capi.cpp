@@ -826,7 +826,8 @@ void run_coalesced_batch(TfheMi355Context *c, TfheMi355Context::Coalescer::Slot 
     if (d.lut) {
         sl.d_luts.reserve(sets * glwe * 8);
         check(hipMemcpyAsync(sl.d_luts.ptr, sl.h_luts.ptr, sets * glwe * 8, hipMemcpyHostToDevice, s), "H2D luts");
-        check(hipMemcpyAsync(sl.d_idx.ptr, hidx, total * 4, hipMemcpyHostToDevice, s), "H2D idx");
+        if (sets > 1)  // one LUT set: no per-row indexes (the launch below passes none)
+            check(hipMemcpyAsync(sl.d_idx.ptr, hidx, total * 4, hipMemcpyHostToDevice, s), "H2D idx");
     }
     d.launch(c, (const uint64_t *)sl.d_in.ptr, (uint64_t *)sl.d_out.ptr, (const uint64_t *)sl.d_luts.ptr,
              d.lut ? sets : 0, d.lut && sets > 1 ? (const uint32_t *)sl.d_idx.ptr : nullptr, total,

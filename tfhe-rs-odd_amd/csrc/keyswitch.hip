@@ -113,9 +113,13 @@ __global__ void __launch_bounds__(256) ksk_repack_kernel(const uint64_t *__restr
 
 // one workgroup per ciphertext: digits D[c][i*L + l] (levels L..1 as the KSK rows) and rowsum
 __global__ void __launch_bounds__(256) ks_digits_kernel(KeyswitchLaunch a, int8_t *__restrict__ dig,
-                                                        int *__restrict__ rowsum, size_t mpad) {
+                                                        int *__restrict__ rowsum, size_t mpad, int zero_out) {
     __shared__ int red[256];
     const int c = blockIdx.x;
+    if (zero_out) {  // split-K: the GEMM's workgroups add their partial products into a zeroed row
+        uint64_t *o = a.lwe_out + (size_t)c * ((size_t)a.out_dim + 1);
+        for (int j = threadIdx.x; j <= a.out_dim; j += 256) o[j] = 0;
+    }
     const int in_dim = a.in_dim, L = a.level, beta = a.base_log;
     const uint64_t mask = (1ULL << beta) - 1;
     const uint64_t *x = a.lwe_in + (size_t)c * (in_dim + 1);
@@ -165,8 +169,10 @@ __global__ void __launch_bounds__(256) ks_mfma_kernel(KeyswitchLaunch a, const i
     // 64-bit atomic adds into an output zeroed beforehand (sums mod 2^64: order-independent, exact)
     const size_t kslice = mpad / gridDim.z / 32 * 32;  // whole 32-row steps; the last slice takes the rest
     const size_t kbeg = kslice * blockIdx.z, kend = blockIdx.z + 1 == gridDim.z ? mpad : kbeg + kslice;
+    // digit rows past the batch (the tile's padding) read as zero: no memset of the scratch
+    const bool arow = c0 + r < a.count;
     for (size_t k = kbeg; k < kend; k += 32) {
-        const ks_v4i av = *reinterpret_cast<const ks_v4i *>(pa + k);
+        const ks_v4i av = arow ? *reinterpret_cast<const ks_v4i *>(pa + k) : ks_v4i{0, 0, 0, 0};
 #pragma unroll
         for (int b = 0; b < 8; b++) {
             const ks_v4i bv = *reinterpret_cast<const ks_v4i *>(pb + (size_t)b * plane + k);
@@ -224,21 +230,15 @@ hipError_t launch_keyswitch_mfma(const KeyswitchLaunch &a, const int8_t *kt, voi
     const int cpad = (a.count + 63) / 64 * 64;
     int8_t *dig = reinterpret_cast<int8_t *>(scratch);
     int *rowsum = reinterpret_cast<int *>(reinterpret_cast<char *>(scratch) + (((size_t)cpad * mpad + 255) / 256) * 256);
-    if (cpad > a.count) {
-        hipError_t e = hipMemsetAsync(dig + (size_t)a.count * mpad, 0, (size_t)(cpad - a.count) * mpad, s);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(ks_digits_kernel, dim3(a.count), dim3(256), 0, s, a, dig, rowsum, mpad);
     // few output tiles (small batches: 12 at 2_2 for up to 64 ciphertexts, each streaming 5 MiB of
-    // KSK planes through one CU): split K over up to ~256 workgroups, >= 8 k-steps each
+    // KSK planes through one CU, latency-bound at one k-step per load round trip): split K over up
+    // to ~1024 workgroups (4 per CU), >= 4 k-steps each; ks_digits_kernel zeroes the output rows
+    // that the slices' 64-bit atomics accumulate into
     const unsigned tiles = (unsigned)(jpad / 64) * (unsigned)(cpad / 64);
     unsigned split = 1;
-    if (tiles < 128) split = (unsigned)std::min<size_t>((256 + tiles - 1) / tiles, mpad / 256);
+    if (tiles < 128) split = (unsigned)std::min<size_t>((1024 + tiles - 1) / tiles, mpad / 128);
     if (split < 2) split = 1;
-    if (split > 1) {  // atomics accumulate into a zeroed output
-        hipError_t e = hipMemsetAsync(a.lwe_out, 0, (size_t)a.count * (a.out_dim + 1) * sizeof(uint64_t), s);
-        if (e != hipSuccess) return e;
-    }
+    hipLaunchKernelGGL(ks_digits_kernel, dim3(a.count), dim3(256), 0, s, a, dig, rowsum, mpad, split > 1 ? 1 : 0);
     hipLaunchKernelGGL(ks_mfma_kernel, dim3((unsigned)(jpad / 64), (unsigned)(cpad / 64), split), dim3(256), 0, s, a,
                        dig, rowsum, kt, mpad, jpad, cpad);
     return hipGetLastError();
