@@ -111,12 +111,15 @@ __global__ void __launch_bounds__(256) ksk_repack_kernel(const uint64_t *__restr
     for (int b = 0; b < 8; b++) kt[((size_t)b * jpad + j) * mpad + m] = (int8_t)(uint8_t)(((v >> (8 * b)) & 0xff) ^ 0x80);
 }
 
-// one workgroup per ciphertext: digits D[c][i*L + l] (levels L..1 as the KSK rows) and rowsum
+// KS_DPARTS workgroups per ciphertext: digits D[c][i*L + l] (levels L..1 as the KSK rows) of an
+// eighth of the inputs each, and that part's digit sum (rowsum[c][part]: the GEMM adds the parts,
+// so no reduction across workgroups and no zeroing is needed)
+constexpr int KS_DPARTS = 8;
 __global__ void __launch_bounds__(256) ks_digits_kernel(KeyswitchLaunch a, int8_t *__restrict__ dig,
                                                         int *__restrict__ rowsum, size_t mpad, int zero_out) {
     __shared__ int red[256];
-    const int c = blockIdx.x;
-    if (zero_out) {  // split-K: the GEMM's workgroups add their partial products into a zeroed row
+    const int c = blockIdx.x / KS_DPARTS, part = blockIdx.x % KS_DPARTS;
+    if (zero_out && part == 0) {  // split-K: the GEMM's workgroups add their partial products into a zeroed row
         uint64_t *o = a.lwe_out + (size_t)c * ((size_t)a.out_dim + 1);
         for (int j = threadIdx.x; j <= a.out_dim; j += 256) o[j] = 0;
     }
@@ -124,8 +127,9 @@ __global__ void __launch_bounds__(256) ks_digits_kernel(KeyswitchLaunch a, int8_
     const uint64_t mask = (1ULL << beta) - 1;
     const uint64_t *x = a.lwe_in + (size_t)c * (in_dim + 1);
     int8_t *d = dig + (size_t)c * mpad;
+    const int per = (in_dim + KS_DPARTS - 1) / KS_DPARTS, i0 = part * per, i1 = min(in_dim, i0 + per);
     int sum = 0;
-    for (int i = threadIdx.x; i < in_dim; i += 256) {
+    for (int i = i0 + threadIdx.x; i < i1; i += 256) {
         uint64_t state = closest_repr(x[i], beta, L) >> (64 - beta * L);
         for (int l = 0; l < L; l++) {
             uint64_t res = state & mask;
@@ -138,14 +142,15 @@ __global__ void __launch_bounds__(256) ks_digits_kernel(KeyswitchLaunch a, int8_
             sum += v;
         }
     }
-    for (size_t m = (size_t)in_dim * L + threadIdx.x; m < mpad; m += 256) d[m] = 0;
+    if (part == KS_DPARTS - 1)
+        for (size_t m = (size_t)in_dim * L + threadIdx.x; m < mpad; m += 256) d[m] = 0;
     red[threadIdx.x] = sum;
     __syncthreads();
     for (int w = 128; w > 0; w >>= 1) {
         if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) rowsum[c] = red[0];
+    if (threadIdx.x == 0) rowsum[(size_t)c * KS_DPARTS + part] = red[0];
 }
 
 // workgroup tile: 64 ciphertexts x 64 output columns, 4 waves of 32 x 32, 8 byte planes each
@@ -189,7 +194,11 @@ __global__ void __launch_bounds__(256) ks_mfma_kernel(KeyswitchLaunch a, const i
         const int c = c0 + (q & 3) + 8 * (q >> 2) + 4 * h;
         if (c >= a.count) continue;
         const bool first = blockIdx.z == 0;
-        uint64_t v = first ? (uint64_t)(int64_t)rowsum[c] * kOffset : 0;
+        int rs = 0;
+        if (first)
+#pragma unroll
+            for (int p = 0; p < KS_DPARTS; p++) rs += rowsum[(size_t)c * KS_DPARTS + p];
+        uint64_t v = (uint64_t)(int64_t)rs * kOffset;
 #pragma unroll
         for (int b = 0; b < 8; b++) v += (uint64_t)(int64_t)acc[b][q] << (8 * b);
         const uint64_t body = (first && j == a.body()) ? a.lwe_in[(size_t)c * in_stride + a.in_dim] : 0;
@@ -210,7 +219,7 @@ bool ks_mfma_supported(int in_dim, int level, int base_log) {
 
 size_t ks_mfma_scratch_bytes(int in_dim, int level, int count) {
     const size_t cp = ((size_t)count + 63) / 64 * 64;
-    return cp * ks_mfma_rows(in_dim, level) + cp * sizeof(int) + 256;
+    return cp * ks_mfma_rows(in_dim, level) + cp * KS_DPARTS * sizeof(int) + 256;
 }
 
 hipError_t launch_ksk_repack(const uint64_t *ksk, int8_t *kt, int in_dim, int level, int out_dim, hipStream_t s) {
@@ -232,13 +241,14 @@ hipError_t launch_keyswitch_mfma(const KeyswitchLaunch &a, const int8_t *kt, voi
     int *rowsum = reinterpret_cast<int *>(reinterpret_cast<char *>(scratch) + (((size_t)cpad * mpad + 255) / 256) * 256);
     // few output tiles (small batches: 12 at 2_2 for up to 64 ciphertexts, each streaming 5 MiB of
     // KSK planes through one CU, latency-bound at one k-step per load round trip): split K over up
-    // to ~1024 workgroups (4 per CU), >= 4 k-steps each; ks_digits_kernel zeroes the output rows
+    // to ~2048 workgroups (8 per CU), >= 2 k-steps each; ks_digits_kernel zeroes the output rows
     // that the slices' 64-bit atomics accumulate into
     const unsigned tiles = (unsigned)(jpad / 64) * (unsigned)(cpad / 64);
     unsigned split = 1;
-    if (tiles < 128) split = (unsigned)std::min<size_t>((1024 + tiles - 1) / tiles, mpad / 128);
+    if (tiles < 128) split = (unsigned)std::min<size_t>((2048 + tiles - 1) / tiles, mpad / 64);
     if (split < 2) split = 1;
-    hipLaunchKernelGGL(ks_digits_kernel, dim3(a.count), dim3(256), 0, s, a, dig, rowsum, mpad, split > 1 ? 1 : 0);
+    hipLaunchKernelGGL(ks_digits_kernel, dim3((unsigned)a.count * KS_DPARTS), dim3(256), 0, s, a, dig, rowsum, mpad,
+                       split > 1 ? 1 : 0);
     hipLaunchKernelGGL(ks_mfma_kernel, dim3((unsigned)(jpad / 64), (unsigned)(cpad / 64), split), dim3(256), 0, s, a,
                        dig, rowsum, kt, mpad, jpad, cpad);
     return hipGetLastError();
