@@ -11,6 +11,8 @@
 // digits.  A workgroup owns a 64-ciphertext x 64-column tile; every KSK row segment it loads
 // (512 B, coalesced) is reused by its 64 ciphertexts, the digits are staged in LDS per chunk
 // of input coefficients and broadcast to the wave.
+#include <cstdlib>
+
 #include "engine.h"
 
 namespace tfhe_mi355 {
@@ -176,6 +178,7 @@ __global__ void __launch_bounds__(256) ks_mfma_kernel(KeyswitchLaunch a, const i
     const size_t kbeg = kslice * blockIdx.z, kend = blockIdx.z + 1 == gridDim.z ? mpad : kbeg + kslice;
     // digit rows past the batch (the tile's padding) read as zero: no memset of the scratch
     const bool arow = c0 + r < a.count;
+#pragma unroll 4
     for (size_t k = kbeg; k < kend; k += 32) {
         const ks_v4i av = arow ? *reinterpret_cast<const ks_v4i *>(pa + k) : ks_v4i{0, 0, 0, 0};
 #pragma unroll
@@ -241,11 +244,17 @@ hipError_t launch_keyswitch_mfma(const KeyswitchLaunch &a, const int8_t *kt, voi
     int *rowsum = reinterpret_cast<int *>(reinterpret_cast<char *>(scratch) + (((size_t)cpad * mpad + 255) / 256) * 256);
     // few output tiles (small batches: 12 at 2_2 for up to 64 ciphertexts, each streaming 5 MiB of
     // KSK planes through one CU, latency-bound at one k-step per load round trip): split K over up
-    // to ~2048 workgroups (8 per CU), >= 2 k-steps each; ks_digits_kernel zeroes the output rows
+    // to ~1024 workgroups (4 per CU; more slices cost more in atomics on the same words than they
+    // gain), >= 2 k-steps each; ks_digits_kernel zeroes the output rows
     // that the slices' 64-bit atomics accumulate into
     const unsigned tiles = (unsigned)(jpad / 64) * (unsigned)(cpad / 64);
     unsigned split = 1;
-    if (tiles < 128) split = (unsigned)std::min<size_t>((2048 + tiles - 1) / tiles, mpad / 64);
+    static const unsigned target = [] {  // TFHE_MI355_KS_SPLIT_WG: workgroups aimed at (A/B)
+        const char *e = std::getenv("TFHE_MI355_KS_SPLIT_WG");
+        const long v = e ? std::atol(e) : 0;
+        return v > 0 ? (unsigned)v : 1024u;
+    }();
+    if (tiles < 128) split = (unsigned)std::min<size_t>((target + tiles - 1) / tiles, mpad / 64);
     if (split < 2) split = 1;
     hipLaunchKernelGGL(ks_digits_kernel, dim3((unsigned)a.count * KS_DPARTS), dim3(256), 0, s, a, dig, rowsum, mpad,
                        split > 1 ? 1 : 0);
