@@ -178,7 +178,6 @@ __global__ void __launch_bounds__(256) ks_mfma_kernel(KeyswitchLaunch a, const i
     const size_t kbeg = kslice * blockIdx.z, kend = blockIdx.z + 1 == gridDim.z ? mpad : kbeg + kslice;
     // digit rows past the batch (the tile's padding) read as zero: no memset of the scratch
     const bool arow = c0 + r < a.count;
-#pragma unroll 4
     for (size_t k = kbeg; k < kend; k += 32) {
         const ks_v4i av = arow ? *reinterpret_cast<const ks_v4i *>(pa + k) : ks_v4i{0, 0, 0, 0};
 #pragma unroll
