@@ -183,8 +183,8 @@ struct TfheMi355Context {
         std::vector<std::thread> workers;
         struct Slot {
             hipStream_t stream = nullptr;
-            PinnedBuffer h_in, h_out, h_luts, h_idx;
-            DeviceBuffer d_in, d_out, d_luts, d_idx, d_scratch;
+            PinnedBuffer h_in, h_out;            // h_in / d_in: [LUT sets | input rows | LUT indexes]
+            DeviceBuffer d_in, d_out, d_scratch;
         } slots[9];  // 0-7: dispatchers; 8: direct calls (coalesced_call)
         bool direct_busy = false;  // slot 8 in use, under m
         // statistics (tfhe_mi355_coalesce_stats), under m
@@ -780,23 +780,15 @@ void run_coalesced_batch(TfheMi355Context *c, TfheMi355Context::Coalescer::Slot 
     // batch is at most `cap` rows (coalesce_max_count() <= cap, submit counts <= cap), the max()
     // keeps the copies below in bounds whatever the settings
     const size_t cap = std::max(coalesce_batch(), total), glwe = c->glwe_len();
-    sl.h_in.reserve(cap * d.in_words * 8);
     sl.h_out.reserve(cap * d.out_words * 8);
-    sl.d_in.reserve(cap * d.in_words * 8);
     sl.d_out.reserve(cap * d.out_words * 8);
     const size_t scratch = d.scratch(c, cap);
     if (scratch) sl.d_scratch.reserve(scratch);
     size_t rows = 0, sets = 0;
     std::vector<std::pair<const uint64_t *, size_t>> seen;  // LUT pointer -> first set index
     std::vector<size_t> seen_count;                           // its lut_count
-    uint32_t *hidx = nullptr;
-    if (d.lut) {
-        sl.h_idx.reserve(cap * 4);
-        sl.d_idx.reserve(cap * 4);
-        hidx = static_cast<uint32_t *>(sl.h_idx.ptr);
-    }
     std::vector<size_t> base(batch.size(), 0);
-    if (d.lut) {  // distinct LUT sets (by pointer) and their offsets, then one staging buffer for all
+    if (d.lut) {  // distinct LUT sets (by pointer) and their offsets
         for (size_t b = 0; b < batch.size(); b++) {
             const CoalescedReq *r = batch[b];
             base[b] = (size_t)-1;
@@ -809,28 +801,34 @@ void run_coalesced_batch(TfheMi355Context *c, TfheMi355Context::Coalescer::Slot 
                 sets += r->lut_count;
             }
         }
-        sl.h_luts.reserve(sets * glwe * 8);
-        for (size_t q = 0; q < seen.size(); q++)
-            std::memcpy(static_cast<uint64_t *>(sl.h_luts.ptr) + seen[q].second * glwe, seen[q].first,
-                        seen_count[q] * glwe * 8);
     }
+    // ONE host->device copy per batch: [LUT sets | input rows | per-row LUT indexes (> 1 set)] packed
+    // in the slot's pinned staging and its device twin (each copy is a DMA with its own ~10 us of
+    // setup: a one-ciphertext call paid three of them).  Capacity: a full batch of rows plus the
+    // sets seen so far, grown (rarely) on demand.
+    const size_t lut_bytes = d.lut ? sets * glwe * 8 : 0;
+    const size_t in_off = align256(lut_bytes), in_bytes = total * d.in_words * 8;
+    const bool with_idx = d.lut && sets > 1;
+    const size_t idx_off = align256(in_off + in_bytes), span = idx_off + (with_idx ? total * 4 : 0);
+    const size_t room = align256(lut_bytes) + align256(cap * d.in_words * 8) + cap * 4;
+    sl.h_in.reserve(std::max(span, room));
+    sl.d_in.reserve(std::max(span, room));
+    char *hs = static_cast<char *>(sl.h_in.ptr);
+    for (size_t q = 0; q < seen.size(); q++)
+        std::memcpy(hs + seen[q].second * glwe * 8, seen[q].first, seen_count[q] * glwe * 8);
+    uint32_t *hidx = reinterpret_cast<uint32_t *>(hs + idx_off);
     for (size_t b = 0; b < batch.size(); b++) {
         const CoalescedReq *r = batch[b];
-        std::memcpy(static_cast<uint64_t *>(sl.h_in.ptr) + rows * d.in_words, r->in, r->count * d.in_words * 8);
-        if (d.lut)
+        std::memcpy(hs + in_off + rows * d.in_words * 8, r->in, r->count * d.in_words * 8);
+        if (with_idx)
             for (size_t i = 0; i < r->count; i++) hidx[rows + i] = (uint32_t)(base[b] + (r->idx ? r->idx[i] : 0));
         rows += r->count;
     }
     const hipStream_t s = sl.stream;
-    check(hipMemcpyAsync(sl.d_in.ptr, sl.h_in.ptr, total * d.in_words * 8, hipMemcpyHostToDevice, s), "H2D batch");
-    if (d.lut) {
-        sl.d_luts.reserve(sets * glwe * 8);
-        check(hipMemcpyAsync(sl.d_luts.ptr, sl.h_luts.ptr, sets * glwe * 8, hipMemcpyHostToDevice, s), "H2D luts");
-        if (sets > 1)  // one LUT set: no per-row indexes (the launch below passes none)
-            check(hipMemcpyAsync(sl.d_idx.ptr, hidx, total * 4, hipMemcpyHostToDevice, s), "H2D idx");
-    }
-    d.launch(c, (const uint64_t *)sl.d_in.ptr, (uint64_t *)sl.d_out.ptr, (const uint64_t *)sl.d_luts.ptr,
-             d.lut ? sets : 0, d.lut && sets > 1 ? (const uint32_t *)sl.d_idx.ptr : nullptr, total,
+    check(hipMemcpyAsync(sl.d_in.ptr, sl.h_in.ptr, span, hipMemcpyHostToDevice, s), "H2D batch");
+    char *ds = static_cast<char *>(sl.d_in.ptr);
+    d.launch(c, (const uint64_t *)(ds + in_off), (uint64_t *)sl.d_out.ptr, (const uint64_t *)ds,
+             d.lut ? sets : 0, with_idx ? (const uint32_t *)(ds + idx_off) : nullptr, total,
              scratch ? sl.d_scratch.ptr : nullptr, scratch ? sl.d_scratch.bytes : 0, s);
     check(hipMemcpyAsync(sl.h_out.ptr, sl.d_out.ptr, total * d.out_words * 8, hipMemcpyDeviceToHost, s), "D2H batch");
     check(hipStreamSynchronize(s), "batch sync");
