@@ -14,7 +14,6 @@
 // from a [c-1][a] copy of the table (coalesced); sub-blocks W_M[16 x] through an LDS table (the
 // oracle's tstride-16 reads of the same table, so bit-identical).
 #include <cstdlib>
-#include <mutex>
 
 #include "engine.h"
 #include "pbs_common.h"
@@ -1446,25 +1445,6 @@ static bool split_fused_enabled() {
     return v;
 }
 
-// TFHE_MI355_SPLIT_LANES=2: the digits-fed CMUX on two streams (halves of the chunk), see below
-static int split_lanes() {
-    static const int v = [] {
-        const char *e = std::getenv("TFHE_MI355_SPLIT_LANES");
-        return e && e[0] ? std::atoi(e) : 1;
-    }();
-    return v;
-}
-// one non-blocking auxiliary stream per device for the second lane (created on first use, kept)
-static hipStream_t split_aux_stream() {
-    static std::mutex m;
-    static hipStream_t streams[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    std::lock_guard<std::mutex> g(m);
-    if (!streams[dev] && hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking) != hipSuccess) streams[dev] = nullptr;
-    return streams[dev];
-}
-
 // TFHE_MI355_PAIR_SUB=1: the classic split CMUX (L <= 2) through large_pair_sub_kernel too (A/B)
 static bool large_pair_sub_classic() {
     static const bool v = [] {
@@ -1522,62 +1502,29 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
         // sub-block workgroup costs more than the spectra it saves (2_5: 2005 vs 2191 KS+PBS/s)
         if constexpr (G == 0 && K == 1 && L == 2 && S::R <= 4) {
             if (large_dsub_enabled()) {  // digits-fed CMUX: digits, sub-blocks from digits, top_inv
+                constexpr int DPER = S::M / 256;
+                const unsigned dig_blocks = (unsigned)((cnt + 7) / 8) * 8 * DPER;
+                const unsigned dsub_blocks = (unsigned)((cnt + 7) / 8) * 8 * S::R;
+                const unsigned fused_blocks = (unsigned)((cnt + 7) / 8) * 8 * 2;  // (ct, row)
                 const bool fused = split_fused_enabled();
-                // CMUX i of the ciphertexts [lct0, lct0 + la.chunk_count) of the chunk on stream st
-                auto cmux = [&](const LargePbsLaunch &la, int lct0, hipStream_t st, int i) {
-                    const int lcnt = la.chunk_count;
-                    constexpr int DPER = S::M / 256;
-                    const unsigned dig_blocks = (unsigned)((lcnt + 7) / 8) * 8 * DPER;
-                    const unsigned dsub_blocks = (unsigned)((lcnt + 7) / 8) * 8 * S::R;
-                    const unsigned fused_blocks = (unsigned)((lcnt + 7) / 8) * 8 * 2;  // (ct, row)
-                    const unsigned ltop_blocks = (unsigned)lcnt * (K + 1) * (1024 / TOPT);
+                for (int i = 0; i < a.n; i++) {
                     if (i == 0 || !fused) {
-                        TimedLaunch tl(la.timer, "split_digits_kernel", st);
-                        hipLaunchKernelGGL((split_digits_kernel<N>), dim3(dig_blocks), dim3(256), 0, st, la, lct0, i);
+                        TimedLaunch tl(a.timer, "split_digits_kernel", s);
+                        hipLaunchKernelGGL((split_digits_kernel<N>), dim3(dig_blocks), dim3(256), 0, s, a, ct0, i);
                     }
                     {
-                        TimedLaunch tl(la.timer, "large_dsub_kernel", st);
-                        hipLaunchKernelGGL((large_dsub_kernel<N>), dim3(dsub_blocks), dim3(Sub::THREADS), Sub::LDS, st,
-                                           la, lct0, i);
+                        TimedLaunch tl(a.timer, "large_dsub_kernel", s);
+                        hipLaunchKernelGGL((large_dsub_kernel<N>), dim3(dsub_blocks), dim3(Sub::THREADS), Sub::LDS, s,
+                                           a, ct0, i);
                     }
-                    if (fused && i + 1 < la.n) {  // top_inv of CMUX i + digits of CMUX i + 1
-                        TimedLaunch tl(la.timer, "split_inv_digits_kernel", st);
+                    if (fused && i + 1 < a.n) {  // top_inv of CMUX i + digits of CMUX i + 1
+                        TimedLaunch tl(a.timer, "split_inv_digits_kernel", s);
                         hipLaunchKernelGGL((split_inv_digits_kernel<N>), dim3(fused_blocks), dim3(1024),
-                                           sizeof(acc_pair) * S::M, st, la, lct0, i);
-                        return;
+                                           sizeof(acc_pair) * S::M, s, a, ct0, i);
+                        continue;
                     }
-                    TimedLaunch tl(la.timer, "large_top_inv_kernel", st);
-                    hipLaunchKernelGGL((large_top_inv_kernel<N, K, G>), dim3(ltop_blocks), dim3(TOPT), 0, st, la, lct0, i);
-                };
-                // Two lanes (TFHE_MI355_SPLIT_LANES=2): the chunk's two halves on two streams, so one
-                // half's memory-bound split_inv_digits (64 KiB of LDS, 16 waves) runs beside the
-                // other half's compute-bound large_dsub (80 KiB, 4 waves) on the same CUs
-                hipStream_t aux = split_lanes() == 2 && cnt >= 16 ? split_aux_stream() : nullptr;
-                if (!aux) {
-                    for (int i = 0; i < a.n; i++) cmux(a, ct0, s, i);
-                } else {
-                    const int h = (cnt / 2 + 7) / 8 * 8;
-                    LargePbsLaunch la = a, lb = a;
-                    la.chunk_count = h;
-                    lb.chunk_count = cnt - h;
-                    lb.acc = a.acc + (size_t)h * (K + 1) * N;
-                    lb.spectra = a.spectra + (size_t)h * L * (K + 1) * S::M;
-                    hipEvent_t fork, join;
-                    hipError_t e = hipEventCreateWithFlags(&fork, hipEventDisableTiming);
-                    if (e != hipSuccess) return e;
-                    if ((e = hipEventCreateWithFlags(&join, hipEventDisableTiming)) != hipSuccess) return e;
-                    // the chunk's init (on s) before lane B's first kernel
-                    if ((e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(aux, fork, 0)) != hipSuccess)
-                        return e;
-                    for (int i = 0; i < a.n; i++) {
-                        cmux(la, ct0, s, i);
-                        cmux(lb, ct0 + h, aux, i);
-                    }
-                    // the extraction (on s) after lane B's last kernel
-                    if ((e = hipEventRecord(join, aux)) != hipSuccess || (e = hipStreamWaitEvent(s, join, 0)) != hipSuccess)
-                        return e;
-                    (void)hipEventDestroy(fork);  // released once the recorded work has completed
-                    (void)hipEventDestroy(join);
+                    TimedLaunch tl(a.timer, "large_top_inv_kernel", s);
+                    hipLaunchKernelGGL((large_top_inv_kernel<N, K, G>), dim3(top_blocks), dim3(TOPT), 0, s, a, ct0, i);
                 }
                 hipLaunchKernelGGL((large_extract_kernel<N, K>), dim3((unsigned)((out_elems + 255) / 256)), dim3(256),
                                    0, s, a, ct0, cnt);
