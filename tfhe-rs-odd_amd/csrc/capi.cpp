@@ -278,7 +278,9 @@ bool is_large(const TfheMi355Context *c) {
 
 // N >= 4096: ciphertexts per pass of the split CMUX.  The chunk's accumulators + spectra should
 // stay resident in the 256 MiB Infinity Cache: 128 at N = 32768 (1.5 MiB per ciphertext at 4_4,
-// best of 64..1024 measured), otherwise ~160 MiB worth in multiples of 64 (64..1024).
+// best of 64..1024 measured), otherwise ~200 MiB of scratch in multiples of 64 (64..1024) --
+// round 4 sweeps (profiles/r04_chunk_sweep.log): 3_3 384 / 512 / 768 -> 5.94k / 6.17k / 5.55k,
+// 2_5 192 / 256 -> 2268 / 2307, 1_4 832 / 1024 -> 13.5k / 14.3k KS+PBS/s (160 MiB gave 384 / 192 / 832).
 size_t large_chunk(const TfheMi355Context *c) {
     static const size_t forced = [] {
         const char *e = std::getenv("TFHE_MI355_LARGE_CHUNK");
@@ -288,7 +290,7 @@ size_t large_chunk(const TfheMi355Context *c) {
     if (forced) return forced;
     if (c->N() >= 32768) return 128;
     const size_t per = large_pbs_scratch_per_ct((int)c->N(), (int)c->k(), (int)c->p.pbs_level);
-    return std::min<size_t>(1024, std::max<size_t>(64, ((size_t)160 << 20) / per / 64 * 64));
+    return std::min<size_t>(1024, std::max<size_t>(64, ((size_t)200 << 20) / per / 64 * 64));
 }
 
 size_t pbs_scratch_bytes(const TfheMi355Context *c, size_t count) {
