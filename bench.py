@@ -286,7 +286,7 @@ def split_chunk(p, units: int) -> int:
         return min(units, 128)
     M, k1 = p.polynomial_size // 2, p.glwe_dimension + 1
     per = k1 * p.polynomial_size * 8 + p.pbs_level * k1 * M * 16
-    return min(units, min(1024, max(64, (160 << 20) // per // 64 * 64)))
+    return min(units, min(1024, max(64, (200 << 20) // per // 64 * 64)))
 
 
 def large_memory_model(p):
