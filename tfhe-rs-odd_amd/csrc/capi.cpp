@@ -13,6 +13,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <atomic>
 #include <shared_mutex>
 #include <stdexcept>
 #include <string>
@@ -123,6 +124,11 @@ struct CoalescedReq {
     const uint32_t *idx;
     size_t count;
     bool sync = false;  // a blocking caller (coalesced_call), not a submitted request
+    // blocking callers copy their own rows out of the slot's pinned staging once woken (in parallel
+    // instead of one after the other on the dispatcher), then release the slot (pending)
+    const uint64_t *src = nullptr;
+    size_t src_bytes = 0;
+    std::atomic<int> *pending = nullptr;
     // completion: set by the dispatcher, waited on by the caller alone (no shared mutex, so a
     // finished batch wakes its callers without a thundering herd on the queue lock)
     std::mutex m;
@@ -185,6 +191,7 @@ struct TfheMi355Context {
             hipStream_t stream = nullptr;
             PinnedBuffer h_in, h_out;            // h_in / d_in: [LUT sets | input rows | LUT indexes]
             DeviceBuffer d_in, d_out, d_scratch;
+            std::atomic<int> copies{0};          // callers of the last batch still copying out of h_out
         } slots[9];  // 0-7: dispatchers; 8: direct calls (coalesced_call)
         bool direct_busy = false;  // slot 8 in use, under m
         // statistics (tfhe_mi355_coalesce_stats), under m
@@ -776,6 +783,8 @@ void run_coalesced_batch(TfheMi355Context *c, TfheMi355Context::Coalescer::Slot 
     check(hipSetDevice(c->device), "hipSetDevice");
     const CoalescedOpDesc d = coalesced_op(c, op);
     if (!sl.stream) check(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking), "hipStreamCreate(slot)");
+    // the previous batch's blocking callers copy their rows out of h_out themselves (a few us each)
+    while (sl.copies.load(std::memory_order_acquire) != 0) std::this_thread::yield();
     size_t total = 0;
     for (auto *r : batch) total += r->count;
     // sized for a full batch once (no hipFree between batches: it would wait for the device); a
@@ -835,10 +844,20 @@ void run_coalesced_batch(TfheMi355Context *c, TfheMi355Context::Coalescer::Slot 
     check(hipMemcpyAsync(sl.h_out.ptr, sl.d_out.ptr, total * d.out_words * 8, hipMemcpyDeviceToHost, s), "D2H batch");
     check(hipStreamSynchronize(s), "batch sync");
     rows = 0;
+    int deferred = 0;
     for (auto *r : batch) {
-        std::memcpy(r->out, static_cast<uint64_t *>(sl.h_out.ptr) + rows * d.out_words, r->count * d.out_words * 8);
+        const uint64_t *src = static_cast<uint64_t *>(sl.h_out.ptr) + rows * d.out_words;
+        if (r->sync) {  // copied by its caller after the wake-up (coalesce_wait)
+            r->src = src;
+            r->src_bytes = r->count * d.out_words * 8;
+            r->pending = &sl.copies;
+            deferred++;
+        } else {
+            std::memcpy(r->out, src, r->count * d.out_words * 8);
+        }
         rows += r->count;
     }
+    sl.copies.store(deferred, std::memory_order_release);  // before any caller is woken
 }
 
 // dispatcher of batch slot q: waits for queued work, lets the window fill the batch, takes the
@@ -949,8 +968,14 @@ void coalesce_enqueue(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
 }
 
 void coalesce_wait(CoalescedReq &r) {
-    std::unique_lock<std::mutex> lk(r.m);
-    r.cv.wait(lk, [&] { return r.done; });
+    {
+        std::unique_lock<std::mutex> lk(r.m);
+        r.cv.wait(lk, [&] { return r.done; });
+    }
+    if (r.pending) {  // this caller's rows are in the slot's staging: copy them, release the slot
+        std::memcpy(r.out, r.src, r.src_bytes);
+        r.pending->fetch_sub(1, std::memory_order_release);
+    }
     if (!r.err.empty()) fail("%s", r.err.c_str());
 }
 
@@ -1209,6 +1234,8 @@ int tfhe_mi355_context_destroy(TfheMi355Context *ctx) {
             x->done = true;
             x->cv.notify_one();
         }
+        for (auto &sl : ctx->co.slots)  // woken callers still copying their rows out of the staging
+            while (sl.copies.load(std::memory_order_acquire) != 0) std::this_thread::yield();
         for (auto &sl : ctx->co.slots)
             if (sl.stream) {
                 (void)hipStreamSynchronize(sl.stream);
