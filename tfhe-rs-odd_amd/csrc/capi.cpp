@@ -129,10 +129,6 @@ struct CoalescedReq {
     const uint64_t *src = nullptr;
     size_t src_bytes = 0;
     std::atomic<int> *pending = nullptr;
-    // blocking callers of one batch are woken as a binary tree: the dispatcher wakes the first,
-    // each woken caller wakes its two children before anything else (log2 depth instead of one
-    // futex wake after another on the dispatcher)
-    CoalescedReq *kid[2] = {nullptr, nullptr};
     // completion: set by the dispatcher, waited on by the caller alone (no shared mutex, so a
     // finished batch wakes its callers without a thundering herd on the queue lock)
     std::mutex m;
@@ -938,24 +934,11 @@ void coalesce_dispatcher(TfheMi355Context *c, size_t q) {
             err = ex.what();
         }
         const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        std::vector<CoalescedReq *> syncs;
         for (auto *x : batch) {  // notified under its lock: the caller may free x as soon as it wakes
-            if (x->sync) {
-                syncs.push_back(x);
-                continue;
-            }
             std::lock_guard<std::mutex> g(x->m);
             x->err = err;
             x->done = true;
             x->cv.notify_one();
-        }
-        for (size_t q = 0; q < syncs.size(); q++)  // read by each parent after its own wake-up
-            for (size_t k = 0; k < 2; k++) syncs[q]->kid[k] = 2 * q + 1 + k < syncs.size() ? syncs[2 * q + 1 + k] : nullptr;
-        if (!syncs.empty()) {
-            std::lock_guard<std::mutex> g(syncs[0]->m);
-            syncs[0]->err = err;
-            syncs[0]->done = true;
-            syncs[0]->cv.notify_one();
         }
         {  // the slot counts as busy until its callers are all woken, so the next batch's window
            // (on whichever slot) starts after they have had the chance to queue again
@@ -985,20 +968,10 @@ void coalesce_enqueue(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
 }
 
 void coalesce_wait(CoalescedReq &r) {
-    CoalescedReq *kid[2];
     {
         std::unique_lock<std::mutex> lk(r.m);
         r.cv.wait(lk, [&] { return r.done; });
-        kid[0] = r.kid[0];
-        kid[1] = r.kid[1];
     }
-    for (CoalescedReq *k : kid)  // the wake-up tree: children first (they wait on their own cv)
-        if (k) {
-            std::lock_guard<std::mutex> g(k->m);
-            k->err = r.err;
-            k->done = true;
-            k->cv.notify_one();
-        }
     if (r.pending) {  // this caller's rows are in the slot's staging: copy them, release the slot
         std::memcpy(r.out, r.src, r.src_bytes);
         r.pending->fetch_sub(1, std::memory_order_release);
