@@ -995,7 +995,10 @@ void coalesced_call(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
     bool direct = false;
     if (coalesce_direct()) {
         std::lock_guard<std::mutex> g(co.m);
-        bool idle = !co.stop && !co.direct_busy && co.in_flight == 0;
+        // ... and only while this entry point's traffic is one blocking caller at a time (its last
+        // dispatcher batch had at most one blocking row): with several callers a direct call would
+        // split their batch in two
+        bool idle = !co.stop && !co.direct_busy && co.in_flight == 0 && co.last_sync_rows[op] <= 1;
         for (int o = 0; o < CO_OPS && idle; o++) idle = co.queue[o].empty();
         if (idle) co.direct_busy = direct = true;
     }
@@ -1017,6 +1020,7 @@ void coalesced_call(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
     {
         std::lock_guard<std::mutex> g(co.m);
         co.direct_busy = false;
+        co.last_sync_rows[op] = 1;
         co.batches++;
         co.rows += r.count;
         co.batch_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
