@@ -1020,7 +1020,6 @@ void coalesced_call(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
     {
         std::lock_guard<std::mutex> g(co.m);
         co.direct_busy = false;
-        co.last_sync_rows[op] = 1;
         co.batches++;
         co.rows += r.count;
         co.batch_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
