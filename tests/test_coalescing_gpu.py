@@ -72,6 +72,33 @@ def test_16_threads_x_64_single_ciphertext_ks_pbs_bit_exact(orc, keys_2_2, eng):
         assert np.array_equal(dec, [fs[a](m) for m in msgs[rows]])
 
 
+def test_lone_caller_runs_directly_and_exactly(orc, keys_2_2):
+    """One blocking caller at a time on a fresh context: every call runs at once on the calling
+    thread (capi.cpp coalesced_call: a batch of its own, never counted in flight), with the same
+    rows as the oracle; KS+PBS with two LUTs and a per-row index through the same path."""
+    from tfhe_mi355 import Engine
+
+    p = keys_2_2.params
+    e = Engine(p, 0)
+    e.upload_bootstrap_key(keys_2_2.bsk)
+    e.upload_keyswitch_key(keys_2_2.ksk)
+    accs = np.stack([orc.fill_accumulator(2048, 1, 4, 4, lambda x: (x + 3) % 16),
+                     orc.fill_accumulator(2048, 1, 4, 4, lambda x: (5 * x) % 16)])
+    msgs = np.arange(6) % 16
+    big = orc.lwe_encrypt(905, keys_2_2.glwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta),
+                          p.glwe_modular_std_dev)
+    small = orc.keyswitch(keys_2_2.ksk, p.big_lwe_dimension, p.lwe_dimension, p.ks_base_log, p.ks_level, big)
+    e.coalesce_stats(reset=True)
+    for i in range(6):
+        idx = np.array([i % 2], dtype=np.uint32)
+        got = e.keyswitch_programmable_bootstrap(big[i:i + 1], accs, lut_indexes=idx)
+        assert np.array_equal(got, keys_2_2.fbsk.pbs(small[i:i + 1], accs[i % 2], threads=1))
+        got = e.programmable_bootstrap(small[i:i + 1], accs[0])
+        assert np.array_equal(got, keys_2_2.fbsk.pbs(small[i:i + 1], accs[0], threads=1))
+    st = e.coalesce_stats()
+    assert st["batches"] == 12 and st["rows"] == 12 and st["max_in_flight"] == 0, st
+
+
 def test_mixed_ops_counts_and_lut_indexes_coalesce_exactly(orc, keys_2_2, eng):
     """Concurrent PBS, KS+PBS and KS calls of 1-5 ciphertexts, some with two LUTs and per-row
     indexes: each result equals the oracle's result of the same call made alone."""
