@@ -27,8 +27,14 @@
 //     C2' = lrow + 4 (col >> 2), positions 4 t + e, e < 4;
 //   the inverse mirrors it; the stage-3 inverse output goes back to stage-2 lanes through this
 //     wave's own quarter of X (wave-private, no barrier).
-// Four workgroup barriers per CMUX: accumulator -> rotation gather, stage 1 -> 2, stage 2 -> MAC,
-// inverse stage 2 -> 1.
+// That mapping (LAT_MAP = 0) has four workgroup barriers per CMUX: accumulator -> rotation gather,
+// stage 1 -> 2, stage 2 -> MAC, inverse stage 2 -> 1.  LAT_MAP = 1 (default) gives wave w the
+// stage-1 butterflies a = w + 4 col instead, so stage 2's butterfly a2 = w of EVERY block cc =
+// col reads only this wave's stage-1 outputs (positions = w mod 4): stages 1 <-> 2 are wave-private
+// both ways and the cross-wave hand-offs are stage 2 <-> 3, which the MAC's row join needs anyway.
+// Three barriers: accumulator -> rotation (A), stage 2 -> MAC (C), inverse stage 3 -> 2 (E); the
+// accumulator pairs move to their own buffer Z so one wave's rotation gather may overlap another's
+// stage-2 stores.  Same operations on the same values, so the outputs are unchanged.
 #include "engine.h"
 #include "pbs_common.h"
 
@@ -37,13 +43,19 @@ namespace tfhe_mi355 {
 namespace {
 
 constexpr int LAT_N = 2048, LAT_M = 1024;
+#ifndef LAT_MAP
+#define LAT_MAP 1  // lane mapping of the transform stages (see the header: 1 = three barriers per CMUX)
+#endif
 // LDS layout in double2 units: per GLWE row an exchange buffer X (stages 1/2) and a buffer Y
-// (stage-2 outputs, and the accumulator pairs of the rotation).  The twiddles and the twist a lane
-// needs are 12 constants per lane, kept in registers (read once from the global tables).
+// (stage-2 outputs; LAT_MAP = 0: also the accumulator pairs of the rotation).  LAT_MAP = 1 keeps
+// the pairs in their own buffer Z: the rotation gather of one wave can then overlap another wave's
+// stage-2 stores, with no barrier between them.  The twiddles and the twist a lane needs are 12
+// constants per lane, kept in registers (read once from the global tables).
 struct LatLds {
     static constexpr int X = 0;
     static constexpr int Y = X + 2 * LAT_M;
-    static constexpr int end = Y + 2 * LAT_M;
+    static constexpr int Z = LAT_MAP ? Y + 2 * LAT_M : Y;
+    static constexpr int end = Z + 2 * LAT_M;
     static constexpr size_t bytes = sizeof(double2) * end;
 };
 static_assert(LatLds::bytes <= 160 * 1024, "latency PBS LDS exceeds a CU");
@@ -53,17 +65,34 @@ __device__ __forceinline__ cx ld2(const double2 *p) {
     return {t.x, t.y};
 }
 __device__ __forceinline__ void st2(double2 *p, cx v) { *p = make_double2(v.re, v.im); }
-// X / Y slot of FFT position P: an XOR swizzle of the 16-byte slot's bank bits (0-3) by bits 4, 6
-// and 7, found by exhaustive search over the linear swizzles of bits 4-7 to make all three access
-// patterns of a wave (stage-1 a1 + 64 C, stage-2 64 cc + a2 + 4 C2, the MAC's blocks 4 t + e) free
-// of bank conflicts for both ds_read_b128 lane groups and ds_write_b128's (the plain layout puts
-// up to 4 lanes of a group on one bank).  LAT_SWZ=0: plain.
+// X / Y slot of FFT position P: an XOR swizzle of the 16-byte slot's bank bits (0-3), found by
+// exhaustive search to make all three access patterns of a wave free of bank conflicts for both
+// ds_read_b128 lane groups and ds_write_b128's (the plain layout puts up to 4 lanes of a group on
+// one bank).  LAT_MAP = 0 (stage 1 a1 + 64 C, a1 = 16 w + col; stage 2 64 cc + a2 + 4 C2; the
+// MAC's blocks 4 t + e): bits 0-3 ^= bits 4, 7, 6, 6 (linear swizzles of bits 4-7).  LAT_MAP = 1
+// (a1 = w + 4 col, cc = col, a2 = w; same blocks): no XOR of bits 4-9 into bits 0-3 works (the
+// stage-1 stores of 8 contiguous lanes differ in bit 3), so bits 0-2 ^= bits 3, 4, 6, 7, 8 ->
+// 1, 0, 2, 1, 0 and bit 3 ^= bit 6 (scripts/probes/lat_swizzle_search.c: 712,704 such maps
+// qualify among the 2^27 with bit 3 as an input).  LAT_SWZ=0: plain.
 #ifndef LAT_SWZ
 #define LAT_SWZ 1
 #endif
 __device__ __forceinline__ int lswz(int P) {
-    return LAT_SWZ ? P ^ (((P >> 4) & 1) | ((P >> 6) & 2) | ((P >> 4) & 4) | ((P >> 3) & 8)) : P;
+    if (!LAT_SWZ) return P;
+    if (LAT_MAP)
+        return P ^ (((P >> 2) & 2) ^ ((P >> 4) & 1) ^ ((P >> 4) & 4) ^ ((P >> 6) & 2) ^ ((P >> 8) & 1) ^ ((P >> 3) & 8));
+    return P ^ (((P >> 4) & 1) | ((P >> 6) & 2) | ((P >> 4) & 4) | ((P >> 3) & 8));
 }
+// Slot of accumulator pair j (acc[j], acc[j + M]) in its buffer.  LAT_MAP = 1: a lane's pairs are
+// j = w + 4 col + 64 (lrow + 4 q), so the stores of 8 contiguous lanes and the rotation gather
+// (pairs j - rem: in a 16-lane read group bits 2-5 take all 16 values, bits 0-1 are fixed) would
+// share banks; bits 0-1 ^= (bit 3 ^ bit 5, bit 4) makes both conflict-free for every rem.
+// Lane mapping of the transform stages (lane = 16 lrow + col, w = the wave's quarter of its row):
+// stage-1 butterfly a1, stage-2 block cc and butterfly a2
+__device__ __forceinline__ int lat_a1(int w, int col) { return LAT_MAP ? w + 4 * col : 16 * w + col; }
+__device__ __forceinline__ int lat_cc(int w, int col) { return LAT_MAP ? col : 4 * w + (col >> 2); }
+__device__ __forceinline__ int lat_a2(int w, int col) { return LAT_MAP ? w : col & 3; }
+__device__ __forceinline__ int aswz(int j) { return LAT_MAP ? j ^ ((((j >> 3) ^ (j >> 5)) & 1) | ((j >> 3) & 2)) : j; }
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations (lgkmcnt), not
 // for its global loads, so the GGSW prefetch stays in flight across it (__syncthreads' fence
 // would wait for vmcnt(0) too and expose the prefetch's latency at the first barrier).
@@ -207,6 +236,7 @@ template <int RPW>
 __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(ClassicPbsLaunch a) {
     constexpr int N = LAT_N, M = LAT_M, K = 1, LOG2N = 11;
     static_assert(RPW == 1 || RPW == 2, "one or both GLWE rows per wave");
+    static_assert(!LAT_MAP || RPW == 1, "the three-barrier lane mapping is written for one row per wave");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double2 *lds = reinterpret_cast<double2 *>(smem);
     const int tid = threadIdx.x;
@@ -222,7 +252,7 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
     const RowTw rtw(lane0 >> 4);
     const RowTwF rtf(lane0 >> 4, false), rti(lane0 >> 4, true);  // LAT_BF = 2
     {
-        const int lrow = lane0 >> 4, col = lane0 & 15, a1 = 16 * w + col, a2 = col & 3;
+        const int lrow = lane0 >> 4, col = lane0 & 15, a1 = lat_a1(w, col), a2 = lat_a2(w, col);
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const int C = lrow + 4 * q;
@@ -252,7 +282,7 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
             const uint64_t *lut = a.luts + (size_t)li * (K + 1) * N + (size_t)(row0 + r) * N;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const int j = 16 * w + (lane0 & 15) + 64 * (lane0 >> 4) + 256 * q;
+                const int j = lat_a1(w, lane0 & 15) + 64 * (lane0 >> 4) + 256 * q;
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
                     const int src = j + h * M + rem;
@@ -268,7 +298,7 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
     // (acc[p], acc[p + M]) live in Y between CMUXes (its stage-2 outputs are dead then)
     auto Xr = [&](int r) { return lds + LatLds::X + (row0 + r) * M; };
     auto Yr = [&](int r) { return lds + LatLds::Y + (row0 + r) * M; };
-    auto Ar = [&](int r) { return reinterpret_cast<uint64_t *>(Yr(r)); };
+    auto Ar = [&](int r) { return reinterpret_cast<uint64_t *>(lds + LatLds::Z + (row0 + r) * M); };
     constexpr size_t ggsw_stride = (size_t)(K + 1) * (K + 1) * M;
     const double k32 = torus_k32();
 
@@ -327,13 +357,14 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
 
         // ---- accumulator -> LDS pairs, rotation gather, ct1 = X^at acc - acc, digits, twist ----
         // (LAT_EARLYACC: the pairs were stored by the previous CMUX's backward conversion, or before
-        // the loop; Y is free then -- its last reads were the MAC's, before barrier D)
+        // the loop; the pair buffer is free then -- LAT_MAP = 0: Y, whose last reads were the MAC's,
+        // before barrier D; LAT_MAP = 1: Z, whose last reads were the rotation's, before barrier C)
         if (!LAT_EARLYACC || i == 0) {
 #pragma unroll
             for (int r = 0; r < RPW; r++)
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
-                    const int j = 16 * w + col + 64 * lrow + 256 * q;
+                    const int j = aswz(lat_a1(w, col) + 64 * lrow + 256 * q);
                     Ar(r)[2 * j] = lo[r][q];
                     Ar(r)[2 * j + 1] = hi[r][q];
                 }
@@ -345,12 +376,12 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
         for (int r = 0; r < RPW; r++)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const int j = 16 * w + col + 64 * lrow + 256 * q;
+                const int j = lat_a1(w, col) + 64 * lrow + 256 * q;
                 // (X^rem p) at j and j + M from ONE pair: u = j - rem, s = u mod M; u >= 0: (lo, hi);
                 // -M <= u < 0: (-hi, lo) (X^M acts as i on the fold); u < -M: (-lo, -hi)
                 const int u = j - rem;
                 const int s = u & (M - 1);
-                const uint64_t plo = Ar(r)[2 * s], phi = Ar(r)[2 * s + 1];
+                const uint64_t plo = Ar(r)[2 * aswz(s)], phi = Ar(r)[2 * aswz(s) + 1];
                 const bool swap = u < 0 && u >= -M;
                 const bool n0 = (u < 0) != full_odd, n1 = (u < -M) != full_odd;
                 const uint64_t x0 = swap ? phi : plo, x1 = swap ? plo : phi;
@@ -367,7 +398,7 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
             if constexpr (LAT_BF == 2) dft16_fwd_rows_sf(v[r], rtf);
             else if (LAT_BF) dft16_fwd_rows_bf(v[r], rtw);
             else dft16_fwd_rows(v[r], lrow);
-            const int a1 = 16 * w + col;
+            const int a1 = lat_a1(w, col);
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const int C = lrow + 4 * q;
@@ -375,11 +406,14 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
             }
         }
         stamp(i, 3);
-        lds_barrier();  // (B)
+        // (B) LAT_MAP = 0: stage 2 reads other waves' stage-1 outputs; LAT_MAP = 1: only this wave's
+        if constexpr (LAT_MAP) WaveLocalSync{}();
+        else lds_barrier();
         stamp(i, 4);
-        // ---- forward stage 2: block cc = 4 w + (col >> 2), butterfly a2 = col & 3 ----
+        // ---- forward stage 2: block cc, butterfly a2 (LAT_MAP = 0: cc = 4 w + (col >> 2),
+        //      a2 = col & 3; LAT_MAP = 1: cc = col, a2 = w) ----
         {
-            const int cc = 4 * w + (col >> 2), a2 = col & 3;
+            const int cc = lat_cc(w, col), a2 = lat_a2(w, col);
 #pragma unroll
             for (int r = 0; r < RPW; r++) {
 #pragma unroll
@@ -441,9 +475,12 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
             for (int e = 0; e < 4; e++)
                 if (!(LAT_TSKIP & 1)) st2(Xr(c) + lswz(tb + e), o[c][e]);
         }
-        if (!(LAT_TSKIP & 1)) WaveLocalSync{}();
+        // LAT_MAP = 0: the blocks are this wave's own stage-2 blocks (wave-private); LAT_MAP = 1:
+        // stage 2 reads one residue class mod 4 of every block, written by all four waves (E)
+        if constexpr (LAT_MAP) lds_barrier();
+        else if (!(LAT_TSKIP & 1)) WaveLocalSync{}();
         {
-            const int cc = 4 * w + (col >> 2), a2 = col & 3;
+            const int cc = lat_cc(w, col), a2 = lat_a2(w, col);
 #pragma unroll
             for (int r = 0; r < RPW; r++) {
 #pragma unroll
@@ -464,11 +501,13 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
                 for (int q = 0; q < 4; q++) st2(Xr(r) + lswz(64 * cc + a2 + 4 * (lrow + 4 * q)), v[r][q]);
         }
         stamp(i, 8);
-        lds_barrier();  // (D)
+        // (D) LAT_MAP = 0: stage 1 reads other waves' stage-2 outputs; LAT_MAP = 1: only this wave's
+        if constexpr (LAT_MAP) WaveLocalSync{}();
+        else lds_barrier();
         stamp(i, 9);
         // ---- inverse stage 1 + backward conversion into the accumulator ----
         {
-            const int a1 = 16 * w + col;
+            const int a1 = lat_a1(w, col);
 #pragma unroll
             for (int r = 0; r < RPW; r++) {
 #pragma unroll
@@ -483,7 +522,7 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
                 for (int q = 0; q < 4; q++) {
                     backward_add(v[r][q], tws[q], lo[r][q], hi[r][q], k32);  // the resident key carries the 1/M
                     if constexpr (LAT_EARLYACC) {  // the next rotation's pair, stored as soon as it is final
-                        const int j = 16 * w + col + 64 * lrow + 256 * q;
+                        const int j = aswz(lat_a1(w, col) + 64 * lrow + 256 * q);
                         Ar(r)[2 * j] = lo[r][q];
                         Ar(r)[2 * j + 1] = hi[r][q];
                     }
@@ -501,7 +540,7 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
             uint64_t *g = a.lwe_out + ((size_t)ct * (K + 1) + row0 + r) * N;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const int j = 16 * w + col + 64 * lrow + 256 * q;
+                const int j = lat_a1(w, col) + 64 * lrow + 256 * q;
                 g[j] = lo[r][q];
                 g[j + M] = hi[r][q];
             }
@@ -514,24 +553,24 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
     for (int r = 0; r < RPW; r++)
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            const int j = 16 * w + col + 64 * lrow + 256 * q;
+            const int j = aswz(lat_a1(w, col) + 64 * lrow + 256 * q);
             Ar(r)[2 * j] = lo[r][q];
             Ar(r)[2 * j + 1] = hi[r][q];
         }
     __syncthreads();
     uint64_t *out = a.lwe_out + (size_t)ct * (K * N + 1);
-    const uint64_t *A0 = reinterpret_cast<const uint64_t *>(lds + LatLds::Y);  // row 0 (K = 1)
+    const uint64_t *A0 = reinterpret_cast<const uint64_t *>(lds + LatLds::Z);  // row 0 (K = 1)
     for (int j = tid; j < N; j += (int)blockDim.x) {
         uint64_t x;
         if (j == 0) {
             x = A0[0];
         } else {
             const int src = N - j;  // acc0[src]: pair (src mod M), lo below M, hi above
-            x = 0 - A0[2 * (src & (M - 1)) + (src >= M)];
+            x = 0 - A0[2 * aswz(src & (M - 1)) + (src >= M)];
         }
         out[j] = x;
     }
-    if (tid == 0) out[K * N] = reinterpret_cast<const uint64_t *>(lds + LatLds::Y + K * M)[0];
+    if (tid == 0) out[K * N] = reinterpret_cast<const uint64_t *>(lds + LatLds::Z + K * M)[0];
 }
 
 bool latency_pbs_supported(int N, int k, int L) { return N == 2048 && k == 1 && L == 1; }
