@@ -27,7 +27,7 @@
  *     the same entry point are coalesced into shared batches that a dispatcher thread of the
  *     context runs on its own stream, each caller blocking until its own rows are written
  *     (a batch closes when no call has arrived for TFHE_MI355_COALESCE_GAP_US = 50, after at most
- *     _WINDOW_US = 500, at _BATCH = 1024 ciphertexts, or -- blocking callers only -- as soon as
+ *     _WINDOW_US = 1000, at _BATCH = 1024 ciphertexts, or -- blocking callers only -- as soon as
  *     as many rows are queued as the previous batch of the entry point had; _SLOTS, _OVERFLOW: a
  *     second batch runs concurrently only when half a batch is queued; a call that finds the
  *     coalescer idle runs at once on the calling thread, TFHE_MI355_COALESCE_DIRECT=0 turns that

@@ -711,7 +711,7 @@ void chunk_pks(TfheMi355Context *c, const uint64_t *i, uint64_t *o, const uint64
 // Calls of at most coalesce_max_count() ciphertexts (default 64; TFHE_MI355_COALESCE_MAX_COUNT,
 // 0 = off) are coalesced: up to coalesce_batch() ciphertexts (default 1024, one ciphertext per PBS
 // slot of the chip at 2_2) gathered until no call has arrived for coalesce_gap() (default 50 us),
-// for at most coalesce_window() (default 500 us) from the first queued call.  Both are small next
+// for at most coalesce_window() (default 1000 us) from the first queued call.  Both are small next
 // to a PBS (milliseconds), and a full batch leaves at once.
 size_t env_size(const char *name, size_t dflt) {
     const char *e = std::getenv(name);
@@ -750,7 +750,7 @@ size_t coalesce_overflow() {
     return v;
 }
 std::chrono::microseconds coalesce_window() {
-    static const size_t v = env_size("TFHE_MI355_COALESCE_WINDOW_US", 500);
+    static const size_t v = env_size("TFHE_MI355_COALESCE_WINDOW_US", 1000);
     return std::chrono::microseconds(v);
 }
 // the batch also closes once no request of its op has arrived for this long: callers woken one by
