@@ -83,15 +83,15 @@ __device__ __forceinline__ int lswz(int P) {
         return P ^ (((P >> 2) & 2) ^ ((P >> 4) & 1) ^ ((P >> 4) & 4) ^ ((P >> 6) & 2) ^ ((P >> 8) & 1) ^ ((P >> 3) & 8));
     return P ^ (((P >> 4) & 1) | ((P >> 6) & 2) | ((P >> 4) & 4) | ((P >> 3) & 8));
 }
-// Slot of accumulator pair j (acc[j], acc[j + M]) in its buffer.  LAT_MAP = 1: a lane's pairs are
-// j = w + 4 col + 64 (lrow + 4 q), so the stores of 8 contiguous lanes and the rotation gather
-// (pairs j - rem: in a 16-lane read group bits 2-5 take all 16 values, bits 0-1 are fixed) would
-// share banks; bits 0-1 ^= (bit 3 ^ bit 5, bit 4) makes both conflict-free for every rem.
 // Lane mapping of the transform stages (lane = 16 lrow + col, w = the wave's quarter of its row):
 // stage-1 butterfly a1, stage-2 block cc and butterfly a2
 __device__ __forceinline__ int lat_a1(int w, int col) { return LAT_MAP ? w + 4 * col : 16 * w + col; }
 __device__ __forceinline__ int lat_cc(int w, int col) { return LAT_MAP ? col : 4 * w + (col >> 2); }
 __device__ __forceinline__ int lat_a2(int w, int col) { return LAT_MAP ? w : col & 3; }
+// Slot of accumulator pair j (acc[j], acc[j + M]) in its buffer.  LAT_MAP = 1: a lane's pairs are
+// j = w + 4 col + 64 (lrow + 4 q), so the stores of 8 contiguous lanes and the rotation gather
+// (pairs j - rem: in a 16-lane read group bits 2-5 take all 16 values, bits 0-1 are fixed) would
+// share banks; bits 0-1 ^= (bit 3 ^ bit 5, bit 4) makes both conflict-free for every rem.
 __device__ __forceinline__ int aswz(int j) { return LAT_MAP ? j ^ ((((j >> 3) ^ (j >> 5)) & 1) | ((j >> 3) & 2)) : j; }
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations (lgkmcnt), not
 // for its global loads, so the GGSW prefetch stays in flight across it (__syncthreads' fence
@@ -576,7 +576,7 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
 bool latency_pbs_supported(int N, int k, int L) { return N == 2048 && k == 1 && L == 1; }
 
 #ifndef LAT_RPW
-#define LAT_RPW 1  // GLWE rows per wave (1: 8 waves per ciphertext, 2: 4 waves)
+#define LAT_RPW 1  // GLWE rows per wave (1: 8 waves per ciphertext, 2: 4 waves; 2 needs LAT_MAP=0)
 #endif
 
 hipError_t launch_latency_pbs(const ClassicPbsLaunch &a, hipStream_t s) {
