@@ -2,7 +2,8 @@
 csrc/pbs_multibit.hip).  A monomial read of lane l fetches entry r = t mod M of t = d (1 - 4 f) mod
 2N, f the lane's frequency slot; ds_read_b64 serves 32-lane groups, bank pair = position mod 32.
 Cost = mean over every d and slot of the largest number of distinct entries on one bank.
-Usage: python twist_swizzle_search.py SEED ITERATIONS  (random linear maps of bits 5-9)."""
+Usage: python twist_swizzle_search.py SEED ITERATIONS [shiftmask]  (random linear maps of bits 5-9;
+with "shiftmask" also every r ^ ((r >> k) & m), about 15 CPU-minutes)."""
 import numpy as np, itertools, sys
 M=1024
 lane=np.arange(64)
@@ -50,3 +51,10 @@ for it in range(int(sys.argv[2]) if len(sys.argv)>2 else 300):
     c=cost(mk(A))
     if c[0]<best[0]: best=(c[0],A.tolist(),c); print(it, c, A.tolist(), flush=True)
 print("best", best)
+
+# Round 4, the shipped family: position r ^ ((r >> k) & m), the same two instructions as the
+# round-3 swizzle (k = 5, m = 31) for every k and 10-bit m.  Best: k = 4, m = 23 -> 2.09, worst 4.
+if len(sys.argv) > 3 and sys.argv[3] == "shiftmask":
+    res = sorted((cost(lambda rr, k=k, m=m: rr ^ ((rr >> k) & m)), k, m) for k in range(1, 11) for m in range(1, 1024))
+    for c, k, m in res[:10]:
+        print("k", k, "m", m, c)
