@@ -39,6 +39,9 @@ namespace tfhe_mi355 {
 #ifndef PBS_MB_BUFLD
 #define PBS_MB_BUFLD 1  // GGSW loads through a buffer resource: scalar offsets, no 64-bit VALU address adds
 #endif
+#ifndef PBS_MB_TSKIP_MONO
+#define PBS_MB_TSKIP_MONO 0
+#endif
 #ifndef PBS_MB_SWK
 #define PBS_MB_SWK 4   // twist-table swizzle: position r ^ ((r >> SWK) & SWM) (M = 1024)
 #endif
@@ -85,7 +88,10 @@ struct TwistLds {
     // (re: q0 ^ q1, im: q1) are XORed into the high words -- no selects
     __device__ static cx mono(uint32_t t) {
         constexpr int LOG2M = ilog2(M);
-        const uint32_t are = ((t & (2u * M - 1)) ^ swz(t)) << 3;
+        // PBS_MB_TSKIP_MONO (timing-only builds, wrong outputs): every lane reads its own entry, so
+        // the monomial reads are conflict-free -- measures what their bank conflicts cost
+        const uint32_t are = PBS_MB_TSKIP_MONO ? ((t & (uint32_t)M) | (uint32_t)__lane_id()) << 3
+                                               : ((t & (2u * M - 1)) ^ swz(t)) << 3;
         const double re = lds_ld_f64(are), im = lds_ld_f64(are ^ IM);
         const uint32_t sim = t << (30 - LOG2M);  // q1 at bit 31; + 2^30 carries q0 into it
         return {flip_sign(re, sim + 0x40000000u), flip_sign(im, sim)};
