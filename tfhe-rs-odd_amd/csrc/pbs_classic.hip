@@ -36,6 +36,9 @@ namespace tfhe_mi355 {
 #ifndef PBS_CPW
 #define PBS_CPW 0  // ciphertexts per workgroup; 0: per-shape default
 #endif
+#ifndef PBS_TSKIP_ROT
+#define PBS_TSKIP_ROT 0  // timing-only builds (wrong outputs): no rotation gather (what the rotation costs)
+#endif
 #ifndef PBS_GGSW_LDS
 #define PBS_GGSW_LDS 0  // measured 2% slower than streaming from L2 (CPW=2 couples 4 waves); kept as an option
 #endif
@@ -236,10 +239,12 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
 
         // ct1 = X^{a~} ct0 - ct0 (polynomial_algorithms.rs:425-490) through the LDS buffer
         // (wave-private: the other waves' last reads of it ended at the post-MAC barrier)
-        wsync();
+        if (!PBS_TSKIP_ROT) {
+            wsync();
 #pragma unroll
-        for (int h = 0; h < 2 * V; h++) xb64[lane + 64 * h] = c0[h];
-        wsync();
+            for (int h = 0; h < 2 * V; h++) xb64[lane + 64 * h] = c0[h];
+            wsync();
+        }
         // (X^d p)[j] = -p[N-d+j] for j < d, p[j-d] otherwise (sign flipped again when the
         // rotation passes a full N); only the top 32 bits of ct1 feed the decomposition.
         // Source index jj = lane - rem + 64 h wraps (jj < 0) exactly for h < hcut, so the gather
@@ -251,6 +256,7 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
         const uint64_t *xpos = xb64 + rbase;
         const uint64_t *xneg = xpos + N;
         auto ct1_hi = [&](int h) -> uint32_t {
+            if (PBS_TSKIP_ROT) return (uint32_t)(c0[h] >> 32) ^ at;  // timing only: no rotation
             const bool wrap = h < hcut;
             const bool neg = wrap != full_odd;
             const uint64_t x = (wrap ? xneg : xpos)[64 * h];
