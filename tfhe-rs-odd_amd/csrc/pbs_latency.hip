@@ -376,12 +376,14 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
         for (int r = 0; r < RPW; r++)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const int j = lat_a1(w, col) + 64 * lrow + 256 * q;
                 // (X^rem p) at j and j + M from ONE pair: u = j - rem, s = u mod M; u >= 0: (lo, hi);
-                // -M <= u < 0: (-hi, lo) (X^M acts as i on the fold); u < -M: (-lo, -hi)
-                const int u = j - rem;
-                const int s = u & (M - 1);
-                const uint64_t plo = Ar(r)[2 * aswz(s)], phi = Ar(r)[2 * aswz(s) + 1];
+                // -M <= u < 0: (-hi, lo) (X^M acts as i on the fold); u < -M: (-lo, -hi).
+                // j = j0 + 256 q: the pair swizzle reads bits 3-5 and changes bits 0-1 only, so
+                // aswz(s) = (aswz(s0) + 256 q) mod M with s0 the q = 0 slot (one add per q)
+                const int u0 = lat_a1(w, col) + 64 * lrow - rem;
+                const int u = u0 + 256 * q;
+                const int s = (aswz(u0 & (M - 1)) + 256 * q) & (M - 1);
+                const uint64_t plo = Ar(r)[2 * s], phi = Ar(r)[2 * s + 1];
                 const bool swap = u < 0 && u >= -M;
                 const bool n0 = (u < 0) != full_odd, n1 = (u < -M) != full_odd;
                 const uint64_t x0 = swap ? phi : plo, x1 = swap ? plo : phi;
