@@ -287,7 +287,8 @@ bool is_large(const TfheMi355Context *c) {
 // stay resident in the 256 MiB Infinity Cache: 128 at N = 32768 (1.5 MiB per ciphertext at 4_4,
 // best of 64..1024 measured), otherwise ~200 MiB of scratch in multiples of 64 (64..1024) --
 // round 4 sweeps (profiles/r04_chunk_sweep.log): 3_3 384 / 512 / 768 -> 5.94k / 6.17k / 5.55k,
-// 2_5 192 / 256 -> 2268 / 2307, 1_4 832 / 1024 -> 13.5k / 14.3k KS+PBS/s (160 MiB gave 384 / 192 / 832).
+// 2_5 192 / 256 -> 2268 / 2307, 1_4 832 / 1024 -> 13.5k / 14.3k KS+PBS/s (160 MiB gave 384 / 192 / 832);
+// multi-bit mb3_3g3 (512 here) 384 / 512 / 768 / 1024 -> 9.11k / 9.30k / 8.59k / 8.19k (r04_mbchunk_*.log).
 size_t large_chunk(const TfheMi355Context *c) {
     static const size_t forced = [] {
         const char *e = std::getenv("TFHE_MI355_LARGE_CHUNK");
