@@ -21,7 +21,9 @@
  *     and return immediately; the others take HOST pointers and return after the outputs are
  *     written (synchronous).  The host-pointer forms pipeline the batch in chunks through
  *     page-locked staging on two streams (copies of one chunk overlap the kernels of the next);
- *   - a context is bound to one GPU; host-pointer calls on one context are thread-safe, so
+ *   - a context is bound to one GPU (tfhe_mi355_context_create) or to a list of GPUs
+ *     (tfhe_mi355_context_create_devices: keys replicated, batches split over the devices, see
+ *     there); host-pointer calls on one context are thread-safe, so
  *     rayon-style concurrent callers sharing a key are safe (SURVEY.md 8b "Threading"): calls of
  *     more than 64 ciphertexts are serialised by an internal mutex, smaller concurrent calls of
  *     the same entry point are coalesced into shared batches that a dispatcher thread of the
@@ -42,8 +44,11 @@
  *     of their own, and the calls can be captured into a hipGraph (no allocation or
  *     synchronisation inside);
  *   - keys: a key upload (any *_key_upload*, *_set_ready) waits for the coalesced batches in
- *     flight and blocks new ones until it is done; _async calls are not ordered with uploads:
- *     do not re-upload a key while _async work that reads it may still run;
+ *     flight and blocks new ones until it is done (a pending upload also keeps new batches from
+ *     starting, so uploads are not starved under load); between tfhe_mi355_bootstrap_key_fourier /
+ *     _keyswitch_key_device and the matching _set_ready the key counts as absent (calls needing it
+ *     fail) rather than half-written; _async calls are not ordered with uploads: do not
+ *     re-upload a key while _async work that reads it may still run;
  *   - _async lut index arrays are not checked on the host (they live on the device): an entry
  *     >= lut_count is clamped to lut_count - 1 by the kernels (no out-of-bounds read); the
  *     host-pointer forms reject such an entry with an error;
@@ -138,6 +143,33 @@ int tfhe_mi355_host_free(void *ptr);
  * (fft64/math/fft/mod.rs:146-193, shortint/engine/mod.rs:23-70,163-235). */
 int tfhe_mi355_context_create(const TfheMi355Parameters *params, int device,
                               TfheMi355Context **out_ctx);
+/* One context over several GPUs of this process (SURVEY.md 8b ctx_create(params, device_mask);
+ * the reference's one process with its rayon pool, shortint/engine/mod.rs:23-25, calling one KS+PBS
+ * per block from par_iter, integer/server_key/radix_parallel/mul.rs:347-407).  `devices` lists
+ * device ordinals (a device may repeat: its shards then run side by side on their own streams);
+ * devices = NULL with device_count = 0 takes every visible device; one device is the same as
+ * tfhe_mi355_context_create.  Behaviour of every entry point on such a context:
+ *   - key uploads (host or device pointer, seeded, serialized, the _fourier/_device + _set_ready
+ *     pairs) go to the first device and are replicated from its memory: RCCL ncclBroadcast among
+ *     the distinct devices (one rank per device, over xGMI; librccl is opened at run time), then
+ *     device-to-device copies to further shards of the same device (TFHE_MI355_REPLICATE=copy:
+ *     peer copies instead of RCCL); device-pointer key inputs live on the first device;
+ *   - batched host-pointer calls (PBS, KS, KS->PBS, PBS->KS, blind rotation, packing KS,
+ *     GLWE products) are split into contiguous row shares, one per device, run concurrently and
+ *     joined before the call returns; outputs are bit-identical to a single-device context;
+ *   - calls of at most TFHE_MI355_COALESCE_MAX_COUNT ciphertexts and tfhe_mi355_submit go to the
+ *     devices' coalescers in turn (round robin);
+ *   - device-pointer (_async) calls and the *_scratch queries address the FIRST device (a device
+ *     pointer belongs to one GPU): use tfhe_mi355_context_device_context for the others;
+ *   - kernel timing and coalescing statistics are summed over the devices. */
+int tfhe_mi355_context_create_devices(const TfheMi355Parameters *params, const int *devices, size_t device_count,
+                                      TfheMi355Context **out_ctx);
+/* Number of devices (shards) of a context: 1 for a single-device context. */
+int tfhe_mi355_context_devices(TfheMi355Context *ctx, size_t *count);
+/* The single-device context of shard `index` and its device ordinal (borrowed: owned and destroyed
+ * by `ctx`; destroying it directly fails).  For a single-device context, index 0 is ctx itself. */
+int tfhe_mi355_context_device_context(TfheMi355Context *ctx, size_t index, TfheMi355Context **out_ctx,
+                                      int *device);
 /* Destroy stops the request coalescer first (a batch already running completes), then frees the
  * device state.  Requests still queued are failed, not run: their tfhe_mi355_wait returns 1, and
  * destroy itself returns 1 saying how many there were (the context is destroyed all the same). */
@@ -191,8 +223,9 @@ int tfhe_mi355_programmable_bootstrap_async(TfheMi355Context *ctx, const uint64_
  *     N = 1024 k = 2 L = 3, N = 256 k = 5 L = 1 -- and 0 at the other classic shapes;
  *   - multi-bit N = 2048 / 512: 0;
  *   - N >= 4096, classic and multi-bit (N = 8192): the accumulators + spectra of one pass of
- *     min(count, chunk) ciphertexts (chunk = 128 at N = 32768, ~160 MiB worth below; e.g.
- *     1.5 MiB per ciphertext at 4_4).  Less scratch runs smaller passes; the call fails below one
+ *     min(count, chunk) ciphertexts (chunk = 128 at N = 32768; below, ~200 MiB worth in multiples
+ *     of 64, at most 1024: 1024 at N = 4096, 512 at N = 8192 (3_3 and multi-bit 3_3), 256 / 192
+ *     at N = 16384, L = 2 / 3; TFHE_MI355_LARGE_CHUNK overrides; e.g. 1.5 MiB per ciphertext at 4_4).  Less scratch runs smaller passes; the call fails below one
  *     ciphertext's worth.
  * tfhe_mi355_programmable_bootstrap_async fails when given less than this (N <= 2048) -- it never
  * falls back silently.  tfhe_mi355_blind_rotate_async takes no scratch and runs the one-pass grid. */

@@ -9,6 +9,10 @@
  *                       shape), a split-CMUX shape (N = 4096, chunk scratch) and multi-bit
  *                       (N = 2048, g = 3, no scratch); an async PBS given a NULL or a short
  *                       scratch fails with rc = 1 instead of running a fallback.
+ *   abi_test multi      a context over devices {0, 0} (tfhe_mi355_context_create_devices: two
+ *                       shards on the box's one GPU) against a single-device context with the same
+ *                       keys: batched PBS / KS->PBS / PBS->KS / KS (split over the shards), count-1
+ *                       calls and submit/wait (spread over the shards' coalescers) bit-identical.
  *   abi_test destroy    (run with TFHE_MI355_COALESCE_WINDOW_US / _GAP_US = 2 s so that the
  *                       request is still queued) destroying a context with an unwaited request
  *                       returns 1, and that request's wait returns 1 with a message.
@@ -77,6 +81,8 @@ typedef struct {
 typedef struct {
     TfheMi355Context *ctx;
     uint64_t *lwe_sk, *glwe_sk;
+    uint64_t *bsk, *ksk;  /* kept for a second context (multi mode) */
+    size_t bsk_len, ksk_len;
     uint64_t *lut;   /* 2 LUTs */
     size_t n, big, glwe;
 } Keys;
@@ -106,13 +112,15 @@ static void setup(const Case *c, Keys *k) {
         ABI(tfhe_mi355_client_gen_bootstrap_key(8, k->lwe_sk, (uint32_t)k->n, k->glwe_sk, p->glwe_dimension,
                                                 p->polynomial_size, p->pbs_base_log, p->pbs_level, c->glwe_std, bsk, 8));
     ABI(tfhe_mi355_bootstrap_key_upload(k->ctx, bsk, bsk_len));
-    free(bsk);
     const size_t ksk_len = k->big * p->ks_level * (k->n + 1);
     uint64_t *ksk = xalloc(ksk_len);
     ABI(tfhe_mi355_client_gen_keyswitch_key(9, k->glwe_sk, (uint32_t)k->big, k->lwe_sk, (uint32_t)k->n, p->ks_base_log,
                                             p->ks_level, c->lwe_std, ksk));
     ABI(tfhe_mi355_keyswitch_key_upload(k->ctx, ksk, ksk_len));
-    free(ksk);
+    k->bsk = bsk;
+    k->ksk = ksk;
+    k->bsk_len = bsk_len;
+    k->ksk_len = ksk_len;
     /* two LUTs: identity and x -> 3x + 1 (shortint fill_accumulator) */
     const uint64_t msg = (uint64_t)p->message_modulus * p->carry_modulus;
     uint64_t *f = xalloc(msg);
@@ -127,6 +135,8 @@ static void setup(const Case *c, Keys *k) {
 static void teardown(Keys *k) {
     int rc = tfhe_mi355_context_destroy(k->ctx);
     CHECK(rc == TFHE_MI355_OK, "destroy: %s", tfhe_mi355_last_error());
+    free(k->bsk);
+    free(k->ksk);
     free(k->lwe_sk);
     free(k->glwe_sk);
     free(k->lut);
@@ -282,6 +292,66 @@ static const Case CASE_2_3 = {"2_3", {64, 1, 4096, 22, 1, 3, 6, 4, 8, 0}, 8.7752
 /* PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS (N = 2048, g = 3), n = 66 */
 static const Case CASE_MB3 = {"mb3", {66, 1, 2048, 21, 1, 7, 2, 4, 4, 3}, 6.125031601933181e-07, 3.152931493498455e-16, 200};
 
+/* multi mode: the same calls on a {0, 0} context and a single-device one, compared row for row */
+static void run_multi(const Case *c) {
+    Keys k;
+    setup(c, &k);
+    const int devs[2] = {0, 0};
+    TfheMi355Context *m = NULL;
+    ABI(tfhe_mi355_context_create_devices(&c->p, devs, 2, &m));
+    size_t nd = 0;
+    ABI(tfhe_mi355_context_devices(m, &nd));
+    CHECK(nd == 2, "%s: %zu devices reported", c->name, nd);
+    TfheMi355Context *shard = NULL;
+    int dev = -1;
+    ABI(tfhe_mi355_context_device_context(m, 1, &shard, &dev));
+    CHECK(shard != NULL && dev == 0, "%s: shard 1 on device %d", c->name, dev);
+    CHECK(tfhe_mi355_context_destroy(shard) == TFHE_MI355_ERROR, "%s: a shard could be destroyed directly", c->name);
+    ABI(tfhe_mi355_bootstrap_key_upload(m, k.bsk, k.bsk_len));
+    ABI(tfhe_mi355_keyswitch_key_upload(m, k.ksk, k.ksk_len));
+    const size_t B = c->count, small_w = k.n + 1, big_w = k.big + 1;
+    uint32_t *idx = lut_indexes(B);
+    uint64_t *ct_small = encrypt(c, k.lwe_sk, k.n, B, c->lwe_std, 21);
+    uint64_t *ct_big = encrypt(c, k.glwe_sk, k.big, B, c->glwe_std, 22);
+    uint64_t *a = xalloc(B * big_w), *b = xalloc(B * big_w);
+    ABI(tfhe_mi355_programmable_bootstrap(k.ctx, ct_small, a, k.lut, 2, idx, B));
+    ABI(tfhe_mi355_programmable_bootstrap(m, ct_small, b, k.lut, 2, idx, B));
+    CHECK(same(a, b, B * big_w), "%s: multi-device PBS differs", c->name);
+    check_decrypt(c, &k, b, B, idx, "multi-device PBS");
+    ABI(tfhe_mi355_keyswitch_programmable_bootstrap(k.ctx, ct_big, a, k.lut, 2, idx, B));
+    ABI(tfhe_mi355_keyswitch_programmable_bootstrap(m, ct_big, b, k.lut, 2, idx, B));
+    CHECK(same(a, b, B * big_w), "%s: multi-device KS->PBS differs", c->name);
+    ABI(tfhe_mi355_keyswitch(k.ctx, ct_big, a, B));
+    ABI(tfhe_mi355_keyswitch(m, ct_big, b, B));
+    CHECK(same(a, b, B * small_w), "%s: multi-device KS differs", c->name);
+    ABI(tfhe_mi355_programmable_bootstrap_keyswitch(k.ctx, ct_small, a, k.lut, 2, idx, B));
+    ABI(tfhe_mi355_programmable_bootstrap_keyswitch(m, ct_small, b, k.lut, 2, idx, B));
+    CHECK(same(a, b, B * small_w), "%s: multi-device PBS->KS differs", c->name);
+    /* count-1 calls and submitted requests: spread over the shards' coalescers */
+    ABI(tfhe_mi355_programmable_bootstrap(k.ctx, ct_small, a, k.lut, 2, idx, B));
+    const size_t R = B < 40 ? B : 40;
+    TfheMi355Request **req = (TfheMi355Request **)calloc(R, sizeof(*req));
+    for (size_t i = 0; i < R; i++)
+        ABI(tfhe_mi355_submit(m, 0, ct_small + i * small_w, b + i * big_w, k.lut, 2, idx + i, 1, &req[i]));
+    for (size_t i = 0; i < R; i++) ABI(tfhe_mi355_wait(req[i]));
+    CHECK(same(a, b, R * big_w), "%s: multi-device submit/wait differs", c->name);
+    ABI(tfhe_mi355_programmable_bootstrap(m, ct_small + 5 * small_w, b, k.lut, 2, idx + 5, 1));
+    CHECK(same(a + 5 * big_w, b, big_w), "%s: multi-device count-1 call differs", c->name);
+    uint64_t batches = 0, rows = 0, inflight = 0;
+    double secs = 0;
+    ABI(tfhe_mi355_coalesce_stats(m, 0, &batches, &rows, &inflight, &secs));
+    CHECK(rows == R + 1, "%s: coalesced rows %llu, expected %zu", c->name, (unsigned long long)rows, R + 1);
+    free(req);
+    free(a);
+    free(b);
+    free(ct_small);
+    free(ct_big);
+    free(idx);
+    CHECK(tfhe_mi355_context_destroy(m) == TFHE_MI355_OK, "multi destroy: %s", tfhe_mi355_last_error());
+    teardown(&k);
+    printf("%s multi: %s\n", c->name, failures ? "FAILED" : "ok");
+}
+
 static int run_destroy(void) {
     Keys k;
     Case c = CASE_2_2;
@@ -302,6 +372,8 @@ static int run_destroy(void) {
     printf("wait: rc %d: %s\n", rc, tfhe_mi355_last_error());
     free(ct);
     free(out);
+    free(k.bsk);
+    free(k.ksk);
     free(k.lwe_sk);
     free(k.glwe_sk);
     free(k.lut);
@@ -317,8 +389,15 @@ int main(int argc, char **argv) {
         return 2;
     }
     if (!strcmp(mode, "destroy")) return run_destroy() ? 1 : 0;
+    if (!strcmp(mode, "multi")) {
+        run_multi(&CASE_2_2);
+        run_multi(&CASE_2_3);
+        run_multi(&CASE_MB3);
+        printf("%s\n", failures ? "FAILED" : "ALL OK");
+        return failures ? 1 : 0;
+    }
     if (strcmp(mode, "contract")) {
-        fprintf(stderr, "usage: abi_test contract|destroy\n");
+        fprintf(stderr, "usage: abi_test contract|multi|destroy\n");
         return 2;
     }
     run_contract(&CASE_2_2);

@@ -40,6 +40,15 @@ def test_c_caller_contract():
 
 
 @pytest.mark.gpu
+def test_c_caller_multi_device_context():
+    """tfhe_mi355_context_create_devices({0, 0}) from C: every batched / count-1 / submitted call
+    bit-identical to a single-device context with the same keys."""
+    r = _run("multi")
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ALL OK" in r.stdout
+
+
+@pytest.mark.gpu
 def test_c_caller_destroy_with_queued_request_fails_it():
     # a 2 s coalescing window keeps the submitted request queued until destroy runs
     r = _run("destroy", {"TFHE_MI355_COALESCE_WINDOW_US": "2000000", "TFHE_MI355_COALESCE_GAP_US": "2000000"})

@@ -2,8 +2,11 @@
 // context = device + parameter set + key material + FFT tables, guarded by a mutex so that
 // concurrent callers (the reference's rayon workers, shortint/engine/mod.rs:23-25) can share one
 // key.  Error convention: 0/1 return + thread-local message (tfhe/src/c_api/utils.rs:3-73).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types only: librccl is opened at run time, when keys are replicated
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -137,6 +140,8 @@ struct CoalescedReq {
     std::string err;
 };
 
+struct RcclComms;  // communicator over a multi-device context's distinct devices (key replication)
+
 struct TfheMi355Context {
     TfheMi355Parameters p{};
     int device = 0;
@@ -144,7 +149,20 @@ struct TfheMi355Context {
     // Key material vs the coalescer's batches: every key upload holds it exclusively, every
     // dispatcher batch shared, so a re-upload waits for the batches in flight and no batch starts
     // on a half-written key (the large host-pointer calls are ordered with uploads by `mu`).
+    // Uploads go through KeyWrite, batches through KeyRead.
     std::shared_mutex keys_mu;
+    // key writers waiting or running: a batch does not take keys_mu while one is pending, so an
+    // upload is never starved by back-to-back batches (libstdc++'s shared_mutex lets new readers
+    // in ahead of a waiting writer)
+    std::atomic<int> key_writers{0};
+    // Multi-device context (tfhe_mi355_context_create_devices): one single-device context per
+    // listed device (a device may repeat), owned by this one; empty for a single-device context.
+    // Every entry point of a multi-device context dispatches to them (see "multi-device").
+    std::vector<TfheMi355Context *> shards;
+    std::atomic<size_t> next_shard{0};  // round robin of coalesced calls and submits
+    RcclComms *rccl = nullptr;
+    TfheMi355Context *owner = nullptr;  // a shard: its multi-device context (destroyed with it)
+    bool multi() const { return !shards.empty(); }
     hipStream_t stream = nullptr;
     FftTables tables;
     DeviceBuffer fbsk, ksk, std_staging;
@@ -220,6 +238,47 @@ struct TfheMi355Context {
 };
 
 namespace {
+
+// ---- key transactions ------------------------------------------------------------------------
+// A key write holds the context's mutex and keys_mu exclusively.  It is re-entrant per thread: a
+// transaction (tfhe_mi355::begin_key_transaction, e.g. the serialized-key upload, which uploads the
+// KSK, fills the Fourier buffer and marks it ready through three ABI calls) keeps both locks for its
+// whole duration, and the nested calls on the same context from the same thread skip the locking.
+thread_local std::vector<const TfheMi355Context *> tl_key_writes;
+
+struct KeyWrite {
+    TfheMi355Context *c = nullptr;
+    std::unique_lock<std::mutex> g;
+    std::unique_lock<std::shared_mutex> k;
+    explicit KeyWrite(TfheMi355Context *c_) {
+        if (std::find(tl_key_writes.begin(), tl_key_writes.end(), c_) != tl_key_writes.end()) return;
+        c = c_;
+        c->key_writers.fetch_add(1, std::memory_order_acq_rel);
+        g = std::unique_lock<std::mutex>(c->mu);
+        k = std::unique_lock<std::shared_mutex>(c->keys_mu);
+        tl_key_writes.push_back(c);
+    }
+    KeyWrite(const KeyWrite &) = delete;
+    KeyWrite &operator=(const KeyWrite &) = delete;
+    ~KeyWrite() {
+        if (!c) return;
+        tl_key_writes.erase(std::find(tl_key_writes.begin(), tl_key_writes.end(), c));
+        k.unlock();
+        g.unlock();
+        c->key_writers.fetch_sub(1, std::memory_order_acq_rel);
+    }
+};
+
+// a coalesced batch reads the keys: it waits while an upload is pending (writer preference), then
+// holds keys_mu shared for the batch
+struct KeyRead {
+    std::shared_lock<std::shared_mutex> k;
+    explicit KeyRead(TfheMi355Context *c) {
+        while (c->key_writers.load(std::memory_order_acquire) > 0)
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        k = std::shared_lock<std::shared_mutex>(c->keys_mu);
+    }
+};
 
 // cos and sin called separately through opaque pointers (no compiler fusion into sincos, whose
 // last bits can differ): the same tables as the oracle's fft_init, bit for bit.
@@ -919,17 +978,17 @@ void coalesce_dispatcher(TfheMi355Context *c, size_t q) {
             qu.erase(qu.begin(), qu.begin() + take);
             co.queued[op] -= cts;
             co.queued_sync[op] -= sync_rows;
-            co.last_sync_rows[op] = sync_rows == cts ? cts : 0;
             if (batch.empty()) {  // another slot took the queue during the window
                 co.in_flight--;
                 continue;
             }
+            co.last_sync_rows[op] = sync_rows == cts ? cts : 0;  // only a batch that ran says how many callers
             if (full()) co.cv.notify_one();  // another full batch: an idle slot can run it now
         }
         std::string err;
         const auto t0 = std::chrono::steady_clock::now();
         try {
-            std::shared_lock<std::shared_mutex> keys(c->keys_mu);  // no key upload mid-batch
+            KeyRead keys(c);  // no key upload mid-batch
             run_coalesced_batch(c, sl, op, batch);
         } catch (const std::exception &ex) {
             err = ex.what();
@@ -1012,7 +1071,7 @@ void coalesced_call(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
     std::string err;
     const auto t0 = std::chrono::steady_clock::now();
     try {
-        std::shared_lock<std::shared_mutex> keys(c->keys_mu);  // no key upload mid-batch
+        KeyRead keys(c);  // no key upload mid-batch
         const std::vector<CoalescedReq *> one{&r};
         run_coalesced_batch(c, co.slots[8], op, one);
     } catch (const std::exception &ex) {
@@ -1029,7 +1088,278 @@ void coalesced_call(TfheMi355Context *c, CoalescedOp op, CoalescedReq &r) {
 }
 
 bool coalescible(size_t count) { return count > 0 && count <= coalesce_max_count(); }
+
+// an ABI call made from inside another one: its failure text becomes ours
+void abi(int rc) {
+    if (rc != TFHE_MI355_OK) fail("%s", tfhe_mi355_last_error());
+}
+
+// ---- multi-device contexts ----------------------------------------------------------------------
+// SURVEY.md 8b `ctx_create(params, device_mask)` / 8e: ONE process drives several GPUs through one
+// context, the way the reference's one process drives its rayon pool (a thread-local ShortintEngine
+// per worker, shortint/engine/mod.rs:23-25, and one KS+PBS per block from par_iter,
+// integer/server_key/radix_parallel/mul.rs:347-407, through the ShortintBootstrappingKey arms,
+// shortint/server_key/mod.rs:104-111,783-857).  A multi-device context owns one single-device context
+// ("shard") per listed device; a device may be listed more than once (shards on one GPU then run
+// side by side on their own streams).
+//   keys: uploaded once, to the first shard, and replicated from its device memory: an RCCL
+//     broadcast over xGMI among the distinct devices (librccl opened at run time; ncclCommInitAll
+//     over the device list, one rank per distinct device), then device-to-device copies to further
+//     shards on the same device.  TFHE_MI355_REPLICATE=copy uses peer copies instead of RCCL,
+//     =rccl forces the broadcast even with one distinct device (a one-rank communicator copying
+//     into the second shard of that device; a test hook);
+//   batched host-pointer calls: split into contiguous shares, one per shard, each run by the shard's
+//     own entry point on a thread of its own (its own stream, staging, lock) and joined before the
+//     call returns;
+//   small calls (the coalesced ones) and submitted requests: round-robin to the shards' coalescers;
+//   device-pointer (_async) calls and their scratch queries: the first device's shard (a device
+//     pointer belongs to one device; tfhe_mi355_context_device_context hands out each shard).
 }  // namespace
+
+struct RcclComms {
+    void *lib = nullptr;
+    decltype(&ncclCommInitAll) init_all = nullptr;
+    decltype(&ncclBroadcast) broadcast = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    std::vector<int> devices;  // rank -> device
+    std::vector<ncclComm_t> comms;
+    ~RcclComms() {
+        for (size_t r = 0; r < comms.size(); r++)
+            if (comms[r] && comm_destroy) {
+                (void)hipSetDevice(devices[r]);
+                (void)comm_destroy(comms[r]);
+            }
+        if (lib) dlclose(lib);
+    }
+};
+
+namespace {
+
+void check_nccl(const RcclComms &rc, ncclResult_t r, const char *what) {
+    if (r != ncclSuccess) fail("%s: %s", what, rc.error_string ? rc.error_string(r) : "RCCL error");
+}
+
+// the communicator over `devices` (rank 0 = the source's device), created once per context
+RcclComms &rccl_for(TfheMi355Context *m, const std::vector<int> &devices) {
+    if (m->rccl && m->rccl->devices == devices) return *m->rccl;
+    delete m->rccl;
+    m->rccl = nullptr;
+    auto rc = std::make_unique<RcclComms>();
+    rc->lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!rc->lib) rc->lib = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!rc->lib) fail("RCCL is not available for key replication (%s); TFHE_MI355_REPLICATE=copy uses peer copies",
+                       dlerror());
+    auto sym = [&](const char *name) {
+        void *f = dlsym(rc->lib, name);
+        if (!f) fail("librccl lacks %s", name);
+        return f;
+    };
+    rc->init_all = reinterpret_cast<decltype(rc->init_all)>(sym("ncclCommInitAll"));
+    rc->broadcast = reinterpret_cast<decltype(rc->broadcast)>(sym("ncclBroadcast"));
+    rc->group_start = reinterpret_cast<decltype(rc->group_start)>(sym("ncclGroupStart"));
+    rc->group_end = reinterpret_cast<decltype(rc->group_end)>(sym("ncclGroupEnd"));
+    rc->comm_destroy = reinterpret_cast<decltype(rc->comm_destroy)>(sym("ncclCommDestroy"));
+    rc->error_string = reinterpret_cast<decltype(rc->error_string)>(sym("ncclGetErrorString"));
+    rc->devices = devices;
+    rc->comms.assign(devices.size(), nullptr);
+    check_nccl(*rc, rc->init_all(rc->comms.data(), (int)devices.size(), devices.data()), "ncclCommInitAll");
+    m->rccl = rc.release();
+    return *m->rccl;
+}
+
+// TFHE_MI355_REPLICATE: "auto" (default), "rccl", "copy"
+std::string replicate_mode() {
+    const char *e = std::getenv("TFHE_MI355_REPLICATE");
+    return e && *e ? std::string(e) : std::string("auto");
+}
+
+enum class KeyPart { Fourier, Ksk };
+
+// shard 0's key part -> every other shard (see above); the ready flags are the caller's business
+void replicate(TfheMi355Context *m, KeyPart part) {
+    auto &S = m->shards;
+    TfheMi355Context *src = S[0];
+    const size_t bytes = part == KeyPart::Fourier ? src->fourier_bsk_bytes() : src->ksk_len() * sizeof(uint64_t);
+    auto buffer = [&](TfheMi355Context *s) -> DeviceBuffer & { return part == KeyPart::Fourier ? s->fbsk : s->ksk; };
+    if (!buffer(src).ptr || buffer(src).bytes < bytes) fail("no key on the first device to replicate");
+    // distinct devices in order of first appearance (rank 0: the source's) and the shards on each
+    std::vector<int> devs;
+    std::vector<std::vector<size_t>> on;
+    for (size_t i = 0; i < S.size(); i++) {
+        const auto it = std::find(devs.begin(), devs.end(), S[i]->device);
+        if (it == devs.end()) {
+            devs.push_back(S[i]->device);
+            on.push_back({i});
+        } else {
+            on[it - devs.begin()].push_back(i);
+        }
+    }
+    for (size_t i = 1; i < S.size(); i++) {
+        check(hipSetDevice(S[i]->device), "hipSetDevice");
+        buffer(S[i]).reserve(bytes);
+    }
+    // the shard of each device that receives the broadcast: the first one on it (on the source's
+    // device: a second shard there, else the source itself, in place)
+    std::vector<size_t> holder(devs.size());
+    for (size_t r = 0; r < devs.size(); r++) holder[r] = r == 0 && on[0].size() > 1 ? on[0][1] : on[r][0];
+    const std::string mode = replicate_mode();
+    const bool use_rccl = mode == "rccl" || (mode != "copy" && devs.size() > 1);
+    auto sync_all = [&] {
+        for (auto *s : S) {
+            check(hipSetDevice(s->device), "hipSetDevice");
+            check(hipStreamSynchronize(s->stream), "key replication sync");
+        }
+    };
+    check(hipSetDevice(src->device), "hipSetDevice");
+    check(hipStreamSynchronize(src->stream), "key source sync");
+    if (use_rccl) {
+        RcclComms &rc = rccl_for(m, devs);
+        check_nccl(rc, rc.group_start(), "ncclGroupStart");
+        for (size_t r = 0; r < devs.size(); r++) {
+            check(hipSetDevice(devs[r]), "hipSetDevice");
+            TfheMi355Context *h = S[holder[r]];
+            const ncclResult_t e =
+                rc.broadcast(buffer(src).ptr, buffer(h).ptr, bytes, ncclUint8, 0, rc.comms[r], h->stream);
+            if (e != ncclSuccess) {
+                (void)rc.group_end();
+                check_nccl(rc, e, "ncclBroadcast");
+            }
+        }
+        check_nccl(rc, rc.group_end(), "ncclGroupEnd");
+    } else {
+        for (size_t r = 0; r < devs.size(); r++) {
+            if (holder[r] == 0) continue;
+            TfheMi355Context *h = S[holder[r]];
+            check(hipSetDevice(h->device), "hipSetDevice");
+            check(h->device == src->device
+                      ? hipMemcpyAsync(buffer(h).ptr, buffer(src).ptr, bytes, hipMemcpyDeviceToDevice, h->stream)
+                      : hipMemcpyPeerAsync(buffer(h).ptr, h->device, buffer(src).ptr, src->device, bytes, h->stream),
+                  "key peer copy");
+        }
+    }
+    sync_all();
+    for (size_t r = 0; r < devs.size(); r++)  // the other shards of each device: from its holder
+        for (size_t i : on[r]) {
+            if (i == 0 || i == holder[r]) continue;
+            check(hipSetDevice(S[i]->device), "hipSetDevice");
+            check(hipMemcpyAsync(buffer(S[i]).ptr, buffer(S[holder[r]]).ptr, bytes, hipMemcpyDeviceToDevice,
+                                 S[i]->stream),
+                  "key device copy");
+        }
+    if (part == KeyPart::Ksk)  // each shard repacks its own byte planes for the MFMA keyswitch
+        for (size_t i = 1; i < S.size(); i++) {
+            check(hipSetDevice(S[i]->device), "hipSetDevice");
+            repack_ksk(S[i], S[i]->stream);
+        }
+    sync_all();
+    check(hipSetDevice(src->device), "hipSetDevice");
+}
+
+// the context itself, or the first shard of a multi-device one (device-pointer calls)
+TfheMi355Context *primary(TfheMi355Context *c) { return c && c->multi() ? c->shards[0] : c; }
+
+// the shard that takes the next small call / submitted request
+TfheMi355Context *pick_shard(TfheMi355Context *m) {
+    return m->shards[m->next_shard.fetch_add(1, std::memory_order_relaxed) % m->shards.size()];
+}
+
+// key writes of a multi-device context: its own lock (uploads in turn), then every shard's (no
+// coalesced batch on any device while the key changes)
+std::vector<std::unique_ptr<KeyWrite>> key_write_all(TfheMi355Context *c) {
+    std::vector<std::unique_ptr<KeyWrite>> w;
+    w.emplace_back(new KeyWrite(c));
+    for (auto *s : c->shards) w.emplace_back(new KeyWrite(s));
+    return w;
+}
+
+void set_ready_all(TfheMi355Context *m, KeyPart part, bool ready) {
+    for (auto *s : m->shards) {
+        if (part == KeyPart::Fourier) s->fbsk_ready = ready;
+        else s->ksk_ready = ready;
+    }
+}
+
+// a batched host-pointer call of a multi-device context: shard i runs rows [count i / S, count (i+1)
+// / S) through `f(shard, first, count)` (an entry point of the shard, 0 = ok), shard 0 on the calling
+// thread and the others on threads of their own; joined, then the first failure is reported
+template <class F>
+void split_rows(TfheMi355Context *m, size_t count, F &&f) {
+    const size_t S = m->shards.size();
+    std::vector<std::string> errs(S);
+    auto run = [&](size_t i) {
+        const size_t a = count * i / S, b = count * (i + 1) / S;
+        if (a == b) return;
+        if (f(m->shards[i], a, b - a) != TFHE_MI355_OK) errs[i] = tfhe_mi355_last_error();
+    };
+    std::vector<std::thread> th;
+    for (size_t i = 1; i < S; i++) th.emplace_back(run, i);
+    run(0);
+    for (auto &t : th) t.join();
+    for (size_t i = 0; i < S; i++)
+        if (!errs[i].empty()) fail("device %d (shard %zu): %s", m->shards[i]->device, i, errs[i].c_str());
+}
+
+// parameter checks shared by the single- and multi-device constructors
+void validate_parameters(const TfheMi355Parameters &p) {
+    if (!is_pow2(p.polynomial_size)) fail("polynomial_size must be a power of two");
+    if (p.grouping_factor != 0) {
+        if (!multibit_pbs_supported((int)p.polynomial_size, (int)p.glwe_dimension, (int)p.pbs_level,
+                                    (int)p.grouping_factor) &&
+            !large_multibit_supported((int)p.polynomial_size, (int)p.glwe_dimension, (int)p.pbs_level,
+                                      (int)p.grouping_factor))
+            fail("no multi-bit kernel for N=%u k=%u pbs_level=%u grouping_factor=%u", p.polynomial_size,
+                 p.glwe_dimension, p.pbs_level, p.grouping_factor);
+        if (p.lwe_dimension % p.grouping_factor)
+            fail("lwe_dimension %u is not a multiple of grouping_factor %u", p.lwe_dimension, p.grouping_factor);
+    } else if (!classic_pbs_supported((int)p.polynomial_size, (int)p.glwe_dimension, (int)p.pbs_level) &&
+               !large_pbs_supported((int)p.polynomial_size, (int)p.glwe_dimension, (int)p.pbs_level)) {
+        fail("no kernel for N=%u k=%u pbs_level=%u", p.polynomial_size, p.glwe_dimension, p.pbs_level);
+    }
+    // the N <= 2048 kernels (and the grouped N = 32768 CMUX) decompose in 32-bit registers;
+    // the split CMUX of N >= 4096 in 64-bit ones (the shortint sets reach 11 x 3 = 33 bits)
+    const bool split = !p.grouping_factor && p.polynomial_size >= 4096;
+    const uint32_t max_bits = split ? 63 : 30;
+    if (p.pbs_base_log < 2 || p.pbs_base_log * p.pbs_level > max_bits)
+        fail("pbs decomposition base_log*level must be in [2, %u] (got %u x %u)", max_bits, p.pbs_base_log,
+             p.pbs_level);
+    // the split CMUX keeps the lower levels' digits as int16 between passes: a signed digit lies
+    // in [-2^(beta-1), 2^(beta-1)], so beta <= 15 (beta = 16 would wrap +2^15 to -2^15); this
+    // also keeps the grouped N = 32768, L = 2 path's 32-bit decomposition at beta * L <= 30
+    if (split && p.pbs_level > 1 && p.pbs_base_log > 15)
+        fail("pbs base_log %u > 15 with %u levels at N = %u (digits are packed as int16)", p.pbs_base_log,
+             p.pbs_level, p.polynomial_size);
+    if (p.ks_level && (p.ks_base_log == 0 || p.ks_base_log * p.ks_level >= 64)) fail("invalid ks decomposition");
+    if (p.lwe_dimension == 0) fail("lwe_dimension must be > 0");
+}
+
+TfheMi355Context *create_single(const TfheMi355Parameters &p, int device) {
+    check(hipSetDevice(device), "hipSetDevice");
+    auto *c = new TfheMi355Context();
+    c->p = p;
+    c->device = device;
+    try {
+        check(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+        for (auto &L : c->lanes) {
+            check(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking), "hipStreamCreate(lane)");
+            for (hipEvent_t *e : {&L.h2d, &L.kern, &L.done})
+                check(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate(lane)");
+        }
+        build_tables(c);
+    } catch (...) {
+        tfhe_mi355_context_destroy(c);
+        throw;
+    }
+    return c;
+}
+}  // namespace
+
+// key transaction of serde.cpp's serialized-key uploads (engine.h)
+std::shared_ptr<void> tfhe_mi355::begin_key_transaction(TfheMi355Context *ctx) {
+    return std::make_shared<std::vector<std::unique_ptr<KeyWrite>>>(key_write_all(ctx));
+}
 
 extern "C" {
 
@@ -1049,6 +1379,10 @@ int tfhe_mi355_kernel_timing_enable(TfheMi355Context *ctx, int every) {
     return guarded([&] {
         if (!ctx) fail("null argument");
         if (every < 0) fail("sampling interval must be >= 0");
+        if (ctx->multi()) {
+            for (auto *s : ctx->shards) abi(tfhe_mi355_kernel_timing_enable(s, every));
+            return;
+        }
         check(hipSetDevice(ctx->device), "hipSetDevice");
         ctx->timer.reset();
         ctx->timer.every = every;
@@ -1062,6 +1396,25 @@ int tfhe_mi355_kernel_timing_entry(TfheMi355Context *ctx, size_t index, char *na
         name[0] = 0;
         *total_ms = 0;
         *launches = 0;
+        if (ctx->multi()) {  // summed over the devices, by kernel family
+            std::map<std::string, std::pair<double, uint64_t>> all;
+            char nm[256];
+            for (auto *s : ctx->shards) {
+                double ms = 0;
+                uint64_t cnt = 0;
+                for (size_t i = 0; tfhe_mi355_kernel_timing_entry(s, i, nm, sizeof nm, &ms, &cnt) == TFHE_MI355_OK; i++) {
+                    all[nm].first += ms;
+                    all[nm].second += cnt;
+                }
+            }
+            if (index >= all.size()) fail("kernel timing index %zu out of range (%zu entries)", index, all.size());
+            auto it = all.begin();
+            std::advance(it, index);
+            std::snprintf(name, name_len, "%s", it->first.c_str());
+            *total_ms = it->second.first;
+            *launches = it->second.second;
+            return;
+        }
         check(hipSetDevice(ctx->device), "hipSetDevice");
         ctx->timer.collect();
         std::lock_guard<std::mutex> g(ctx->timer.mu);
@@ -1086,6 +1439,10 @@ int tfhe_mi355_submit(TfheMi355Context *ctx, int op, const uint64_t *lwe_in, uin
         *out_req = nullptr;
         if (!ctx || !lwe_in || !lwe_out) fail("null argument");
         if (op < 0 || op >= CO_OPS) fail("unknown op %d (0 PBS, 1 KS->PBS, 2 PBS->KS, 3 KS)", op);
+        if (ctx->multi()) {  // round robin over the devices' coalescers
+            abi(tfhe_mi355_submit(pick_shard(ctx), op, lwe_in, lwe_out, luts, lut_count, lut_indexes, count, out_req));
+            return;
+        }
         if (count == 0 || count > coalesce_batch())
             fail("submit takes 1..%zu ciphertexts (larger batches: the batched entry points)", coalesce_batch());
         check(hipSetDevice(ctx->device), "hipSetDevice");
@@ -1115,6 +1472,20 @@ int tfhe_mi355_coalesce_stats(TfheMi355Context *ctx, int reset, uint64_t *batche
                               uint64_t *max_in_flight, double *batch_seconds) {
     return guarded([&] {
         if (!ctx || !batches || !rows || !max_in_flight || !batch_seconds) fail("null argument");
+        if (ctx->multi()) {  // summed over the devices (max_in_flight: the sum of the devices' maxima)
+            *batches = *rows = *max_in_flight = 0;
+            *batch_seconds = 0;
+            for (auto *s : ctx->shards) {
+                uint64_t b = 0, r = 0, m = 0;
+                double t = 0;
+                abi(tfhe_mi355_coalesce_stats(s, reset, &b, &r, &m, &t));
+                *batches += b;
+                *rows += r;
+                *max_in_flight += m;
+                *batch_seconds += t;
+            }
+            return;
+        }
         auto &co = ctx->co;
         std::lock_guard<std::mutex> g(co.m);
         *batches = co.batches;
@@ -1151,59 +1522,85 @@ int tfhe_mi355_context_create(const TfheMi355Parameters *params, int device, Tfh
         if (!out_ctx) fail("null out_ctx");
         *out_ctx = nullptr;
         if (!params) fail("null params");
-        const TfheMi355Parameters &p = *params;
-        if (!is_pow2(p.polynomial_size)) fail("polynomial_size must be a power of two");
-        if (p.grouping_factor != 0) {
-            if (!multibit_pbs_supported((int)p.polynomial_size, (int)p.glwe_dimension, (int)p.pbs_level,
-                                        (int)p.grouping_factor) &&
-                !large_multibit_supported((int)p.polynomial_size, (int)p.glwe_dimension, (int)p.pbs_level,
-                                          (int)p.grouping_factor))
-                fail("no multi-bit kernel for N=%u k=%u pbs_level=%u grouping_factor=%u", p.polynomial_size,
-                     p.glwe_dimension, p.pbs_level, p.grouping_factor);
-            if (p.lwe_dimension % p.grouping_factor)
-                fail("lwe_dimension %u is not a multiple of grouping_factor %u", p.lwe_dimension, p.grouping_factor);
-        } else if (!classic_pbs_supported((int)p.polynomial_size, (int)p.glwe_dimension, (int)p.pbs_level) &&
-                   !large_pbs_supported((int)p.polynomial_size, (int)p.glwe_dimension, (int)p.pbs_level)) {
-            fail("no kernel for N=%u k=%u pbs_level=%u", p.polynomial_size, p.glwe_dimension, p.pbs_level);
+        validate_parameters(*params);
+        *out_ctx = create_single(*params, device);
+    });
+}
+
+int tfhe_mi355_context_create_devices(const TfheMi355Parameters *params, const int *devices, size_t device_count,
+                                      TfheMi355Context **out_ctx) {
+    return guarded([&] {
+        if (!out_ctx) fail("null out_ctx");
+        *out_ctx = nullptr;
+        if (!params || (!devices && device_count)) fail("null argument");
+        validate_parameters(*params);
+        int visible = 0;
+        check(hipGetDeviceCount(&visible), "hipGetDeviceCount");
+        std::vector<int> devs(devices, devices + device_count);
+        if (devs.empty())  // no list: every visible device
+            for (int d = 0; d < visible; d++) devs.push_back(d);
+        if (devs.empty()) fail("no GPU visible");
+        if (devs.size() > 64) fail("at most 64 devices per context (%zu listed)", devs.size());
+        for (int d : devs)
+            if (d < 0 || d >= visible) fail("device %d is not visible (%d devices)", d, visible);
+        if (devs.size() == 1) {
+            *out_ctx = create_single(*params, devs[0]);
+            return;
         }
-        // the N <= 2048 kernels (and the grouped N = 32768 CMUX) decompose in 32-bit registers;
-        // the split CMUX of N >= 4096 in 64-bit ones (the shortint sets reach 11 x 3 = 33 bits)
-        const bool split = !p.grouping_factor && p.polynomial_size >= 4096;
-        const uint32_t max_bits = split ? 63 : 30;
-        if (p.pbs_base_log < 2 || p.pbs_base_log * p.pbs_level > max_bits)
-            fail("pbs decomposition base_log*level must be in [2, %u] (got %u x %u)", max_bits, p.pbs_base_log,
-                 p.pbs_level);
-        // the split CMUX keeps the lower levels' digits as int16 between passes: a signed digit lies
-        // in [-2^(beta-1), 2^(beta-1)], so beta <= 15 (beta = 16 would wrap +2^15 to -2^15); this
-        // also keeps the grouped N = 32768, L = 2 path's 32-bit decomposition at beta * L <= 30
-        if (split && p.pbs_level > 1 && p.pbs_base_log > 15)
-            fail("pbs base_log %u > 15 with %u levels at N = %u (digits are packed as int16)", p.pbs_base_log,
-                 p.pbs_level, p.polynomial_size);
-        if (p.ks_level && (p.ks_base_log == 0 || p.ks_base_log * p.ks_level >= 64)) fail("invalid ks decomposition");
-        if (p.lwe_dimension == 0) fail("lwe_dimension must be > 0");
-        check(hipSetDevice(device), "hipSetDevice");
-        auto *c = new TfheMi355Context();
-        c->p = p;
-        c->device = device;
+        auto *m = new TfheMi355Context();
+        m->p = *params;
+        m->device = devs[0];
         try {
-            check(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
-            for (auto &L : c->lanes) {
-                check(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking), "hipStreamCreate(lane)");
-                for (hipEvent_t *e : {&L.h2d, &L.kern, &L.done})
-                    check(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate(lane)");
+            for (int d : devs) {
+                m->shards.push_back(create_single(*params, d));
+                m->shards.back()->owner = m;
             }
-            build_tables(c);
         } catch (...) {
-            tfhe_mi355_context_destroy(c);
+            tfhe_mi355_context_destroy(m);
             throw;
         }
-        *out_ctx = c;
+        check(hipSetDevice(devs[0]), "hipSetDevice");
+        *out_ctx = m;
+    });
+}
+
+int tfhe_mi355_context_devices(TfheMi355Context *ctx, size_t *count) {
+    return guarded([&] {
+        if (!ctx || !count) fail("null argument");
+        *count = ctx->multi() ? ctx->shards.size() : 1;
+    });
+}
+
+int tfhe_mi355_context_device_context(TfheMi355Context *ctx, size_t index, TfheMi355Context **out_ctx,
+                                      int *device) {
+    return guarded([&] {
+        if (!out_ctx) fail("null out_ctx");
+        *out_ctx = nullptr;
+        if (!ctx) fail("null ctx");
+        const size_t n = ctx->multi() ? ctx->shards.size() : 1;
+        if (index >= n) fail("device index %zu out of range (%zu devices)", index, n);
+        TfheMi355Context *s = ctx->multi() ? ctx->shards[index] : ctx;
+        if (device) *device = s->device;
+        *out_ctx = s;
     });
 }
 
 int tfhe_mi355_context_destroy(TfheMi355Context *ctx) {
     return guarded([&] {
         if (!ctx) return;
+        if (ctx->owner) fail("this context belongs to a multi-device context: destroy that one");
+        if (ctx->multi()) {  // every shard (each reports its own queued requests), then the communicator
+            std::string errs;
+            for (auto *s : ctx->shards) {
+                s->owner = nullptr;
+                if (tfhe_mi355_context_destroy(s) != TFHE_MI355_OK)
+                    errs += std::string(errs.empty() ? "" : "; ") + tfhe_mi355_last_error();
+            }
+            delete ctx->rccl;
+            delete ctx;
+            if (!errs.empty()) fail("%s", errs.c_str());
+            return;
+        }
         (void)hipSetDevice(ctx->device);
         // 1. The coalescer first: take every still-queued request out of the queues and stop the
         //    dispatchers (a batch already running completes; its callers get their rows), join
@@ -1266,13 +1663,34 @@ int tfhe_mi355_context_destroy(TfheMi355Context *ctx) {
     });
 }
 
+}  // extern "C"
+
+namespace {
+// a key upload of a multi-device context: `first` (the same entry point) on the first device's
+// shard, then the key part replicated to the other shards (RCCL broadcast / device copies)
+template <class F>
+void multi_key_upload(TfheMi355Context *m, KeyPart part, F &&first) {
+    auto w = key_write_all(m);
+    set_ready_all(m, part, false);
+    abi(first(m->shards[0]));
+    replicate(m, part);
+    set_ready_all(m, part, true);
+}
+}  // namespace
+
+extern "C" {
+
 int tfhe_mi355_bootstrap_key_upload(TfheMi355Context *ctx, const uint64_t *bsk, size_t len) {
     return guarded([&] {
         if (!ctx || !bsk) fail("null argument");
-        std::lock_guard<std::mutex> g(ctx->mu);
-        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
+        if (ctx->multi())
+            return multi_key_upload(ctx, KeyPart::Fourier, [&](TfheMi355Context *s) {
+                return tfhe_mi355_bootstrap_key_upload(s, bsk, len);
+            });
+        KeyWrite kw(ctx);  // no coalesced batch in flight, none starts until done
         check(hipSetDevice(ctx->device), "hipSetDevice");
         if (len != ctx->std_bsk_len()) fail("bootstrapping key has %zu words, expected %zu", len, ctx->std_bsk_len());
+        ctx->fbsk_ready = false;
         ctx->std_staging.reserve(len * sizeof(uint64_t));
         check(hipMemcpyAsync(ctx->std_staging.ptr, bsk, len * sizeof(uint64_t), hipMemcpyHostToDevice,
                              ctx->stream), "upload bsk");
@@ -1300,11 +1718,15 @@ int tfhe_mi355_bootstrap_key_upload_seeded(TfheMi355Context *ctx, const uint64_t
                                            uint64_t seed_lo, uint64_t seed_hi) {
     return guarded([&] {
         if (!ctx || !bodies) fail("null argument");
-        std::lock_guard<std::mutex> g(ctx->mu);
-        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
+        if (ctx->multi())
+            return multi_key_upload(ctx, KeyPart::Fourier, [&](TfheMi355Context *s) {
+                return tfhe_mi355_bootstrap_key_upload_seeded(s, bodies, len, seed_lo, seed_hi);
+            });
+        KeyWrite kw(ctx);  // no coalesced batch in flight, none starts until done
         check(hipSetDevice(ctx->device), "hipSetDevice");
         const size_t rows = ctx->ggsw_count() * ctx->p.pbs_level * (ctx->k() + 1);
         if (len != rows * ctx->N()) fail("seeded bootstrapping key has %zu body words, expected %zu", len, rows * ctx->N());
+        ctx->fbsk_ready = false;
         DeviceBuffer tab;
         upload_aes_tables(ctx, seed_lo, seed_hi, tab);
         DeviceBuffer d_bodies;
@@ -1330,8 +1752,11 @@ int tfhe_mi355_keyswitch_key_upload_seeded(TfheMi355Context *ctx, const uint64_t
                                            uint64_t seed_lo, uint64_t seed_hi) {
     return guarded([&] {
         if (!ctx || !bodies) fail("null argument");
-        std::lock_guard<std::mutex> g(ctx->mu);
-        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
+        if (ctx->multi())
+            return multi_key_upload(ctx, KeyPart::Ksk, [&](TfheMi355Context *s) {
+                return tfhe_mi355_keyswitch_key_upload_seeded(s, bodies, len, seed_lo, seed_hi);
+            });
+        KeyWrite kw(ctx);  // no coalesced batch in flight, none starts until done
         check(hipSetDevice(ctx->device), "hipSetDevice");
         const size_t rows = ctx->big_dim() * ctx->p.ks_level;
         if (len != rows) fail("seeded keyswitching key has %zu body words, expected %zu", len, rows);
@@ -1357,6 +1782,7 @@ int tfhe_mi355_keyswitch_key_upload_seeded(TfheMi355Context *ctx, const uint64_t
 int tfhe_mi355_csprng_mask_words(TfheMi355Context *ctx, uint64_t seed_lo, uint64_t seed_hi, uint64_t *out,
                                  size_t words) {
     return guarded([&] {
+        ctx = primary(ctx);  // device pointers: the first device's shard
         if (!ctx || (!out && words)) fail("null argument");
         std::lock_guard<std::mutex> g(ctx->mu);
         check(hipSetDevice(ctx->device), "hipSetDevice");
@@ -1378,8 +1804,11 @@ int tfhe_mi355_bootstrap_key_convert_async(TfheMi355Context *ctx, const uint64_t
                                            void *stream) {
     return guarded([&] {
         if (!ctx || !d_bsk) fail("null argument");
-        std::lock_guard<std::mutex> g(ctx->mu);
-        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
+        if (ctx->multi())  // d_bsk on the first device
+            return multi_key_upload(ctx, KeyPart::Fourier, [&](TfheMi355Context *s) {
+                return tfhe_mi355_bootstrap_key_convert_async(s, d_bsk, len, stream);
+            });
+        KeyWrite kw(ctx);  // no coalesced batch in flight, none starts until done
         check(hipSetDevice(ctx->device), "hipSetDevice");
         if (len != ctx->std_bsk_len()) fail("bootstrapping key has %zu words, expected %zu", len, ctx->std_bsk_len());
         ctx->fbsk_ready = false;
@@ -1404,9 +1833,17 @@ int tfhe_mi355_bootstrap_key_fourier(TfheMi355Context *ctx, void **d_ptr, size_t
         if (!ctx || !d_ptr || !bytes) fail("null argument");
         *d_ptr = nullptr;
         *bytes = 0;
-        std::lock_guard<std::mutex> g(ctx->mu);
-        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
+        if (ctx->multi()) {  // the first device's buffer; _set_ready replicates it
+            auto w = key_write_all(ctx);
+            set_ready_all(ctx, KeyPart::Fourier, false);
+            abi(tfhe_mi355_bootstrap_key_fourier(ctx->shards[0], d_ptr, bytes));
+            return;
+        }
+        KeyWrite kw(ctx);  // no coalesced batch in flight, none starts until done
         check(hipSetDevice(ctx->device), "hipSetDevice");
+        // the buffer is about to be written by the caller: batches fail ("not uploaded") until
+        // _set_ready instead of bootstrapping with a half-written key
+        ctx->fbsk_ready = false;
         ctx->fbsk.reserve(ctx->fourier_bsk_bytes());
         *d_ptr = ctx->fbsk.ptr;
         *bytes = ctx->fourier_bsk_bytes();
@@ -1416,8 +1853,11 @@ int tfhe_mi355_bootstrap_key_fourier(TfheMi355Context *ctx, void **d_ptr, size_t
 int tfhe_mi355_bootstrap_key_fourier_set_ready(TfheMi355Context *ctx) {
     return guarded([&] {
         if (!ctx) fail("null ctx");
-        std::lock_guard<std::mutex> g(ctx->mu);
-        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
+        if (ctx->multi())
+            return multi_key_upload(ctx, KeyPart::Fourier, [&](TfheMi355Context *s) {
+                return tfhe_mi355_bootstrap_key_fourier_set_ready(s);
+            });
+        KeyWrite kw(ctx);  // no coalesced batch in flight, none starts until done
         if (!ctx->fbsk.ptr) fail("no Fourier key buffer");
         ctx->fbsk_ready = true;
     });
@@ -1426,10 +1866,14 @@ int tfhe_mi355_bootstrap_key_fourier_set_ready(TfheMi355Context *ctx) {
 int tfhe_mi355_keyswitch_key_upload(TfheMi355Context *ctx, const uint64_t *ksk, size_t len) {
     return guarded([&] {
         if (!ctx || !ksk) fail("null argument");
-        std::lock_guard<std::mutex> g(ctx->mu);
-        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
+        if (ctx->multi())
+            return multi_key_upload(ctx, KeyPart::Ksk, [&](TfheMi355Context *s) {
+                return tfhe_mi355_keyswitch_key_upload(s, ksk, len);
+            });
+        KeyWrite kw(ctx);  // no coalesced batch in flight, none starts until done
         check(hipSetDevice(ctx->device), "hipSetDevice");
         if (len != ctx->ksk_len()) fail("keyswitching key has %zu words, expected %zu", len, ctx->ksk_len());
+        ctx->ksk_ready = false;
         ctx->ksk.reserve(len * sizeof(uint64_t));
         check(hipMemcpy(ctx->ksk.ptr, ksk, len * sizeof(uint64_t), hipMemcpyHostToDevice), "upload ksk");
         repack_ksk(ctx, ctx->stream);
@@ -1442,8 +1886,11 @@ int tfhe_mi355_keyswitch_key_upload_async(TfheMi355Context *ctx, const uint64_t 
                                           void *stream) {
     return guarded([&] {
         if (!ctx || !d_ksk) fail("null argument");
-        std::lock_guard<std::mutex> g(ctx->mu);
-        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
+        if (ctx->multi())  // d_ksk on the first device
+            return multi_key_upload(ctx, KeyPart::Ksk, [&](TfheMi355Context *s) {
+                return tfhe_mi355_keyswitch_key_upload_async(s, d_ksk, len, stream);
+            });
+        KeyWrite kw(ctx);  // no coalesced batch in flight, none starts until done
         check(hipSetDevice(ctx->device), "hipSetDevice");
         if (len != ctx->ksk_len()) fail("keyswitching key has %zu words, expected %zu", len, ctx->ksk_len());
         ctx->ksk.reserve(len * sizeof(uint64_t));
@@ -1461,9 +1908,17 @@ int tfhe_mi355_keyswitch_key_device(TfheMi355Context *ctx, void **d_ptr, size_t 
         if (!ctx || !d_ptr || !bytes) fail("null argument");
         *d_ptr = nullptr;
         *bytes = 0;
-        std::lock_guard<std::mutex> g(ctx->mu);
-        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
+        if (ctx->multi()) {  // the first device's buffer; _set_ready replicates it
+            auto w = key_write_all(ctx);
+            set_ready_all(ctx, KeyPart::Ksk, false);
+            abi(tfhe_mi355_keyswitch_key_device(ctx->shards[0], d_ptr, bytes));
+            return;
+        }
+        KeyWrite kw(ctx);  // no coalesced batch in flight, none starts until done
         check(hipSetDevice(ctx->device), "hipSetDevice");
+        // about to be written by the caller: keyswitches fail until _set_ready (see above)
+        ctx->ksk_ready = false;
+        ctx->ksk_planes_ready = false;
         ctx->ksk.reserve(ctx->ksk_len() * sizeof(uint64_t));
         *d_ptr = ctx->ksk.ptr;
         *bytes = ctx->ksk_len() * sizeof(uint64_t);
@@ -1473,8 +1928,11 @@ int tfhe_mi355_keyswitch_key_device(TfheMi355Context *ctx, void **d_ptr, size_t 
 int tfhe_mi355_keyswitch_key_set_ready(TfheMi355Context *ctx) {
     return guarded([&] {
         if (!ctx) fail("null ctx");
-        std::lock_guard<std::mutex> g(ctx->mu);
-        std::unique_lock<std::shared_mutex> keys(ctx->keys_mu);  // no coalesced batch in flight
+        if (ctx->multi())
+            return multi_key_upload(ctx, KeyPart::Ksk, [&](TfheMi355Context *s) {
+                return tfhe_mi355_keyswitch_key_set_ready(s);
+            });
+        KeyWrite kw(ctx);  // no coalesced batch in flight, none starts until done
         if (!ctx->ksk.ptr) fail("no keyswitching key buffer");
         check(hipSetDevice(ctx->device), "hipSetDevice");
         repack_ksk(ctx, ctx->stream);
@@ -1488,6 +1946,16 @@ int tfhe_mi355_programmable_bootstrap(TfheMi355Context *ctx, const uint64_t *lwe
                                       size_t count) {
     return guarded([&] {
         if (!ctx || (!lwe_in && count) || (!lwe_out && count) || !luts) fail("null argument");
+        if (ctx->multi()) {
+            const size_t wi = ctx->n() + 1, wo = ctx->big_dim() + 1;
+            if (coalescible(count))
+                return abi(tfhe_mi355_programmable_bootstrap(pick_shard(ctx), lwe_in, lwe_out, luts, lut_count,
+                                                             lut_indexes, count));
+            return split_rows(ctx, count, [&](TfheMi355Context *s, size_t a, size_t n) {
+                return tfhe_mi355_programmable_bootstrap(s, lwe_in + a * wi, lwe_out + a * wo, luts, lut_count,
+                                                         lut_indexes ? lut_indexes + a : nullptr, n);
+            });
+        }
         check(hipSetDevice(ctx->device), "hipSetDevice");
         require_fbsk(ctx);
         if (lut_count == 0) fail("lut_count must be >= 1");
@@ -1504,6 +1972,7 @@ int tfhe_mi355_programmable_bootstrap(TfheMi355Context *ctx, const uint64_t *lwe
 
 int tfhe_mi355_programmable_bootstrap_scratch(TfheMi355Context *ctx, size_t count, size_t *bytes) {
     return guarded([&] {
+        ctx = primary(ctx);  // device pointers: the first device's shard
         if (!ctx || !bytes) fail("null argument");
         *bytes = pbs_scratch_bytes(ctx, count);
     });
@@ -1513,6 +1982,7 @@ int tfhe_mi355_programmable_bootstrap_async(TfheMi355Context *ctx, const uint64_
                                             const uint64_t *d_luts, size_t lut_count, const uint32_t *d_idx,
                                             size_t count, void *d_scratch, size_t scratch_bytes, void *stream) {
     return guarded([&] {
+        ctx = primary(ctx);  // device pointers: the first device's shard
         if (!ctx || (!d_in && count) || (!d_out && count) || !d_luts) fail("null argument");
         check(hipSetDevice(ctx->device), "hipSetDevice");
         // the scratch query is the contract: the persistent grid's ticket word at the classic
@@ -1528,6 +1998,11 @@ int tfhe_mi355_blind_rotate(TfheMi355Context *ctx, const uint64_t *lwe_in, uint6
                             size_t lut_count, const uint32_t *lut_indexes, size_t count) {
     return guarded([&] {
         if (!ctx || (!lwe_in && count) || (!glwe_out && count) || !luts) fail("null argument");
+        if (ctx->multi())
+            return split_rows(ctx, count, [&](TfheMi355Context *s, size_t a, size_t n) {
+                return tfhe_mi355_blind_rotate(s, lwe_in + a * (ctx->n() + 1), glwe_out + a * ctx->glwe_len(), luts,
+                                               lut_count, lut_indexes ? lut_indexes + a : nullptr, n);
+            });
         std::lock_guard<std::mutex> g(ctx->mu);
         check(hipSetDevice(ctx->device), "hipSetDevice");
         require_fbsk(ctx);
@@ -1543,6 +2018,7 @@ int tfhe_mi355_blind_rotate_async(TfheMi355Context *ctx, const uint64_t *d_in, u
                                   const uint64_t *d_luts, size_t lut_count, const uint32_t *d_lut_indexes,
                                   size_t count, void *stream) {
     return guarded([&] {
+        ctx = primary(ctx);  // device pointers: the first device's shard
         if (!ctx || (!d_in && count) || (!d_glwe_out && count) || !d_luts) fail("null argument");
         check(hipSetDevice(ctx->device), "hipSetDevice");
         launch_pbs_dev(ctx, d_in, d_glwe_out, d_luts, lut_count, d_lut_indexes, count, nullptr, 0,
@@ -1555,7 +2031,12 @@ int tfhe_mi355_packing_keyswitch_key_upload(TfheMi355Context *ctx, const uint64_
     return guarded([&] {
         if (!ctx || !pksk) fail("null argument");
         if (level == 0 || base_log == 0 || base_log * level >= 64) fail("invalid packing ks decomposition");
-        std::lock_guard<std::mutex> g(ctx->mu);
+        if (ctx->multi()) {  // a gadget-layer key: uploaded to every device from the host
+            auto w = key_write_all(ctx);
+            for (auto *s : ctx->shards) abi(tfhe_mi355_packing_keyswitch_key_upload(s, pksk, len, base_log, level));
+            return;
+        }
+        KeyWrite kw(ctx);
         check(hipSetDevice(ctx->device), "hipSetDevice");
         if (len != ctx->pksk_len(level))
             fail("packing keyswitching key has %zu words, expected %zu", len, ctx->pksk_len(level));
@@ -1580,6 +2061,10 @@ int tfhe_mi355_packing_keyswitch_key_upload(TfheMi355Context *ctx, const uint64_
 int tfhe_mi355_packing_keyswitch(TfheMi355Context *ctx, const uint64_t *lwe_in, uint64_t *glwe_out, size_t count) {
     return guarded([&] {
         if (!ctx || (!lwe_in && count) || (!glwe_out && count)) fail("null argument");
+        if (ctx->multi())
+            return split_rows(ctx, count, [&](TfheMi355Context *s, size_t a, size_t n) {
+                return tfhe_mi355_packing_keyswitch(s, lwe_in + a * (ctx->big_dim() + 1), glwe_out + a * ctx->glwe_len(), n);
+            });
         std::lock_guard<std::mutex> g(ctx->mu);
         check(hipSetDevice(ctx->device), "hipSetDevice");
         if (!ctx->pksk_ready) fail("packing keyswitching key not uploaded");
@@ -1590,6 +2075,7 @@ int tfhe_mi355_packing_keyswitch(TfheMi355Context *ctx, const uint64_t *lwe_in, 
 
 int tfhe_mi355_packing_keyswitch_scratch(TfheMi355Context *ctx, size_t count, size_t *bytes) {
     return guarded([&] {
+        ctx = primary(ctx);  // device pointers: the first device's shard
         if (!ctx || !bytes) fail("null argument");
         std::lock_guard<std::mutex> g(ctx->mu);
         if (!ctx->pksk_ready) fail("packing keyswitching key not uploaded: its decomposition sizes the scratch");
@@ -1600,6 +2086,7 @@ int tfhe_mi355_packing_keyswitch_scratch(TfheMi355Context *ctx, size_t count, si
 int tfhe_mi355_packing_keyswitch_async(TfheMi355Context *ctx, const uint64_t *d_lwe_in, uint64_t *d_glwe_out,
                                        size_t count, void *d_scratch, size_t scratch_bytes, void *stream) {
     return guarded([&] {
+        ctx = primary(ctx);  // device pointers: the first device's shard
         if (!ctx || (!d_lwe_in && count) || (!d_glwe_out && count)) fail("null argument");
         check(hipSetDevice(ctx->device), "hipSetDevice");
         launch_packing_ks_dev(ctx, d_lwe_in, d_glwe_out, count, d_scratch, scratch_bytes, (hipStream_t)stream);
@@ -1610,6 +2097,13 @@ int tfhe_mi355_glwe_poly_mul(TfheMi355Context *ctx, const uint64_t *glwe_in, siz
                              const uint64_t *polys, size_t npoly, size_t count, int extract, uint64_t *out) {
     return guarded([&] {
         if (!ctx || (!glwe_in && count) || (!polys && npoly) || (!out && count && npoly)) fail("null argument");
+        if (ctx->multi()) {
+            const size_t wo = npoly * (extract ? ctx->big_dim() + 1 : ctx->glwe_len());
+            return split_rows(ctx, count, [&](TfheMi355Context *s, size_t a, size_t n) {
+                return tfhe_mi355_glwe_poly_mul(s, glwe_in + a * glwe_per_item * ctx->glwe_len(), glwe_per_item, polys,
+                                                npoly, n, extract, out + a * wo);
+            });
+        }
         std::lock_guard<std::mutex> g(ctx->mu);
         check(hipSetDevice(ctx->device), "hipSetDevice");
         if (count == 0 || npoly == 0) return;
@@ -1634,6 +2128,7 @@ int tfhe_mi355_glwe_poly_mul_async(TfheMi355Context *ctx, const uint64_t *d_glwe
                                    const uint64_t *d_polys, size_t npoly, size_t count, int extract,
                                    uint64_t *d_out, void *stream) {
     return guarded([&] {
+        ctx = primary(ctx);  // device pointers: the first device's shard
         if (!ctx || (!d_glwe_in && count) || (!d_polys && npoly) || (!d_out && count && npoly))
             fail("null argument");
         check(hipSetDevice(ctx->device), "hipSetDevice");
@@ -1646,6 +2141,13 @@ int tfhe_mi355_glwe_poly_mul_async(TfheMi355Context *ctx, const uint64_t *d_glwe
 int tfhe_mi355_keyswitch(TfheMi355Context *ctx, const uint64_t *lwe_in, uint64_t *lwe_out, size_t count) {
     return guarded([&] {
         if (!ctx || (!lwe_in && count) || (!lwe_out && count)) fail("null argument");
+        if (ctx->multi()) {
+            const size_t wi = ctx->big_dim() + 1, wo = ctx->n() + 1;
+            if (coalescible(count)) return abi(tfhe_mi355_keyswitch(pick_shard(ctx), lwe_in, lwe_out, count));
+            return split_rows(ctx, count, [&](TfheMi355Context *s, size_t a, size_t n) {
+                return tfhe_mi355_keyswitch(s, lwe_in + a * wi, lwe_out + a * wo, n);
+            });
+        }
         check(hipSetDevice(ctx->device), "hipSetDevice");
         require_ksk(ctx);
         if (coalescible(count)) {
@@ -1660,6 +2162,7 @@ int tfhe_mi355_keyswitch(TfheMi355Context *ctx, const uint64_t *lwe_in, uint64_t
 
 int tfhe_mi355_keyswitch_scratch(TfheMi355Context *ctx, size_t count, size_t *bytes) {
     return guarded([&] {
+        ctx = primary(ctx);  // device pointers: the first device's shard
         if (!ctx || !bytes) fail("null argument");
         std::lock_guard<std::mutex> g(ctx->mu);
         *bytes = ks_scratch_bytes(ctx, count);
@@ -1669,6 +2172,7 @@ int tfhe_mi355_keyswitch_scratch(TfheMi355Context *ctx, size_t count, size_t *by
 int tfhe_mi355_keyswitch_async(TfheMi355Context *ctx, const uint64_t *d_in, uint64_t *d_out, size_t count,
                                void *d_scratch, size_t scratch_bytes, void *stream) {
     return guarded([&] {
+        ctx = primary(ctx);  // device pointers: the first device's shard
         if (!ctx || (!d_in && count) || (!d_out && count)) fail("null argument");
         check(hipSetDevice(ctx->device), "hipSetDevice");
         launch_ks_dev(ctx, d_in, d_out, count, d_scratch, scratch_bytes, (hipStream_t)stream);
@@ -1677,6 +2181,7 @@ int tfhe_mi355_keyswitch_async(TfheMi355Context *ctx, const uint64_t *d_in, uint
 
 int tfhe_mi355_keyswitch_programmable_bootstrap_scratch(TfheMi355Context *ctx, size_t count, size_t *bytes) {
     return guarded([&] {
+        ctx = primary(ctx);  // device pointers: the first device's shard
         if (!ctx || !bytes) fail("null argument");
         std::lock_guard<std::mutex> g(ctx->mu);
         *bytes = ks_pbs_scratch_bytes(ctx, count);
@@ -1688,6 +2193,7 @@ int tfhe_mi355_keyswitch_programmable_bootstrap_async(TfheMi355Context *ctx, con
                                                       const uint32_t *d_idx, size_t count, void *d_scratch,
                                                       size_t scratch_bytes, void *stream) {
     return guarded([&] {
+        ctx = primary(ctx);  // device pointers: the first device's shard
         if (!ctx || (!d_in && count) || (!d_out && count) || !d_luts || (!d_scratch && count))
             fail("null argument");
         check(hipSetDevice(ctx->device), "hipSetDevice");
@@ -1701,6 +2207,15 @@ int tfhe_mi355_keyswitch_programmable_bootstrap(TfheMi355Context *ctx, const uin
                                                 const uint32_t *lut_indexes, size_t count) {
     return guarded([&] {
         if (!ctx || (!lwe_in && count) || (!lwe_out && count) || !luts) fail("null argument");
+        if (ctx->multi()) {
+            const size_t wi = ctx->big_dim() + 1, wo = ctx->big_dim() + 1;
+            if (coalescible(count))
+                return abi(tfhe_mi355_keyswitch_programmable_bootstrap(pick_shard(ctx), lwe_in, lwe_out, luts, lut_count, lut_indexes, count));
+            return split_rows(ctx, count, [&](TfheMi355Context *s, size_t a, size_t n) {
+                return tfhe_mi355_keyswitch_programmable_bootstrap(s, lwe_in + a * wi, lwe_out + a * wo, luts, lut_count,
+                            lut_indexes ? lut_indexes + a : nullptr, n);
+            });
+        }
         check(hipSetDevice(ctx->device), "hipSetDevice");
         require_fbsk(ctx);
         require_ksk(ctx);
@@ -1718,6 +2233,7 @@ int tfhe_mi355_keyswitch_programmable_bootstrap(TfheMi355Context *ctx, const uin
 
 int tfhe_mi355_programmable_bootstrap_keyswitch_scratch(TfheMi355Context *ctx, size_t count, size_t *bytes) {
     return guarded([&] {
+        ctx = primary(ctx);  // device pointers: the first device's shard
         if (!ctx || !bytes) fail("null argument");
         std::lock_guard<std::mutex> g(ctx->mu);
         *bytes = pbs_ks_scratch_bytes(ctx, count);
@@ -1729,6 +2245,7 @@ int tfhe_mi355_programmable_bootstrap_keyswitch_async(TfheMi355Context *ctx, con
                                                       const uint32_t *d_idx, size_t count, void *d_scratch,
                                                       size_t scratch_bytes, void *stream) {
     return guarded([&] {
+        ctx = primary(ctx);  // device pointers: the first device's shard
         if (!ctx || (!d_in && count) || (!d_out && count) || !d_luts || (!d_scratch && count))
             fail("null argument");
         check(hipSetDevice(ctx->device), "hipSetDevice");
@@ -1742,6 +2259,15 @@ int tfhe_mi355_programmable_bootstrap_keyswitch(TfheMi355Context *ctx, const uin
                                                 const uint32_t *lut_indexes, size_t count) {
     return guarded([&] {
         if (!ctx || (!lwe_in && count) || (!lwe_out && count) || !luts) fail("null argument");
+        if (ctx->multi()) {
+            const size_t wi = ctx->n() + 1, wo = ctx->n() + 1;
+            if (coalescible(count))
+                return abi(tfhe_mi355_programmable_bootstrap_keyswitch(pick_shard(ctx), lwe_in, lwe_out, luts, lut_count, lut_indexes, count));
+            return split_rows(ctx, count, [&](TfheMi355Context *s, size_t a, size_t n) {
+                return tfhe_mi355_programmable_bootstrap_keyswitch(s, lwe_in + a * wi, lwe_out + a * wo, luts, lut_count,
+                            lut_indexes ? lut_indexes + a : nullptr, n);
+            });
+        }
         check(hipSetDevice(ctx->device), "hipSetDevice");
         require_fbsk(ctx);
         require_ksk(ctx);
@@ -1760,6 +2286,7 @@ int tfhe_mi355_programmable_bootstrap_keyswitch(TfheMi355Context *ctx, const uin
 int tfhe_mi355_lwe_scalar_mul_add_async(TfheMi355Context *ctx, uint64_t *d_y, const uint64_t *d_x, uint64_t scalar,
                                         size_t rows, size_t words, size_t y_stride, size_t x_stride, void *stream) {
     return guarded([&] {
+        ctx = primary(ctx);  // device pointers: the first device's shard
         if (!ctx || (!d_y && rows * words)) fail("null argument");
         if (words > y_stride || (d_x && words > x_stride)) fail("row stride smaller than the row");
         check(hipSetDevice(ctx->device), "hipSetDevice");
@@ -1771,6 +2298,7 @@ int tfhe_mi355_lwe_scalar_mul_add_async(TfheMi355Context *ctx, uint64_t *d_y, co
 int tfhe_mi355_trivial_pbs_async(TfheMi355Context *ctx, uint64_t *d_body, size_t rows, size_t stride,
                                  const uint64_t *d_lut, void *stream) {
     return guarded([&] {
+        ctx = primary(ctx);  // device pointers: the first device's shard
         if (!ctx || ((!d_body || !d_lut) && rows)) fail("null argument");
         const uint64_t msup = (uint64_t)ctx->p.message_modulus * ctx->p.carry_modulus;
         if (msup == 0 || ctx->N() % msup) fail("message space does not divide the polynomial size");

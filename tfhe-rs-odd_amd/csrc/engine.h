@@ -5,11 +5,20 @@
 #include <stdint.h>
 
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
 
+struct TfheMi355Context;  // include/tfhe_mi355.h (opaque there), capi.cpp
+
 namespace tfhe_mi355 {
+
+// Key transaction (capi.cpp): holds the context's key locks (every shard's, for a multi-device
+// context) exclusively until the returned holder is released.  Key uploads made from this thread in
+// the meantime skip their own locking, so a multi-call upload (serde.cpp: keyswitching key, Fourier
+// buffer, ready flag) is seen by coalesced batches only as a whole.
+std::shared_ptr<void> begin_key_transaction(TfheMi355Context *ctx);
 
 // Per-kernel durations measured on the launch stream (a profiling aid, off unless enabled through
 // tfhe_mi355_kernel_timing_enable): the launchers bracket every `every`-th launch of a kernel

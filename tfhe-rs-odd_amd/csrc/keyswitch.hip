@@ -174,8 +174,10 @@ __global__ void __launch_bounds__(256) ks_mfma_kernel(KeyswitchLaunch a, const i
         for (int q = 0; q < 16; q++) acc[b][q] = 0;
     // split K (gridDim.z > 1, small batches): slice z of the rows, the partial products combined by
     // 64-bit atomic adds into an output zeroed beforehand (sums mod 2^64: order-independent, exact)
-    const size_t kslice = mpad / gridDim.z / 32 * 32;  // whole 32-row steps; the last slice takes the rest
-    const size_t kbeg = kslice * blockIdx.z, kend = blockIdx.z + 1 == gridDim.z ? mpad : kbeg + kslice;
+    // whole 32-row steps spread evenly (slices differ by at most one step: the critical path is the
+    // longest slice)
+    const size_t steps = mpad / 32;
+    const size_t kbeg = 32 * (steps * blockIdx.z / gridDim.z), kend = 32 * (steps * (blockIdx.z + 1) / gridDim.z);
     // digit rows past the batch (the tile's padding) read as zero: no memset of the scratch
     const bool arow = c0 + r < a.count;
     for (size_t k = kbeg; k < kend; k += 32) {
@@ -253,6 +255,7 @@ hipError_t launch_keyswitch_mfma(const KeyswitchLaunch &a, const int8_t *kt, voi
         const long v = e ? std::atol(e) : 0;
         return v > 0 ? (unsigned)v : 1024u;
     }();
+    // (mpad is a multiple of 32: mpad / 64 slices keep >= 2 k-steps each)
     if (tiles < 128) split = (unsigned)std::min<size_t>((target + tiles - 1) / tiles, mpad / 64);
     if (split < 2) split = 1;
     hipLaunchKernelGGL(ks_digits_kernel, dim3((unsigned)a.count * KS_DPARTS), dim3(256), 0, s, a, dig, rowsum, mpad,

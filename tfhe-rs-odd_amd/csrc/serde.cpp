@@ -54,6 +54,7 @@
 #include <vector>
 
 #include "../../include/tfhe_mi355.h"
+#include "engine.h"
 #include "errors.h"
 
 namespace {
@@ -419,6 +420,7 @@ int tfhe_mi355_compressed_server_key_upload(TfheMi355Context *ctx, const uint8_t
     return guarded([&] {
         if (!ctx || !bytes) fail("null argument");
         const Key k = parse_compressed(bytes, len);
+        const auto txn = tfhe_mi355::begin_key_transaction(ctx);  // both keys change as one
         TfheMi355Parameters cp;
         abi(tfhe_mi355_context_parameters(ctx, &cp));
         require_same(k.params, cp);
@@ -435,6 +437,8 @@ int tfhe_mi355_server_key_upload(TfheMi355Context *ctx, const uint8_t *bytes, si
     return guarded([&] {
         if (!ctx || !bytes) fail("null argument");
         const Key k = parse_standard(bytes, len);
+        // no coalesced batch between the keyswitching key, the Fourier buffer and its ready flag
+        const auto txn = tfhe_mi355::begin_key_transaction(ctx);
         TfheMi355Parameters cp;
         abi(tfhe_mi355_context_parameters(ctx, &cp));
         require_same(k.params, cp);

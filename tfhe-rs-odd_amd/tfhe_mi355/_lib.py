@@ -57,6 +57,10 @@ SIGNATURES = [
     ("tfhe_mi355_host_free", ctypes.c_int, [vp]),
     ("tfhe_mi355_context_create", ctypes.c_int,
      [ctypes.POINTER(TfheMi355Parameters), ctypes.c_int, ctypes.POINTER(vp)]),
+    ("tfhe_mi355_context_create_devices", ctypes.c_int,
+     [ctypes.POINTER(TfheMi355Parameters), ctypes.POINTER(ctypes.c_int), sz, ctypes.POINTER(vp)]),
+    ("tfhe_mi355_context_devices", ctypes.c_int, [vp, ctypes.POINTER(sz)]),
+    ("tfhe_mi355_context_device_context", ctypes.c_int, [vp, sz, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int)]),
     ("tfhe_mi355_context_destroy", ctypes.c_int, [vp]),
     ("tfhe_mi355_bootstrap_key_upload", ctypes.c_int, [vp, u64p, sz]),
     ("tfhe_mi355_bootstrap_key_convert_async", ctypes.c_int, [vp, vp, sz, vp]),

@@ -9,7 +9,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import TfheMi355Parameters, u32p, u64p, vp
+from ._lib import TfheMi355Parameters, sz, u32p, u64p, vp
 from .parameters import ClassicPBSParameters
 
 
@@ -75,15 +75,37 @@ def device_count() -> int:
 
 
 class Engine:
-    """MI355X PBS engine context bound to `device`."""
+    """MI355X PBS engine context bound to `device`, or -- `devices` = a list of device ordinals
+    (repeats allowed; [] = every visible GPU) -- one context over several GPUs of this process
+    (tfhe_mi355_context_create_devices): keys replicated from the first device, batched calls split
+    over the devices, small calls and submits spread round robin; device-tensor (async) calls run on
+    the first device."""
 
-    def __init__(self, params: ClassicPBSParameters, device: int = 0):
+    def __init__(self, params: ClassicPBSParameters, device: int = 0, devices=None):
         self.params = params
-        self.device = device
         self._cp = c_params(params)
         h = vp()
-        _lib.call("tfhe_mi355_context_create", ctypes.byref(self._cp), device, ctypes.byref(h))
+        if devices is None:
+            self.device = device
+            _lib.call("tfhe_mi355_context_create", ctypes.byref(self._cp), device, ctypes.byref(h))
+        else:
+            arr = (ctypes.c_int * max(len(devices), 1))(*devices)
+            _lib.call("tfhe_mi355_context_create_devices", ctypes.byref(self._cp), arr, len(devices),
+                      ctypes.byref(h))
         self._h = h
+        if devices is not None:
+            self.device = self.device_ordinals()[0]
+
+    def device_ordinals(self) -> list:
+        """Device ordinal of each shard (one entry for a single-device context)."""
+        n = sz()
+        _lib.call("tfhe_mi355_context_devices", self._h, ctypes.byref(n))
+        out = []
+        for i in range(n.value):
+            sub, dev = vp(), ctypes.c_int()
+            _lib.call("tfhe_mi355_context_device_context", self._h, i, ctypes.byref(sub), ctypes.byref(dev))
+            out.append(dev.value)
+        return out
 
     # -- lifetime ---------------------------------------------------------------------
     def close(self):
