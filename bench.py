@@ -506,15 +506,18 @@ def launch_ranks(args) -> int:
 # (entry name, --params, extra options).  `4_4_full` is config 3 at its stated size (65,536
 # ciphertexts in one call, a GLOBAL batch: split over the ranks at N > 1, i.e. strong scaling for
 # that entry), warmed up on its first 1024 ciphertexts.
+# `callers`: the entry also measures the reference's calling pattern (one ciphertext per blocking
+# call from 1 / 64 / 256 native threads, and 256 submitted requests from one thread), every row
+# checked against a batched call (bench.py --callers-only).
 OTHER_WORKLOADS = (
-    ("2_2ks", "2_2ks", {"steps": 3}),
-    ("mb3", "mb3", {"steps": 3}),
+    ("2_2ks", "2_2ks", {"steps": 3, "callers": True}),
+    ("mb3", "mb3", {"steps": 3, "callers": True}),
     ("mb2", "mb2", {"steps": 3}),
     ("4_4", "4_4", {"steps": 3}),
     ("mul32", "mul32", {"steps": 2}),
     ("4_4_full", "4_4", {"steps": 1, "global_batch": 65536, "warmup_batch": 1024}),
-    ("3_3", "3_3", {"steps": 3}),
-    ("mb3_3g3", "mb3_3g3", {"steps": 3}),
+    ("3_3", "3_3", {"steps": 3, "callers": True}),
+    ("mb3_3g3", "mb3_3g3", {"steps": 3, "callers": True}),
 )
 # Wall-clock budget of one such workload (keys, warm-up, steps, checks).  N = 1: the child's
 # subprocess timeout; N > 1: a per-rank watchdog (below).  BENCH_WORKLOAD_BUDGET_S overrides.
@@ -525,20 +528,59 @@ def workload_budget() -> float:
     return float(os.environ.get("BENCH_WORKLOAD_BUDGET_S", WORKLOAD_BUDGET_S))
 
 
+def callers_summary(host_abi: dict | None) -> dict | None:
+    """Compact form of host_abi.single_ct: calls/s at 1 / 16 / 64 / 256 blocking callers and of the
+    submitted windows, with the total of rows that differed from the batched call."""
+    sct = (host_abi or {}).get("single_ct")
+    if not sct:
+        return None
+    out = {f"callers_{t}": round(v["value"], 1) for t, v in sct.get("callers", {}).items()}
+    out.update({f"submit_{w}": round(v["value"], 1) for w, v in sct.get("submit_wait", {}).items()})
+    if "64" in sct.get("callers", {}):
+        out["callers_64_frac_of_batched"] = round(sct["callers"]["64"]["frac_of_batched_device_rate"], 3)
+    out["mismatching_rows"] = int(sum(v["mismatching_rows"] + v["failed_calls"]
+                                      for grp in ("callers", "submit_wait") for v in sct.get(grp, {}).values()))
+    return out
+
+
 def summarize(line: dict) -> dict:
     rl = line.get("roofline") or {}
-    return {"value": line["value"], "unit": line["unit"], "ms_per_step": line["ms_per_step"],
-            "steps": line["steps"], "n_gpus": line["n_gpus"], "world_size": line.get("world_size"),
-            "scaling": line.get("scaling"), "workload": line["config"]["workload"],
-            "batch": line["config"].get("global_batch", line["config"].get("global_pairs")),
-            "kernel": rl.get("kernel"), "bound": rl.get("bound"), "frac": rl.get("frac"),
-            "check": line.get("check"), "setup": line.get("setup"),
-            "single_call_latency_ms": line.get("single_call_latency_ms")}
+    out = {"value": line["value"], "unit": line["unit"], "ms_per_step": line["ms_per_step"],
+           "steps": line["steps"], "n_gpus": line["n_gpus"], "world_size": line.get("world_size"),
+           "scaling": line.get("scaling"), "workload": line["config"]["workload"],
+           "batch": line["config"].get("global_batch", line["config"].get("global_pairs")),
+           "kernel": rl.get("kernel"), "bound": rl.get("bound"), "frac": rl.get("frac"),
+           "check": line.get("check"), "setup": line.get("setup"),
+           "single_call_latency_ms": line.get("single_call_latency_ms")}
+    cs = callers_summary(line.get("host_abi"))
+    if cs:
+        out["callers"] = cs
+    return out
+
+
+def compact_summary(line: dict) -> dict:
+    """One short entry per workload (value, roofline frac, one-call latency, 1 / 64 / 256 blocking
+    callers, 256 submitted, rows that differed), printed as the LAST key of the JSON line and on
+    stderr, so that a tail of the output keeps every configuration's numbers."""
+    def one(e):
+        c = e.get("callers") or {}
+        pairs = (("v", round(e["value"], 1) if e.get("value") is not None else None),
+                 ("frac", round(e["frac"], 3) if e.get("frac") is not None else None),
+                 ("lat_ms", round(e["single_call_latency_ms"], 2) if e.get("single_call_latency_ms") is not None
+                  else None),
+                 ("c1", c.get("callers_1")), ("c64", c.get("callers_64")), ("c256", c.get("callers_256")),
+                 ("s1x256", c.get("submit_1x256")), ("bad", c.get("mismatching_rows")))
+        return {k: v for k, v in pairs if v is not None}
+    out = {"2_2": one(summarize(line))}
+    for k, v in (line.get("other_workloads") or {}).items():
+        out[k] = one(v) if "error" not in v else {"error": str(v["error"])[:80]}
+    return out
 
 
 def _child_args(args, params, opts) -> list:
     a = ["--params", params, "--steps", str(opts["steps"]), "--warmup", str(opts.get("warmup", 1)),
-         "--no-cpu-baseline", "--no-host-abi", "--seed", str(args.seed)]
+         "--no-cpu-baseline", "--seed", str(args.seed)]
+    a += ["--callers-only"] if opts.get("callers") else ["--no-host-abi"]
     if opts.get("global_batch"):
         a += ["--global-batch", str(opts["global_batch"])]
     if opts.get("warmup_batch"):
@@ -767,6 +809,9 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="ciphertexts per GPU per step (default 4096; 1024 at 4_4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-abi", action="store_true", help="skip the host-pointer ABI rate")
+    ap.add_argument("--callers-only", action="store_true",
+                    help="host-pointer ABI: only the one-ciphertext-per-call leg (1 / 64 / 256 callers, 1 x 256 "
+                         "submitted), not the batched pageable / pinned rates")
     ap.add_argument("--no-single-call", action="store_true",
                     help="skip the one-ciphertext call latency (kernel traces / PMC runs of the batch)")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -816,7 +861,12 @@ def main():
                                                        emit=lambda res: print(json.dumps(merge_other(line, res)),
                                                                               flush=True)))
     if R.rank == 0:
+        if default_run:
+            line["summary"] = compact_summary(line)
         print(json.dumps(line), flush=True)
+        if default_run:
+            print("bench.py summary: " + json.dumps(line["summary"], separators=(",", ":")), file=sys.stderr,
+                  flush=True)
     R.finish()
 
 
@@ -1082,9 +1132,13 @@ def run_pbs(args, P, pname, workload, kname, R):
     # (profiling runs skip it: its count = 1 launches would mix into the per-kernel averages)
     latency = single_call_latency(eng, pname, cts, acc, with_ks) if R.rank == 0 and not args.no_single_call else None
     host_abi = None
-    if not args.no_host_abi and R.rank == 0 and P.polynomial_size <= 2048:
-        host_abi = host_abi_rate(eng, P, cts, acc, with_ks)
-        host_abi["single_ct"] = single_ct_rates(eng, cts, acc, with_ks, nb * args.steps / wall)
+    if not args.no_host_abi and R.rank == 0:
+        if args.callers_only:  # the reference's calling pattern only (other_workloads children)
+            host_abi = {"single_ct": single_ct_rates(eng, cts, acc, with_ks, nb * args.steps / wall, secs=1.5,
+                                                     callers=(1, 64, 256), submit_windows=((1, 256),))}
+        else:
+            host_abi = host_abi_rate(eng, P, cts, acc, with_ks)
+            host_abi["single_ct"] = single_ct_rates(eng, cts, acc, with_ks, nb * args.steps / wall)
 
     if R.rank == 0:
         unit = "KS+PBS/s" if with_ks else "PBS/s"

@@ -78,3 +78,23 @@ def test_mall_ceiling_is_the_committed_probe():
     best = max(float(l.split(": ")[1].split(" TB/s")[0]) for l in txt.splitlines() if "TB/s" in l and "MiB x3" in l
                and 96 <= int(l.split("working set ")[1].split(" MiB")[0]) <= 255)
     assert abs(best * 1000 - bench.MALL_STREAM_GBS) < 50
+
+
+def test_compact_summary_keeps_every_workload_and_the_callers():
+    """The default line ends with a short per-workload summary (value, frac, one-call latency,
+    64 / 256 blocking callers, mismatching rows) that a 2000-character tail of the output keeps."""
+    sct = {"callers": {t: {"value": 1000.0 * int(t), "frac_of_batched_device_rate": 0.1, "mismatching_rows": 0,
+                           "failed_calls": 0} for t in ("1", "64", "256")},
+           "submit_wait": {"1x256": {"value": 7e4, "mismatching_rows": 0, "failed_calls": 0}}}
+    head = {"value": 130000.0, "unit": "PBS/s", "ms_per_step": 31.5, "steps": 10, "n_gpus": 1,
+            "config": {"workload": "w", "global_batch": 4096}, "roofline": {"frac": 0.318},
+            "single_call_latency_ms": 2.5, "host_abi": {"single_ct": sct}}
+    child = bench.summarize(dict(head, value=6000.0, host_abi={"single_ct": sct}))
+    assert child["callers"]["callers_64"] == 64000.0 and child["callers"]["mismatching_rows"] == 0
+    line = dict(head, other_workloads={"3_3": child, "4_4": {"error": "rc=1: boom", "wall_s": 1.0}})
+    s = bench.compact_summary(line)
+    assert s["2_2"] == {"v": 130000.0, "frac": 0.318, "lat_ms": 2.5, "c1": 1000.0, "c64": 64000.0,
+                        "c256": 256000.0, "s1x256": 70000.0, "bad": 0}
+    assert s["3_3"]["v"] == 6000.0 and s["3_3"]["c64"] == 64000.0
+    assert "error" in s["4_4"]
+    assert len(json.dumps(s)) < 1500

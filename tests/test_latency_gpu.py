@@ -80,3 +80,59 @@ def test_latency_keyswitch_pbs_equals_throughput(orc, keys_2_2, eng):
     lat = eng.keyswitch_programmable_bootstrap(big[:SMALL], acc)
     assert np.array_equal(lat, thr[:SMALL])
     assert np.array_equal(decode(orc.lwe_decrypt(keys_2_2.glwe_sk, lat), p.delta) % 16, (msgs[:SMALL] + 5) % 16)
+
+
+# ---- multi-bit latency kernel (pbs_mb_latency_kernel: N = 2048, k = 1, L = 1, g = 2 / 3) ----
+
+@pytest.fixture(scope="module")
+def mb_keys(orc, keys_mb):
+    """g = 3 (BASELINE config 5's set, full n = 888) and g = 2 (n reduced to 96: the kernel does not
+    depend on n beyond the group count)."""
+    from conftest import KeySet
+    from tfhe_mi355.parameters import PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_2_KS_PBS as P2
+
+    return {3: keys_mb, 2: KeySet(orc, P2.with_(lwe_dimension=96), seed=71)}
+
+
+@pytest.mark.parametrize("g", [3, 2])
+def test_mb_latency_equals_throughput_kernel_and_oracle(orc, mb_keys, g):
+    """The same rows through the latency kernel (a batch of <= 256) and the slot-split throughput
+    kernel (inside a batch of 300), edge bodies and masks, three LUTs: every word equal; a sample of
+    rows equal to the oracle's deterministic multi-bit PBS."""
+    from tfhe_mi355 import Engine
+
+    keys = mb_keys[g]
+    e = Engine(keys.params, 0)
+    e.upload_bootstrap_key(keys.bsk)
+    fs = [lambda x: x, lambda x: (x * x) % 16, lambda x: (7 * x + 3) % 16]
+    luts = np.stack([orc.fill_accumulator(2048, 1, 4, 4, f) for f in fs])
+    cts = _edge_batch(keys, BIG, 47 + g)
+    idx = (np.arange(BIG) * 5 % 3).astype(np.uint32)
+    thr = e.programmable_bootstrap(cts, luts, lut_indexes=idx)
+    lat = e.programmable_bootstrap(cts[:SMALL], luts, lut_indexes=idx[:SMALL])
+    assert np.array_equal(lat, thr[:SMALL]), f"{np.count_nonzero(lat != thr[:SMALL])} words differ"
+    sub = np.r_[0:7, 199:200]
+    exp = keys.fbsk.pbs(cts[sub], luts, lut_idx=idx[sub], threads=16)
+    assert np.array_equal(lat[sub], exp)
+    # one ciphertext (the reference's per-call pattern) and glwe output (blind rotation)
+    assert np.array_equal(e.programmable_bootstrap(cts[5:6], luts[1]), e.programmable_bootstrap(cts[:BIG], luts[1])[5:6])
+    br_thr = e.blind_rotate(cts, luts[2])
+    assert np.array_equal(e.blind_rotate(cts[:SMALL], luts[2]), br_thr[:SMALL])
+    e.close()
+
+
+def test_mb_latency_decrypts_at_every_small_count(orc, mb_keys):
+    keys = mb_keys[3]
+    p = keys.params
+    from tfhe_mi355 import Engine
+
+    e = Engine(p, 0)
+    e.upload_bootstrap_key(keys.bsk)
+    acc = orc.fill_accumulator(2048, 1, 4, 4, lambda x: (5 * x + 2) % 16)
+    for count in (1, 3, 64, 256):
+        msgs = (np.arange(count) * 7) % 16
+        cts = orc.lwe_encrypt(600 + count, keys.lwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta),
+                              p.lwe_modular_std_dev)
+        got = e.programmable_bootstrap(cts, acc)
+        assert np.array_equal(decode(orc.lwe_decrypt(keys.glwe_sk, got), p.delta) % 16, (5 * msgs + 2) % 16)
+    e.close()

@@ -438,6 +438,12 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
         a.base_log = (int)c->p.pbs_base_log;
         a.count = (int)count;
         a.glwe_out = glwe_out;
+        if (count <= latency_max() && latency_multibit_supported((int)c->N(), (int)c->k(), (int)c->p.pbs_level,
+                                                                 (int)c->p.grouping_factor)) {
+            TimedLaunch tl(c->timer_or_null(), "pbs_mb_latency_kernel", s);
+            check(launch_latency_multibit_pbs((int)c->p.grouping_factor, a, s), "launch multi-bit latency pbs");
+            return;
+        }
         TimedLaunch tl(c->timer_or_null(), "pbs_multibit", s);
         check(launch_multibit_pbs((int)c->N(), (int)c->k(), (int)c->p.pbs_level, (int)c->p.grouping_factor, a, s),
               "launch multi-bit pbs");

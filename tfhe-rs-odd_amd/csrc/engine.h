@@ -159,6 +159,10 @@ struct MultiBitPbsLaunch {
 };
 bool multibit_pbs_supported(int N, int k, int L, int g);
 hipError_t launch_multibit_pbs(int N, int k, int L, int g, const MultiBitPbsLaunch &a, hipStream_t s);
+// latency form (pbs_latency.hip): one ciphertext per workgroup of 8 waves, keybundle built into LDS
+// beside the forward transform; same outputs.  N = 2048, k = 1, L = 1, g = 2 / 3; no scratch.
+bool latency_multibit_supported(int N, int k, int L, int g);
+hipError_t launch_latency_multibit_pbs(int g, const MultiBitPbsLaunch &a, hipStream_t s);
 
 // N = 32768 classic PBS: accumulator and spectra in device scratch, three launches per CMUX
 struct LargePbsLaunch {

@@ -575,6 +575,295 @@ __global__ void __launch_bounds__(512 / RPW, 2 / RPW) pbs_latency_kernel(Classic
     if (tid == 0) out[K * N] = reinterpret_cast<const uint64_t *>(lds + LatLds::Z + K * M)[0];
 }
 
+// ---------------------------------------------------------------------------------------------
+// Multi-bit latency form (N = 2048, k = 1, L = 1, grouping g = 2, 3: the PARAM_MULTI_BIT_MESSAGE_2_
+// CARRY_2 sets, shortint/parameters/multi_bit.rs:173-190), the reference's one-ciphertext call
+// (shortint/server_key/mod.rs:829-851 -> multi_bit_programmable_bootstrap_lwe_ciphertext,
+// lwe_multi_bit_programmable_bootstrapping.rs:1035-1128, deterministic group order :548-828).
+// One ciphertext per workgroup of 8 waves with the transform split of the kernel above (LAT_MAP =
+// 1 lane mapping), the CMUX replaced by  acc <- ExtProd(KB_j, acc),  KB_j = sum_sel X^{d_sel}
+// GGSW_{j,sel}  (prepare_multi_bit_ggsw_mem_optimized :18-84, update_with_fmadd_factor ggsw.rs:
+// 699-754).  The keybundle does not depend on the accumulator, so it is built into LDS by all 512
+// lanes -- each lane two frequencies of all four (row, column) polynomials, its GGSW operands read
+// coalesced (1 KiB per wave instruction) in the engine layout -- while the forward transform of the
+// same group runs; the MAC lanes read it back by position after the stage-2 barrier.  No rotation
+// (ct1 = acc), so a group has two workgroup barriers: stage 2 -> MAC (C, which also publishes the
+// keybundle) and inverse stage 3 -> 2 (E); the backward conversion overwrites the accumulator (the
+// reference's zeroed ping-pong destination).  Keybundle in selector order with the fma forms of
+// pbs_multibit.hip and the oracle's mb_keybundle, MAC over rows in order: outputs bit-identical to
+// the throughput kernels and to oracle/pbs_oracle.c.
+// ---------------------------------------------------------------------------------------------
+namespace {
+// LDS (double2 units): twist planes (TwistLds<1024>: re [M] doubles | im [M] doubles, at byte 0
+// for its address-free monomial reads) | X [2 rows][M] | Y [2 rows][M] | keybundle [row][col][M]
+// (the accumulator pairs for the sample extraction reuse it at the end)
+struct MbLatLds {
+    static constexpr int TW = 0;
+    static constexpr int X = LAT_M;
+    static constexpr int Y = X + 2 * LAT_M;
+    static constexpr int KB = Y + 2 * LAT_M;
+    static constexpr int end = KB + 4 * LAT_M;
+    static constexpr size_t bytes = sizeof(double2) * end;
+};
+static_assert(MbLatLds::bytes <= 160 * 1024, "multi-bit latency PBS LDS exceeds a CU");
+// keybundle slot of engine element E (written by consecutive lanes, read by the MAC blocks:
+// bit 2 ^= bit 4 spreads a MAC read group's 8 lanes over 8 distinct 16-byte slots mod 8)
+__device__ __forceinline__ int kswz(int E) { return E ^ ((E >> 2) & 4); }
+}  // namespace
+
+#ifndef MBL_WINDOW
+#define MBL_WINDOW 2  // keybundle elements whose GGSW loads may be in flight at once (register bound)
+#endif
+
+template <int G>
+__global__ void __launch_bounds__(512, 2) pbs_mb_latency_kernel(MultiBitPbsLaunch a) {
+    constexpr int N = LAT_N, M = LAT_M, K = 1, LOG2N = 11, NSEL = 1 << G;
+    static_assert(LAT_MAP == 1, "written for the three-barrier lane mapping");
+    using Tw = TwistLds<M>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double2 *lds = reinterpret_cast<double2 *>(smem);
+    const int tid = threadIdx.x;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int row0 = wid >> 2;  // this wave's GLWE row (transforms) and output column (MAC)
+    const int w = wid & 3;      // quarter of the row's transform
+    const int lane0 = tid & 63;
+
+    Tw::fill(reinterpret_cast<double *>(lds + MbLatLds::TW), a.twist, tid, blockDim.x);
+    cx tw1[4], tw2[4], tws[4];
+    const RowTwF rtf(lane0 >> 4, false), rti(lane0 >> 4, true);
+    {
+        const int lrow = lane0 >> 4, col = lane0 & 15, a1 = lat_a1(w, col), a2 = lat_a2(w, col);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int C = lrow + 4 * q;
+            tw1[q] = ld2(a.W + a1 * C);
+            tw2[q] = ld2(a.W + 16 * a2 * C);
+            tws[q] = ld2(a.twist + a1 + 64 * C);
+        }
+    }
+
+    const int ct = blockIdx.x;
+    const int n = a.n, groups = n / G;
+    const uint64_t *in = a.lwe_in + (size_t)ct * (n + 1);
+    const __attribute__((address_space(4))) uint64_t *in_s = (const __attribute__((address_space(4))) uint64_t *)(
+        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)in >> 32)) << 32) |
+        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)in));
+    const uint32_t li = a.lut_indexes ? min(a.lut_indexes[ct], a.lut_count - 1u) : 0u;
+    const DigitL1 digit_l1(a.base_log);
+
+    // acc = LUT / X^{b~} (:372-389): this lane's pairs j_q = a1 + 64 (lrow + 4 q), j_q + M of row row0
+    uint64_t lo[4], hi[4];
+    {
+        const uint32_t bt = pbs_modulus_switch<LOG2N>(in[n]);
+        const int full = bt / N, rem = bt % N;
+        const uint64_t *lut = a.luts + (size_t)li * (K + 1) * N + (size_t)row0 * N;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int j = lat_a1(w, lane0 & 15) + 64 * (lane0 >> 4) + 256 * q;
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int src = j + h * M + rem;
+                const bool wrap = src >= N;
+                const uint64_t v = lut[wrap ? src - N : src];
+                const uint64_t c = (wrap != (bool)(full & 1)) ? 0 - v : v;
+                (h ? hi : lo)[q] = c;
+            }
+        }
+    }
+    auto Xr = [&](int r) { return lds + MbLatLds::X + r * M; };
+    auto Yr = [&](int r) { return lds + MbLatLds::Y + r * M; };
+    double2 *kbl = lds + MbLatLds::KB;
+    constexpr size_t ggsw_len = (size_t)(K + 1) * (K + 1) * M;
+    const __amdgpu_buffer_rsrc_t gres = make_rsrc(a.fbsk);
+    // keybundle elements of this lane: E = tid and tid + 512, frequency fl + freq_slot(wid) (+ 32)
+    // (element s 64 + lane of WaveFft<1024>'s engine layout, s = wid and wid + 8)
+    const int32_t kf0 = (int32_t)(WaveFft<M>::freq_lane(lane0) + WaveFft<M>::freq_slot(wid));
+    const double k32 = torus_k32();
+    __syncthreads();  // twist planes
+
+    for (int j = 0; j < groups; j++) {
+        int lane = lane0;
+        asm volatile("" : "+v"(lane));
+        const int lrow = lane >> 4, col = lane & 15;
+        const int ccm = 4 * w + (col & 3), xm = col >> 2;
+
+        // ---- keybundle of group j into LDS (every lane; independent of the accumulator) ----
+        {
+            int32_t dd[NSEL];  // monomial degrees of the 2^g - 1 non-constant GGSWs (:700-716), SGPRs
+            {
+                uint64_t av[G];
+#pragma unroll
+                for (int i = 0; i < G; i++) av[i] = in_s[j * G + i];
+#pragma unroll
+                for (int sel = 1; sel < NSEL; sel++) {
+                    uint64_t deg = 0;
+#pragma unroll
+                    for (int i = 0; i < G; i++)
+                        if ((sel >> (G - 1 - i)) & 1) deg += av[i];
+                    dd[sel] = (int32_t)pbs_modulus_switch<LOG2N>(deg);  // <= 2N
+                }
+            }
+            uint32_t loff = 16u * (uint32_t)tid;
+            const uint32_t goff = (uint32_t)((size_t)j * NSEL * ggsw_len * 16);  // < 2^31 (MB-BSK bytes)
+            double dep = 0.0;
+            double depq[MBL_WINDOW];
+#pragma unroll
+            for (int q = 0; q < MBL_WINDOW; q++) depq[q] = 0.0;
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                // t = d (1 - 4 f) mod 2N as a 24-bit signed product (|1 - 4 f| < 2^12, d <= 2^12)
+                const int32_t wf = 1 - 4 * (kf0 + 32 * h);
+                cx mono[NSEL];
+#pragma unroll
+                for (int sel = 1; sel < NSEL; sel++) mono[sel] = Tw::mono((uint32_t)__mul24(dd[sel], wf));
+#pragma unroll
+                for (int p = 0; p < 4; p++) {  // polynomial (row rr = p >> 1, column c = p & 1)
+                    const int e = 4 * h + p;
+                    // issue window: this element's loads wait (as far as the compiler knows) for the
+                    // element MBL_WINDOW back, so at most that many elements' operands are live
+                    if (e >= MBL_WINDOW) {
+                        dep = depq[e % MBL_WINDOW];
+                        asm volatile("" : "+v"(loff) : "v"(dep));
+                    }
+                    const uint32_t eoff = goff + (uint32_t)(((size_t)p * M + (size_t)h * 512) * 16);
+                    double2 kb = buffer_ld_d2(gres, loff, eoff);
+#pragma unroll
+                    for (int sel = 1; sel < NSEL; sel++) {
+                        const double2 gg = buffer_ld_d2(gres, loff, eoff + (uint32_t)(sel * ggsw_len * 16));
+                        kb.x = fma(gg.x, mono[sel].re, fma(-gg.y, mono[sel].im, kb.x));
+                        kb.y = fma(gg.x, mono[sel].im, fma(gg.y, mono[sel].re, kb.y));
+                    }
+                    depq[e % MBL_WINDOW] = kb.x;
+                    kbl[p * M + kswz(tid + 512 * h)] = kb;
+                }
+            }
+        }
+
+        // ---- digits of the accumulator (ct1 = acc), twist, forward stage 1 (wave-private) ----
+        cx v[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int32_t d0 = digit_l1((uint32_t)(lo[q] >> 32));
+            const int32_t d1 = digit_l1((uint32_t)(hi[q] >> 32));
+            v[q] = cmulw(cx{(double)d0, (double)d1}, tws[q].re, tws[q].im);  // convert_forward_integer
+        }
+        dft16_fwd_rows_sf(v, rtf);
+        {
+            const int a1 = lat_a1(w, col);
+#pragma unroll
+            for (int q = 0; q < 4; q++) st2(Xr(row0) + lswz(a1 + 64 * (lrow + 4 * q)), cmulw(v[q], tw1[q].re, tw1[q].im));
+        }
+        WaveLocalSync{}();
+        // ---- forward stage 2 (block cc = col, butterfly a2 = w) ----
+        const int cc = lat_cc(w, col), a2 = lat_a2(w, col);
+#pragma unroll
+        for (int q = 0; q < 4; q++) v[q] = ld2(Xr(row0) + lswz(64 * cc + a2 + 4 * (lrow + 4 * q)));
+        dft16_fwd_rows_sf(v, rtf);
+#pragma unroll
+        for (int q = 0; q < 4; q++) st2(Yr(row0) + lswz(64 * cc + a2 + 4 * (lrow + 4 * q)), cmulw(v[q], tw2[q].re, tw2[q].im));
+        lds_barrier();  // (C) both rows' stage-2 outputs and the whole keybundle
+
+        // ---- stage 3 of both rows + MAC of column row0 on block t with the keybundle ----
+        const int tb = 64 * ccm + 4 * (lrow + 4 * xm);  // first position of block t
+        cx o[4];
+        {
+            cx f[K + 1][4];
+#pragma unroll
+            for (int rr = 0; rr <= K; rr++) {
+                const double2 *y = lds + MbLatLds::Y + rr * M;
+#pragma unroll
+                for (int e = 0; e < 4; e++) f[rr][e] = ld2(y + lswz(tb + e));
+                r4_fwd(f[rr][0], f[rr][1], f[rr][2], f[rr][3]);
+            }
+#pragma unroll
+            for (int rr = 0; rr <= K; rr++)
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    // position tb + e is engine element (4 lrow + e) 64 + 16 xm + ccm
+                    const double2 kb = kbl[(rr * (K + 1) + row0) * M + kswz((4 * lrow + e) * 64 + 16 * xm + ccm)];
+                    const double2 ff = make_double2(f[rr][e].re, f[rr][e].im);
+                    if (rr == 0) {  // MAC over rows (update_with_fmadd order)
+                        o[e].re = fma(kb.x, ff.x, -(kb.y * ff.y));
+                        o[e].im = fma(kb.x, ff.y, kb.y * ff.x);
+                    } else {
+                        o[e].re = fma(kb.x, ff.x, fma(-kb.y, ff.y, o[e].re));
+                        o[e].im = fma(kb.x, ff.y, fma(kb.y, ff.x, o[e].im));
+                    }
+                }
+        }
+        r4_inv(o[0], o[1], o[2], o[3]);
+#pragma unroll
+        for (int e = 0; e < 4; e++) st2(Xr(row0) + lswz(tb + e), o[e]);
+        lds_barrier();  // (E) inverse stage 2 reads one residue class of every block (all four waves)
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            v[q] = cmulw(ld2(Xr(row0) + lswz(64 * cc + a2 + 4 * (lrow + 4 * q))), tw2[q].re, -tw2[q].im);
+        dft16_inv_rows_sf(v, rti);
+        WaveLocalSync{}();
+#pragma unroll
+        for (int q = 0; q < 4; q++) st2(Xr(row0) + lswz(64 * cc + a2 + 4 * (lrow + 4 * q)), v[q]);
+        WaveLocalSync{}();
+        // ---- inverse stage 1 + backward conversion (overwrites the accumulator) ----
+        {
+            const int a1 = lat_a1(w, col);
+#pragma unroll
+            for (int q = 0; q < 4; q++) v[q] = cmulw(ld2(Xr(row0) + lswz(a1 + 64 * (lrow + 4 * q))), tw1[q].re, -tw1[q].im);
+            dft16_inv_rows_sf(v, rti);
+#pragma unroll
+            for (int q = 0; q < 4; q++) backward_convert(v[q], tws[q], lo[q], hi[q], k32);  // the key carries 1/M
+        }
+    }
+
+    // ---- output ----
+    const int lrow = lane0 >> 4, col = lane0 & 15;
+    if (a.glwe_out) {  // bootstrap_without_sample_extract (fork, bootstrap.rs:383-412)
+        uint64_t *g = a.lwe_out + ((size_t)ct * (K + 1) + row0) * N;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int jj = lat_a1(w, col) + 64 * lrow + 256 * q;
+            g[jj] = lo[q];
+            g[jj + M] = hi[q];
+        }
+        return;
+    }
+    __syncthreads();  // every wave's last keybundle reads are done: its area takes the pairs
+    uint64_t *A = reinterpret_cast<uint64_t *>(lds + MbLatLds::KB);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int jj = aswz(lat_a1(w, col) + 64 * lrow + 256 * q);
+        A[2 * (row0 * M + jj)] = lo[q];
+        A[2 * (row0 * M + jj) + 1] = hi[q];
+    }
+    __syncthreads();
+    // sample extract at degree 0 (glwe_sample_extraction.rs:91-147)
+    uint64_t *out = a.lwe_out + (size_t)ct * (K * N + 1);
+    for (int jj = tid; jj < N; jj += (int)blockDim.x) {
+        uint64_t x;
+        if (jj == 0) {
+            x = A[0];
+        } else {
+            const int src = N - jj;
+            x = 0 - A[2 * aswz(src & (M - 1)) + (src >= M)];
+        }
+        out[jj] = x;
+    }
+    if (tid == 0) out[K * N] = A[2 * M * K];
+}
+
+bool latency_multibit_supported(int N, int k, int L, int g) { return N == 2048 && k == 1 && L == 1 && (g == 2 || g == 3); }
+
+hipError_t launch_latency_multibit_pbs(int g, const MultiBitPbsLaunch &a, hipStream_t s) {
+    if (a.count <= 0) return hipSuccess;
+    if (a.n % g) return hipErrorInvalidValue;
+    if (g == 3)
+        hipLaunchKernelGGL(pbs_mb_latency_kernel<3>, dim3(a.count), dim3(512), MbLatLds::bytes, s, a);
+    else if (g == 2)
+        hipLaunchKernelGGL(pbs_mb_latency_kernel<2>, dim3(a.count), dim3(512), MbLatLds::bytes, s, a);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
 bool latency_pbs_supported(int N, int k, int L) { return N == 2048 && k == 1 && L == 1; }
 
 #ifndef LAT_RPW

@@ -39,64 +39,7 @@ namespace tfhe_mi355 {
 #ifndef PBS_MB_BUFLD
 #define PBS_MB_BUFLD 1  // GGSW loads through a buffer resource: scalar offsets, no 64-bit VALU address adds
 #endif
-#ifndef PBS_MB_TSKIP_MONO
-#define PBS_MB_TSKIP_MONO 0
-#endif
-#ifndef PBS_MB_SWK
-#define PBS_MB_SWK 4   // twist-table swizzle: position r ^ ((r >> SWK) & SWM) (M = 1024)
-#endif
-#ifndef PBS_MB_SWM
-#define PBS_MB_SWM 23
-#endif
-// Twist table in LDS, shared by the linear twist reads (digits, backward conversion) and the
-// keybundle's monomial reads.  A monomial read fetches entry r of t = d (1 - 4 f) mod 2N, lanes
-// 16 apart in f stepping t by 4d and the two 16-lane halves of a ds_read_b64 group by 256d.  As one
-// [M] double2 array the 32 lanes of a group put 8.1 distinct entries on one bank on average (PMC:
-// 56 % of the g = 3 kernel's LDS cycles were conflict cycles, profiles/r03_pmc_mb3.json).  Here re
-// and im are two [M] double planes and entry r sits at position r ^ ((r >> SWK) & SWM): 2.09 on
-// average, worst 4 (exhaustive over d and slots) with SWK = 4, SWM = 23, the best of every shift
-// and 10-bit mask (round 3: r ^ ((r >> 5) & 31), 2.36 / worst 8; scripts/probes/
-// twist_swizzle_search.py); same two instructions per monomial read, and a linear read
-// (r = lane + 64 b) stays conflict-free (the map is linear: position = 64 b + (lane ^ swz(lane) ^
-// swz(64 b))).
-// (M = 256, the k = 3 sets: plain planes, no swizzle.)
-template <int M>
-struct TwistLds {
-    static_assert(M == 1024 || M == 256, "twist table layouts for M = 1024 (swizzled) and 256");
-    static constexpr bool SW = M == 1024;
-    static constexpr uint32_t IM = 8u * M;  // byte offset of the im plane (table at LDS byte 0)
-    static constexpr uint32_t SWK = PBS_MB_SWK, SWM = PBS_MB_SWM;
-    static_assert(SWM >> (10 - SWK) == 0, "the swizzle reads bits of r only (not the quadrant bit)");
-    __device__ static uint32_t swz(uint32_t r) { return SW ? (r >> SWK) & SWM : 0u; }
-    __device__ static uint32_t pos(uint32_t r) { return r ^ swz(r); }
-    __device__ static void fill(double *t, const double2 *twist, int tid, int nt) {
-        for (int e = tid; e < M; e += nt) {
-            const uint32_t p = pos((uint32_t)e);
-            t[p] = twist[e].x;
-            t[M + p] = twist[e].y;
-        }
-    }
-    // 8 (lane ^ swz(lane)): position of twist[lane + 64 b] is 64 b + (lane ^ swz(lane) ^ swz(64 b))
-    // (swz(64 b) < 64 for every swizzle allowed here)
-    __device__ static uint32_t lane_base(int lane) { return 8u * (uint32_t)(SW ? lane ^ swz(lane) : lane); }
-    __device__ static cx linear(uint32_t lb, int b) {  // twist[lane + 64 b]; b compile-time: one XOR
-        const uint32_t a = (SW ? lb ^ (8u * swz(64u * (uint32_t)b)) : lb) + 512u * (uint32_t)b;
-        return {lds_ld_f64(a), lds_ld_f64(a + IM)};
-    }
-    // i^q twist[r] for t = q M + r (t mod 2^32, bits 0 .. log2 M + 1 used): the swap for odd q is
-    // the plane choice of the two reads (re at the returned address, im at address ^ IM), the signs
-    // (re: q0 ^ q1, im: q1) are XORed into the high words -- no selects
-    __device__ static cx mono(uint32_t t) {
-        constexpr int LOG2M = ilog2(M);
-        // PBS_MB_TSKIP_MONO (timing-only builds, wrong outputs): every lane reads its own entry, so
-        // the monomial reads are conflict-free -- measures what their bank conflicts cost
-        const uint32_t are = PBS_MB_TSKIP_MONO ? ((t & (uint32_t)M) | (uint32_t)__lane_id()) << 3
-                                               : ((t & (2u * M - 1)) ^ swz(t)) << 3;
-        const double re = lds_ld_f64(are), im = lds_ld_f64(are ^ IM);
-        const uint32_t sim = t << (30 - LOG2M);  // q1 at bit 31; + 2^30 carries q0 into it
-        return {flip_sign(re, sim + 0x40000000u), flip_sign(im, sim)};
-    }
-};
+// TwistLds (the twist table in LDS, shared with the multi-bit latency kernel): pbs_common.h
 
 constexpr int mb_wpe() { return PBS_WAVES_PER_EU > 0 ? PBS_WAVES_PER_EU : (PBS_MB_CPW >= 4 ? 2 : 1); }
 
