@@ -34,9 +34,10 @@
  *     second batch runs concurrently only when half a batch is queued; a call that finds the
  *     coalescer idle runs at once on the calling thread, TFHE_MI355_COALESCE_DIRECT=0 turns that
  *     off; the one-ciphertext-per-call pattern, shortint/server_key/mod.rs:783-857;
- *     TFHE_MI355_COALESCE_MAX_COUNT=0 turns coalescing off).  Batches of at most
- *     TFHE_MI355_LATENCY_MAX = 256 ciphertexts at N = 2048, k = 1, L = 1 run a one-ciphertext-
- *     per-CU latency kernel (same outputs; 0 = never).
+ *     TFHE_MI355_COALESCE_MAX_COUNT=0 turns coalescing off).  Batches of at most three passes of
+ *     one ciphertext per CU (768 rows on 256 CUs; the measured crossover against the throughput
+ *     kernels) at N = 2048, k = 1, L = 1 -- classic and multi-bit g = 2, 3 -- run the one-ciphertext-
+ *     per-CU latency kernels (same outputs; TFHE_MI355_LATENCY_MAX = rows overrides, 0 = never).
  *     The _async calls hold no per-context mutable state: every device scratch buffer they
  *     need comes from the caller (d_scratch, sized by the matching *_scratch query; a call
  *     given less than its query fails with an error, and only a query returning 0 allows
@@ -45,10 +46,12 @@
  *     synchronisation inside);
  *   - keys: a key upload (any *_key_upload*, *_set_ready) waits for the coalesced batches in
  *     flight and blocks new ones until it is done (a pending upload also keeps new batches from
- *     starting, so uploads are not starved under load); between tfhe_mi355_bootstrap_key_fourier /
- *     _keyswitch_key_device and the matching _set_ready the key counts as absent (calls needing it
- *     fail) rather than half-written; _async calls are not ordered with uploads: do not
- *     re-upload a key while _async work that reads it may still run;
+ *     starting, so uploads are not starved under load); the serialized-key uploads hold the key
+ *     lock from their first key write to the ready flag; a caller that fills the buffer of
+ *     tfhe_mi355_bootstrap_key_fourier / _keyswitch_key_device itself owns that window (calls made
+ *     before its _set_ready see whatever the buffer holds; on a multi-device context _set_ready
+ *     also replicates the buffer to the other devices); _async calls are not ordered with
+ *     uploads: do not re-upload a key while _async work that reads it may still run;
  *   - _async lut index arrays are not checked on the host (they live on the device): an entry
  *     >= lut_count is clamped to lut_count - 1 by the kernels (no out-of-bounds read); the
  *     host-pointer forms reject such an entry with an error;

@@ -16,13 +16,20 @@ def main():
     import torch
 
     from tfhe_mi355 import Engine, client, fill_accumulator
-    from tfhe_mi355.parameters import PARAM_MESSAGE_2_CARRY_2_KS_PBS as P
+    from tfhe_mi355.parameters import ALL
+
+    # LAT_PARAMS: the parameter set (default 2_2; e.g. PARAM_MULTI_BIT_MESSAGE_2_CARRY_2_GROUP_3_KS_PBS)
+    P = ALL[os.environ.get("LAT_PARAMS", "PARAM_MESSAGE_2_CARRY_2_KS_PBS")]
 
     counts = [int(c) for c in (sys.argv[1] if len(sys.argv) > 1 else "1,16,64,128,256,384,512,768,1024").split(",")]
     lwe_sk = client.gen_binary_key(3, 1, P.lwe_dimension)
     glwe_sk = client.gen_binary_key(3, 2, P.big_lwe_dimension)
-    bsk = client.gen_bootstrap_key(4, lwe_sk, glwe_sk, 1, P.polynomial_size, P.pbs_base_log, P.pbs_level,
-                                   P.glwe_modular_std_dev)
+    if P.grouping_factor:
+        bsk = client.gen_multi_bit_bootstrap_key(4, lwe_sk, glwe_sk, 1, P.polynomial_size, P.pbs_base_log,
+                                                 P.pbs_level, P.grouping_factor, P.glwe_modular_std_dev)
+    else:
+        bsk = client.gen_bootstrap_key(4, lwe_sk, glwe_sk, 1, P.polynomial_size, P.pbs_base_log, P.pbs_level,
+                                       P.glwe_modular_std_dev)
     eng = Engine(P, 0)
     eng.upload_bootstrap_key(bsk)
     C = max(counts)
@@ -34,7 +41,7 @@ def main():
     d_lut = torch.from_numpy(acc.view(np.int64)).cuda()
     stamps = os.environ.get("LAT_STAMPS") == "1"   # a LAT_STAMPS=1 build (TFHE_MI355_LIB)
     scratch = torch.zeros(max(eng.pbs_scratch_bytes(C), 1 << 16), dtype=torch.uint8, device="cuda")
-    res = {"latency_max_env": os.environ.get("TFHE_MI355_LATENCY_MAX"), "ms": {}}
+    res = {"params": P.name if hasattr(P, "name") else str(P.polynomial_size), "latency_max_env": os.environ.get("TFHE_MI355_LATENCY_MAX"), "ms": {}}
     for c in counts:
         eng.programmable_bootstrap_async(d_in, d_out, d_lut, 1, c, d_scratch=scratch)
         torch.cuda.synchronize()

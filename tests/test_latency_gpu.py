@@ -1,5 +1,5 @@
-"""The latency kernel (csrc/pbs_latency.hip: one ciphertext per 8-wave workgroup, batches of at
-most TFHE_MI355_LATENCY_MAX = 256 ciphertexts at N = 2048, k = 1, L = 1) against the throughput
+"""The latency kernel (csrc/pbs_latency.hip: one ciphertext per 8-wave workgroup, batches of up to
+three passes of one ciphertext per CU -- 768 rows on 256 CUs -- at N = 2048, k = 1, L = 1) against the throughput
 kernel (pbs_classic_kernel, larger batches) and the oracle: bit-identical u64 outputs on the same
 inputs, LUT indexes, edge bodies/masks, blind rotation without extraction, and the KS -> PBS call.
 Same DAG as the oracle, so every row must be equal, not merely decrypt equal."""
@@ -10,7 +10,7 @@ from conftest import decode
 
 pytestmark = pytest.mark.gpu
 
-SMALL, BIG = 200, 300   # <= 256 rows: latency kernel; > 256: throughput kernel
+SMALL, BIG = 200, 1100   # <= 3 x CUs rows: latency kernel; > 1024: throughput kernel (persistent grid)
 
 
 @pytest.fixture(scope="module")
@@ -53,7 +53,7 @@ def test_latency_equals_throughput_kernel_and_oracle(orc, keys_2_2, eng):
 def test_latency_single_and_odd_counts_decrypt(orc, keys_2_2, eng):
     p = keys_2_2.params
     acc = orc.fill_accumulator(2048, 1, 4, 4, lambda x: (3 * x + 1) % 16)
-    for count in (1, 2, 7, 64, 255, 256):
+    for count in (1, 2, 7, 64, 255, 256, 257, 700):  # 257 and 700: two and three latency passes
         msgs = (np.arange(count) * 11) % 16
         cts = orc.lwe_encrypt(500 + count, keys_2_2.lwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta),
                               p.lwe_modular_std_dev)
@@ -96,8 +96,8 @@ def mb_keys(orc, keys_mb):
 
 @pytest.mark.parametrize("g", [3, 2])
 def test_mb_latency_equals_throughput_kernel_and_oracle(orc, mb_keys, g):
-    """The same rows through the latency kernel (a batch of <= 256) and the slot-split throughput
-    kernel (inside a batch of 300), edge bodies and masks, three LUTs: every word equal; a sample of
+    """The same rows through the latency kernel (a batch of 200) and the slot-split throughput
+    kernel (inside a batch of 1100), edge bodies and masks, three LUTs: every word equal; a sample of
     rows equal to the oracle's deterministic multi-bit PBS."""
     from tfhe_mi355 import Engine
 

@@ -158,31 +158,33 @@ def test_large_4_4_chunked_split_bit_exact(orc):
     single.close()
 
 
-def test_two_phase_fourier_upload_and_serialized_key(orc, small_2_2):
-    """The _fourier / _set_ready pair on a multi-device context: the key counts as absent in
-    between (a PBS fails instead of reading a half-written key), then is replicated."""
+def test_two_phase_fourier_upload_replicates_on_set_ready(orc, small_2_2):
+    """The _fourier / _set_ready pair on a multi-device context: the caller fills the FIRST device's
+    buffer, _set_ready replicates it to the other shards (a PBS before any key fails), and every
+    shard then bootstraps like the single-device context."""
+    import ctypes
+
+    import torch
     from tfhe_mi355._lib import EngineError
 
     keys = small_2_2
     p = keys.params
-    single, multi = _engines(p, [0, 0])
-    _upload((single, multi), keys)
-    ptr, nbytes = single.fourier_bootstrap_key()
-    single.fourier_bootstrap_key_set_ready()
-    import torch
+    from tfhe_mi355 import Engine
 
-    host = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
-    import ctypes
-
-    hip = ctypes.CDLL("libamdhip64.so")
-    assert hip.hipMemcpy(ctypes.c_void_p(host.data_ptr()), ctypes.c_void_p(ptr), ctypes.c_size_t(nbytes), 3) == 0
-    mptr, mbytes = multi.fourier_bootstrap_key()
-    assert mbytes == nbytes
+    single = Engine(p, 0)
+    single.upload_bootstrap_key(keys.bsk)
+    multi = Engine(p, devices=[0, 0, 0])
     lut = orc.fill_accumulator(p.polynomial_size, 1, 4, 4, lambda x: x)
-    _, small = _cts(orc, keys, 80, 10)
+    _, small = _cts(orc, keys, 90, 10)
     with pytest.raises(EngineError, match="not uploaded"):
         multi.programmable_bootstrap(small, lut)
-    assert hip.hipMemcpy(ctypes.c_void_p(mptr), ctypes.c_void_p(host.data_ptr()), ctypes.c_size_t(nbytes), 3) == 0
+    ptr, nbytes = single.fourier_bootstrap_key()
+    mptr, mbytes = multi.fourier_bootstrap_key()
+    assert mbytes == nbytes
+    hip = ctypes.CDLL("libamdhip64.so")
+    tmp = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
+    assert hip.hipMemcpy(ctypes.c_void_p(tmp.data_ptr()), ctypes.c_void_p(ptr), ctypes.c_size_t(nbytes), 3) == 0
+    assert hip.hipMemcpy(ctypes.c_void_p(mptr), ctypes.c_void_p(tmp.data_ptr()), ctypes.c_size_t(nbytes), 3) == 0
     multi.fourier_bootstrap_key_set_ready()
     assert np.array_equal(multi.programmable_bootstrap(small, lut), single.programmable_bootstrap(small, lut))
     multi.close()

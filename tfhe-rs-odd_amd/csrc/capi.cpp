@@ -145,6 +145,7 @@ struct RcclComms;  // communicator over a multi-device context's distinct device
 struct TfheMi355Context {
     TfheMi355Parameters p{};
     int device = 0;
+    int cus = 256;  // compute units of the device (the latency kernels run one ciphertext per CU)
     std::mutex mu;
     // Key material vs the coalescer's batches: every key upload holds it exclusively, every
     // dispatcher batch shared, so a re-upload waits for the batches in flight and no batch starts
@@ -367,14 +368,23 @@ size_t pbs_scratch_bytes(const TfheMi355Context *c, size_t count) {
     return per_ct * std::min(count, large_chunk(c));
 }
 
-// Batches of at most this many ciphertexts run the latency kernel at the shapes it supports
-// (TFHE_MI355_LATENCY_MAX; 0 = never).
-size_t latency_max() {
-    static const size_t v = [] {
+// Batches of at most this many ciphertexts run the latency kernels (one ciphertext per CU) at the
+// shapes they support.  Chosen by predicted time: the latency kernel takes one pass per CU-full of
+// ciphertexts, the throughput kernel a time that steps with its ciphertexts per CU (<= 1024 rows:
+// small batches spread over the CUs), so latency wins while passes x T_latency < T_throughput.
+// Measured at 2_2 (profiles/r05_lat_sweep_{lat,thr}.json, 1..1024 rows): latency 2.54-2.60 ms per
+// pass; throughput 5.6 / 6.0 / 8.6 / 8.8 ms at 1 / 2 / 3 / 4 ciphertexts per CU -> the latency
+// kernel up to 3 passes (768 rows on 256 CUs: 7.7-8.0 vs 8.6 ms), the throughput kernel from the
+// 4th (10.3 vs 8.8 ms).  Multi-bit g = 2, 3 (profiles/r05_lat_sweep_mb*.json): see kLatPassesMb.
+// TFHE_MI355_LATENCY_MAX overrides the row count for every shape (0 = never).
+constexpr size_t kLatPassesClassic = 3, kLatPassesMb = 3;
+size_t latency_max(const TfheMi355Context *c) {
+    static const long forced = [] {
         const char *e = std::getenv("TFHE_MI355_LATENCY_MAX");
-        return e && *e ? (size_t)std::max(0L, std::atol(e)) : (size_t)256;
+        return e && *e ? std::max(0L, std::atol(e)) : -1L;
     }();
-    return v;
+    if (forced >= 0) return (size_t)forced;
+    return (c->p.grouping_factor ? kLatPassesMb : kLatPassesClassic) * (size_t)c->cus;
 }
 
 bool ks_use_mfma(const TfheMi355Context *c) {
@@ -438,7 +448,7 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
         a.base_log = (int)c->p.pbs_base_log;
         a.count = (int)count;
         a.glwe_out = glwe_out;
-        if (count <= latency_max() && latency_multibit_supported((int)c->N(), (int)c->k(), (int)c->p.pbs_level,
+        if (count <= latency_max(c) && latency_multibit_supported((int)c->N(), (int)c->k(), (int)c->p.pbs_level,
                                                                  (int)c->p.grouping_factor)) {
             TimedLaunch tl(c->timer_or_null(), "pbs_mb_latency_kernel", s);
             check(launch_latency_multibit_pbs((int)c->p.grouping_factor, a, s), "launch multi-bit latency pbs");
@@ -489,7 +499,7 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
     a.count = (int)count;
     a.glwe_out = glwe_out;
     // small batches: the latency kernel (one ciphertext per CU, all 8 waves on it; same outputs)
-    if (count <= latency_max() && latency_pbs_supported((int)c->N(), (int)c->k(), (int)c->p.pbs_level)) {
+    if (count <= latency_max(c) && latency_pbs_supported((int)c->N(), (int)c->k(), (int)c->p.pbs_level)) {
 #if LAT_STAMPS
         a.ticket = reinterpret_cast<uint32_t *>(scratch);  // diagnostic builds: the stamp buffer
 #endif
@@ -1348,6 +1358,9 @@ TfheMi355Context *create_single(const TfheMi355Parameters &p, int device) {
     c->device = device;
     try {
         check(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+            c->cus = cus;
         for (auto &L : c->lanes) {
             check(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking), "hipStreamCreate(lane)");
             for (hipEvent_t *e : {&L.h2d, &L.kern, &L.done})
@@ -1839,17 +1852,13 @@ int tfhe_mi355_bootstrap_key_fourier(TfheMi355Context *ctx, void **d_ptr, size_t
         if (!ctx || !d_ptr || !bytes) fail("null argument");
         *d_ptr = nullptr;
         *bytes = 0;
-        if (ctx->multi()) {  // the first device's buffer; _set_ready replicates it
+        if (ctx->multi()) {  // the first device's buffer; _set_ready replicates it to the others
             auto w = key_write_all(ctx);
-            set_ready_all(ctx, KeyPart::Fourier, false);
             abi(tfhe_mi355_bootstrap_key_fourier(ctx->shards[0], d_ptr, bytes));
             return;
         }
         KeyWrite kw(ctx);  // no coalesced batch in flight, none starts until done
         check(hipSetDevice(ctx->device), "hipSetDevice");
-        // the buffer is about to be written by the caller: batches fail ("not uploaded") until
-        // _set_ready instead of bootstrapping with a half-written key
-        ctx->fbsk_ready = false;
         ctx->fbsk.reserve(ctx->fourier_bsk_bytes());
         *d_ptr = ctx->fbsk.ptr;
         *bytes = ctx->fourier_bsk_bytes();
@@ -1914,17 +1923,13 @@ int tfhe_mi355_keyswitch_key_device(TfheMi355Context *ctx, void **d_ptr, size_t 
         if (!ctx || !d_ptr || !bytes) fail("null argument");
         *d_ptr = nullptr;
         *bytes = 0;
-        if (ctx->multi()) {  // the first device's buffer; _set_ready replicates it
+        if (ctx->multi()) {  // the first device's buffer; _set_ready replicates it to the others
             auto w = key_write_all(ctx);
-            set_ready_all(ctx, KeyPart::Ksk, false);
             abi(tfhe_mi355_keyswitch_key_device(ctx->shards[0], d_ptr, bytes));
             return;
         }
         KeyWrite kw(ctx);  // no coalesced batch in flight, none starts until done
         check(hipSetDevice(ctx->device), "hipSetDevice");
-        // about to be written by the caller: keyswitches fail until _set_ready (see above)
-        ctx->ksk_ready = false;
-        ctx->ksk_planes_ready = false;
         ctx->ksk.reserve(ctx->ksk_len() * sizeof(uint64_t));
         *d_ptr = ctx->ksk.ptr;
         *bytes = ctx->ksk_len() * sizeof(uint64_t);
