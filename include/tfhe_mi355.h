@@ -34,10 +34,11 @@
  *     second batch runs concurrently only when half a batch is queued; a call that finds the
  *     coalescer idle runs at once on the calling thread, TFHE_MI355_COALESCE_DIRECT=0 turns that
  *     off; the one-ciphertext-per-call pattern, shortint/server_key/mod.rs:783-857;
- *     TFHE_MI355_COALESCE_MAX_COUNT=0 turns coalescing off).  Batches of at most three passes of
- *     one ciphertext per CU (768 rows on 256 CUs; the measured crossover against the throughput
- *     kernels) at N = 2048, k = 1, L = 1 -- classic and multi-bit g = 2, 3 -- run the one-ciphertext-
- *     per-CU latency kernels (same outputs; TFHE_MI355_LATENCY_MAX = rows overrides, 0 = never).
+ *     TFHE_MI355_COALESCE_MAX_COUNT=0 turns coalescing off).  At N = 2048, k = 1, L = 1, batches
+ *     of at most three (classic) / two (multi-bit g = 2, 3) passes of one ciphertext per CU (768 /
+ *     512 rows on 256 CUs: the measured crossovers against the throughput kernels) run the
+ *     one-ciphertext-per-CU latency kernels (same outputs; TFHE_MI355_LATENCY_MAX = rows
+ *     overrides, 0 = never).
  *     The _async calls hold no per-context mutable state: every device scratch buffer they
  *     need comes from the caller (d_scratch, sized by the matching *_scratch query; a call
  *     given less than its query fails with an error, and only a query returning 0 allows

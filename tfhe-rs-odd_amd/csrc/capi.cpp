@@ -375,9 +375,11 @@ size_t pbs_scratch_bytes(const TfheMi355Context *c, size_t count) {
 // Measured at 2_2 (profiles/r05_lat_sweep_{lat,thr}.json, 1..1024 rows): latency 2.54-2.60 ms per
 // pass; throughput 5.6 / 6.0 / 8.6 / 8.8 ms at 1 / 2 / 3 / 4 ciphertexts per CU -> the latency
 // kernel up to 3 passes (768 rows on 256 CUs: 7.7-8.0 vs 8.6 ms), the throughput kernel from the
-// 4th (10.3 vs 8.8 ms).  Multi-bit g = 2, 3 (profiles/r05_lat_sweep_mb*.json): see kLatPassesMb.
-// TFHE_MI355_LATENCY_MAX overrides the row count for every shape (0 = never).
-constexpr size_t kLatPassesClassic = 3, kLatPassesMb = 3;
+// 4th (10.3 vs 8.8 ms).  Multi-bit (profiles/r05_lat_sweep_mb{3,2}_{lat,thr}.json): latency kernel
+// 1.8-2.1 ms per pass (g = 3; 2.0 at g = 2), the slot-split throughput kernel 4.7-5.2 ms (g = 3;
+// 5.0 at g = 2) for any batch up to 1024 rows -> two passes (512 rows: 4.25 vs 4.72 ms), not three
+// (6.0 vs 4.7 ms).  TFHE_MI355_LATENCY_MAX overrides the row count for every shape (0 = never).
+constexpr size_t kLatPassesClassic = 3, kLatPassesMb = 2;
 size_t latency_max(const TfheMi355Context *c) {
     static const long forced = [] {
         const char *e = std::getenv("TFHE_MI355_LATENCY_MAX");
