@@ -177,13 +177,35 @@ __device__ __forceinline__ int32_t decomp_digit32(uint32_t &state, int beta, uin
 // (r = lane + 64 b) stays conflict-free (the map is linear: position = 64 b + (lane ^ swz(lane) ^
 // swz(64 b))).
 // (M = 256, the k = 3 sets: plain planes, no swizzle.)
+// (M = 4096, the N = 8192 multi-bit paired sub-block kernel: r ^ ((r >> 6) & 31), the best worst
+// case of the shift-mask family for that kernel's read pattern (lanes step t by 16 d R): 2.12
+// distinct entries per bank on average, worst 4, against 19.6 / 32 for the plain planes
+// (scripts/probes/twist_swizzle_search_8192.py; k = 7 gives 2.10 but worst 6).)
+#ifndef PBS_MB8_SWK
+#define PBS_MB8_SWK 6
+#endif
+#ifndef PBS_MB8_SWM
+#define PBS_MB8_SWM 31
+#endif
+template <int M>
+struct TwistSwz {
+    static constexpr uint32_t K = 0, MASK = 0;
+};
+template <>
+struct TwistSwz<1024> {
+    static constexpr uint32_t K = PBS_MB_SWK, MASK = PBS_MB_SWM;
+};
+template <>
+struct TwistSwz<4096> {
+    static constexpr uint32_t K = PBS_MB8_SWK, MASK = PBS_MB8_SWM;
+};
 template <int M>
 struct TwistLds {
-    static_assert(M == 1024 || M == 256, "twist table layouts for M = 1024 (swizzled) and 256");
-    static constexpr bool SW = M == 1024;
+    static_assert(M == 1024 || M == 256 || M == 4096, "twist table layouts for M = 1024, 4096 (swizzled) and 256");
+    static constexpr bool SW = TwistSwz<M>::MASK != 0;
     static constexpr uint32_t IM = 8u * M;  // byte offset of the im plane (table at LDS byte 0)
-    static constexpr uint32_t SWK = PBS_MB_SWK, SWM = PBS_MB_SWM;
-    static_assert(SWM >> (10 - SWK) == 0, "the swizzle reads bits of r only (not the quadrant bit)");
+    static constexpr uint32_t SWK = TwistSwz<M>::K, SWM = TwistSwz<M>::MASK;
+    static_assert(!SW || SWM >> (ilog2(M) - SWK) == 0, "the swizzle reads bits of r only (not the quadrant bit)");
     __device__ static uint32_t swz(uint32_t r) { return SW ? (r >> SWK) & SWM : 0u; }
     __device__ static uint32_t pos(uint32_t r) { return r ^ swz(r); }
     __device__ static void fill(double *t, const double2 *twist, int tid, int nt) {

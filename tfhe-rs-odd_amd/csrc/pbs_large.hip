@@ -787,6 +787,193 @@ __global__ void __launch_bounds__((PairSubCfg<K, L>::THREADS), 2) large_pair_sub
 }
 
 // ---------------------------------------------------------------------------------------
+// Multi-bit paired sub-block kernel with the monomials from LDS (N = 8192, k = 1, L = 2, g = 2 / 3:
+// the PARAM_MULTI_BIT_MESSAGE_3_CARRY_3 sets, multi_bit.rs:134,192).  The kernel
+// above reads every monomial spectrum i^q twist[r] from the global twist table: 2^g - 1 gathers per
+// (ciphertext, slot), 64 lanes on scattered 16-byte entries, which with the GGSW operand loads make
+// up ~half of its time (timing-only builds).  Here the table lives in LDS as two
+// swizzled double planes (TwistLds<4096>, 64 KiB, the address-free form of pbs_multibit.hip), which
+// fits once the spectra no longer occupy the whole 128 KiB exchange region during the MAC:
+//   phase 1  wave (c, p): forward sub-FFT of polynomial p of ciphertext c (its 16 KiB exchange block
+//            of the region), spectrum kept in registers; then the region becomes [twist planes |
+//            half buffer];
+//   phase 2  two rounds h = 0, 1: every wave publishes slots 8h .. 8h + 7 of its spectrum into the
+//            half buffer (8 polynomials x 8 slots, 64 KiB), then wave w builds the keybundle and MAC
+//            of slot 8h + w for both ciphertexts and both columns (GGSW operands loaded once per
+//            pair, as above; monomials from LDS);
+//   phase 3  the MAC outputs (2 ciphertexts x 2 columns x 16 slots) go to the half buffer, and wave
+//            (c, col) inverse-transforms its column in it.
+// Per (ciphertext, column, frequency) the keybundle (selector order) and MAC (levels L..1, rows
+// 0..k) are those of the kernel above, so the outputs are bit-identical.  TFHE_MI355_MB_PAIR2=0
+// selects the kernel above (A/B).
+// ---------------------------------------------------------------------------------------
+template <int N, int G>
+struct MbPair2Cfg {
+    static constexpr int K = 1, L = 2, CPW = 2, PW = (K + 1) * L, WAVES = CPW * PW, THREADS = 64 * WAVES;
+    static constexpr int M = N / 2;
+    static constexpr int REGION = WAVES * SubFft::XL;      // double2: phase-1 exchange blocks
+    static constexpr int TWIST = 0;                        // phase 2: twist planes (2 M doubles) at byte 0
+    static constexpr int HALF = M;                         // then the half buffer [poly][8 slots][64]
+    static constexpr int S1 = REGION;                      // sub-FFT twiddle table
+    static constexpr size_t LDS = sizeof(double2) * (S1 + SubFft::Lds::s1_len);
+    static_assert(M + WAVES * 8 * 64 <= REGION, "twist planes + half buffer fit the exchange region");
+    static_assert(LDS <= 160 * 1024, "LDS per workgroup exceeds a CU");
+};
+
+template <int N, int G>
+__global__ void __launch_bounds__((MbPair2Cfg<N, G>::THREADS), 2) large_mb_pair2_kernel(LargePbsLaunch a, int ct0, int i) {
+    using Cfg = MbPair2Cfg<N, G>;
+    using S = Split<N>;
+    using Tw = TwistLds<Cfg::M>;
+    constexpr int K = 1, L = 2, M = S::M, R = S::R, NSEL = 1 << G;
+    constexpr int CPW = Cfg::CPW, PW = Cfg::PW;
+    static_assert(M == Cfg::M, "split shape");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double2 *lds = reinterpret_cast<double2 *>(smem);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int q, cp;
+    pair_sub_block_of<R>(blockIdx.x, q, cp);
+    const int cnt = a.chunk_count;
+    if (2 * cp >= cnt) return;  // whole workgroup
+    double2 *s1 = lds + Cfg::S1;
+    for (int e = threadIdx.x; e < SubFft::Lds::s1_len; e += Cfg::THREADS) s1[e] = a.W[R * (e & 63) * ((e >> 6) + 1)];
+    const SubFft::Lds tw{s1, s1};
+    WaveLocalSync wsync;
+    auto ct_of = [&](int c) { return min(2 * cp + c, cnt - 1); };  // idle slot: a valid ciphertext
+    auto spectra = [&](int c) { return a.spectra + (size_t)ct_of(c) * L * (K + 1) * M; };
+
+    // ---- phase 1: forward sub-FFT of polynomial p of ciphertext c (spectrum stays in registers) ----
+    const int c1 = wave / PW, p1 = wave % PW;
+    cx v[16];
+    {
+        const double2 *src = spectra(c1) + (size_t)p1 * M + 1024 * q + lane;
+#pragma unroll
+        for (int b = 0; b < 16; b++) v[b] = gld(src + 64 * b);
+        __syncthreads();  // twiddle table
+        cx *xb = reinterpret_cast<cx *>(lds) + wave * SubFft::XL;
+        SubFft::forward(v, xb, tw, lane, wsync);
+    }
+    // monomial degrees of each ciphertext's 2^g - 1 non-constant GGSWs (wave-uniform)
+    uint32_t deg[CPW][NSEL];
+#pragma unroll
+    for (int c = 0; c < CPW; c++) {
+        const uint64_t *in = a.lwe_in + (size_t)(ct0 + ct_of(c)) * (a.n + 1) + (size_t)i * G;
+#pragma unroll
+        for (int sel = 1; sel < NSEL; sel++) {
+            uint64_t d = 0;
+#pragma unroll
+            for (int b = 0; b < G; b++)
+                if ((sel >> (G - 1 - b)) & 1) d += in[b];
+            deg[c][sel] = pbs_modulus_switch<S::LOGN>(d);
+        }
+    }
+    __syncthreads();  // every wave's exchange block is free: the region becomes twist | half buffer
+    Tw::fill(reinterpret_cast<double *>(lds + Cfg::TWIST), a.twist, threadIdx.x, Cfg::THREADS);
+    double2 *half = lds + Cfg::HALF;
+    auto hslot = [&](int c, int p, int sl) { return half + ((c * PW + p) * 8 + sl) * 64 + lane; };
+
+    constexpr size_t ggsw_len = (size_t)L * (K + 1) * (K + 1) * M;
+    constexpr uint32_t rowb = 16u * (uint32_t)((K + 1) * M);
+    const __amdgpu_buffer_rsrc_t grs = make_rsrc(a.fbsk + (size_t)i * NSEL * ggsw_len);
+    const uint32_t gvo = 16u * (uint32_t)(1024 * q + lane);
+    // t = d (1 - 4 f) mod 2N with f = fl + R freq_slot(s): per lane and ciphertext-selector the
+    // slot-independent part, t(s) = tl - 4 d R freq_slot(s)  (mod 2^32; the low bits are exact)
+    const uint32_t fl = (uint32_t)q + (uint32_t)R * SubFft::freq_lane(lane);
+    cx o[2][CPW][K + 1];  // MAC outputs of the wave's slot in round 0 and round 1
+
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        // ---- publish slots 8h .. 8h + 7 of this wave's spectrum ----
+#pragma unroll
+        for (int sl = 0; sl < 8; sl++) *hslot(c1, p1, sl) = make_double2(v[8 * h + sl].re, v[8 * h + sl].im);
+        __syncthreads();  // (h = 0: also the twist planes)
+        const int s = 8 * h + wave;  // this wave's slot in round h (wave-uniform)
+        const uint32_t f = fl + (uint32_t)R * SubFft::freq_slot(s);
+        cx mono[CPW][NSEL];
+#pragma unroll
+        for (int c = 0; c < CPW; c++)
+#pragma unroll
+            for (int sel = 1; sel < NSEL; sel++) mono[c][sel] = Tw::mono(deg[c][sel] - 4u * deg[c][sel] * f);
+#pragma unroll
+        for (int lvl = L; lvl >= 1; lvl--) {
+            cx ff[CPW][K + 1];
+#pragma unroll
+            for (int c = 0; c < CPW; c++)
+#pragma unroll
+                for (int r = 0; r <= K; r++) {
+                    const double2 t = *hslot(c, (lvl - 1) * (K + 1) + r, wave);
+                    ff[c][r] = cx{t.x, t.y};
+                }
+#pragma unroll
+            for (int col = 0; col <= K; col++) {
+                __builtin_amdgcn_sched_barrier(0);  // one (level, column) operand batch in flight
+                double2 g[K + 1][NSEL];
+#pragma unroll
+                for (int r = 0; r <= K; r++)
+#pragma unroll
+                    for (int sel = 0; sel < NSEL; sel++)
+                        g[r][sel] = buffer_ld_d2(grs, gvo,
+                                                 (uint32_t)(16u * sel * ggsw_len) + (uint32_t)((lvl - 1) * (K + 1) + r) * rowb +
+                                                     16u * (uint32_t)(col * M) + 1024u * (uint32_t)s);
+#pragma unroll
+                for (int c = 0; c < CPW; c++) {
+#pragma unroll
+                    for (int r = 0; r <= K; r++) {
+                        double2 kb = g[r][0];
+#pragma unroll
+                        for (int sel = 1; sel < NSEL; sel++) {
+                            kb.x = fma(g[r][sel].x, mono[c][sel].re, fma(-g[r][sel].y, mono[c][sel].im, kb.x));
+                            kb.y = fma(g[r][sel].x, mono[c][sel].im, fma(g[r][sel].y, mono[c][sel].re, kb.y));
+                        }
+                        cx &oc = o[h][c][col];
+                        if (lvl == L && r == 0) {
+                            oc.re = fma(kb.x, ff[c][r].re, -(kb.y * ff[c][r].im));
+                            oc.im = fma(kb.x, ff[c][r].im, kb.y * ff[c][r].re);
+                        } else {
+                            oc.re = fma(kb.x, ff[c][r].re, fma(-kb.y, ff[c][r].im, oc.re));
+                            oc.im = fma(kb.x, ff[c][r].im, fma(kb.y, ff[c][r].re, oc.im));
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();  // every wave has read round h's half buffer
+    }
+    // ---- phase 3: outputs -> the half buffer as [c][col][16 slots][64], inverse sub-FFTs ----
+    auto oslot = [&](int c, int col, int sl) { return half + ((c * (K + 1) + col) * 16 + sl) * 64 + lane; };
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int c = 0; c < CPW; c++)
+#pragma unroll
+            for (int col = 0; col <= K; col++)
+                *oslot(c, col, 8 * h + wave) = make_double2(o[h][c][col].re, o[h][c][col].im);
+    __syncthreads();
+    if (wave >= CPW * (K + 1)) return;
+    const int c = wave / (K + 1), col = wave % (K + 1);
+#pragma unroll
+    for (int sl = 0; sl < 16; sl++) {
+        const double2 t = *oslot(c, col, sl);
+        v[sl] = cx{t.x, t.y};
+    }
+    cx *xb = reinterpret_cast<cx *>(oslot(c, col, 0) - lane);  // this column's 16 KiB: its exchange block
+    wsync();
+    SubFft::inverse(v, xb, tw, lane, wsync);
+    if (2 * cp + c >= cnt) return;
+    double2 *dst = spectra(c) + (size_t)col * M + 1024 * q + lane;  // (lvl 1, row col) slot: this WG only
+    store_sub_out<LARGE_SUB_AUX>(dst, v, lane);
+}
+
+static bool mb_pair2_enabled() {
+    static const bool v = [] {
+        const char *e = std::getenv("TFHE_MI355_MB_PAIR2");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
+// ---------------------------------------------------------------------------------------
 // Grouped CMUX (k = 1, L = 2).  The top DIF radix-16 is R4 over stride 4, twiddles
 // omega_16^{A c}, R4 (dft16_fwd): its outputs c = G, G+4, G+8, G+12 come from ONE second-layer
 // R4, which needs only output G of each first-layer R4.  So a workgroup per (ciphertext, group G,
@@ -1543,9 +1730,21 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
                 // PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_3; for the classic sets it measured slower
                 // than large_sub_kernel: 4640 vs 4895 KS+PBS/s at 3_3, 939 vs 1036 at 4_4 split)
                 using PairSub = PairSubCfg<K, L>;
-                TimedLaunch tl(a.timer, "large_pair_sub_kernel", s);
-                hipLaunchKernelGGL((large_pair_sub_kernel<N, K, L, G, 1>), dim3(pair_sub_blocks<S::R>((cnt + 1) / 2)),
-                                   dim3(PairSub::THREADS), PairSub::LDS, s, a, ct0, i);
+                bool pair2 = false;
+                if constexpr (N == 8192 && K == 1 && L == 2) {  // monomials from LDS (large_mb_pair2_kernel)
+                    if (mb_pair2_enabled()) {
+                        using P2 = MbPair2Cfg<N, G>;
+                        TimedLaunch tl(a.timer, "large_mb_pair2_kernel", s);
+                        hipLaunchKernelGGL((large_mb_pair2_kernel<N, G>), dim3(pair_sub_blocks<S::R>((cnt + 1) / 2)),
+                                           dim3(P2::THREADS), P2::LDS, s, a, ct0, i);
+                        pair2 = true;
+                    }
+                }
+                if (!pair2) {
+                    TimedLaunch tl(a.timer, "large_pair_sub_kernel", s);
+                    hipLaunchKernelGGL((large_pair_sub_kernel<N, K, L, G, 1>), dim3(pair_sub_blocks<S::R>((cnt + 1) / 2)),
+                                       dim3(PairSub::THREADS), PairSub::LDS, s, a, ct0, i);
+                }
             } else {
                 bool paired = false;
                 if constexpr (16 % (2 * (K + 1) * L) == 0) {  // L <= 2 at k = 1
