@@ -128,13 +128,16 @@ def _split_params():
         out[f"mb3_3g{g}"] = (name, f"shortint apply_lookup_table (keyswitch -> multi-bit PBS, grouping {g}) at {name} "
                                    f"(shortint/parameters/multi_bit.rs:{line}), N={p.polynomial_size}, batch per GPU; "
                                    "the reference publishes no number for this set",
-                             f"large_pair_sub_kernel<{p.polynomial_size},1,{p.pbs_level},{g},1> (+ large_top_fwd/top_inv "
-                             "per group, ks_mfma_kernel)")
+                             (f"large_mb_pair2_kernel<{p.polynomial_size},{g}> (+ large_mb_inv_fwd per group, "
+                              "ks_mfma_kernel)" if os.environ.get("TFHE_MI355_MB_PAIR2", "1") != "0" else
+                              f"large_pair_sub_kernel<{p.polynomial_size},1,{p.pbs_level},{g},1> (+ large_top_fwd/top_inv "
+                              "per group, ks_mfma_kernel)"))
     return out
 
 
 PARAMS.update(_split_params())
-SPLIT_TAGS = {t for t, v in PARAMS.items() if v[2].startswith(("large_sub_kernel", "large_pair_sub_kernel", "large_dsub_kernel"))}
+SPLIT_TAGS = {t for t, v in PARAMS.items()
+              if v[2].startswith(("large_sub_kernel", "large_pair_sub_kernel", "large_mb_pair2_kernel", "large_dsub_kernel"))}
 WITH_KS = {"4_4", "2_2ks"} | SPLIT_TAGS
 
 

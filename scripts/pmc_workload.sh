@@ -13,7 +13,7 @@ case $tag in
   mb2)   K='pbs_multibit'; U='pbs_multibit'; UPD=4096; M='pbs_multibit'; ARGS="--params mb2" ;;
   4_4)   K='large_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=128; M='large_group_cmux_kernel'; ARGS="--params 4_4 --batch 128" ;;
   3_3)   K='large_|split_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=512; M='large_dsub_kernel|large_sub_kernel'; ARGS="--params 3_3 --batch 512" ;;
-  mb3_3g2|mb3_3g3) K='large_|split_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=512; M='large_pair_sub_kernel|large_sub_kernel'; ARGS="--params $tag --batch 512" ;;
+  mb3_3g2|mb3_3g3) K='large_|split_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=512; M='large_mb_pair2_kernel|large_pair_sub_kernel|large_sub_kernel'; ARGS="--params $tag --batch 512" ;;
   *) echo "unknown tag $tag"; exit 2 ;;
 esac
 B="$ARGS --steps 2 --warmup 1 --no-cpu-baseline --no-host-abi --no-single-call"

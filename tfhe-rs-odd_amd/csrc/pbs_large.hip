@@ -1406,6 +1406,96 @@ __device__ __forceinline__ void top_inv_body(const LargePbsLaunch &a, int cl, in
     }
 }
 
+// Multi-bit split CMUX (G > 0): large_top_inv of group i fused with large_top_fwd of group i + 1.
+// Without a rotation (ct1 = acc) the new accumulator pair at positions j = t + 1024 b, b < R, that
+// butterfly t of column r produces is exactly what butterfly t of row r decomposes next, so one
+// thread runs both: top DIT radix-R of U, backward conversion (the reference's zeroed ping-pong
+// destination, lwe_multi_bit_programmable_bootstrapping.rs:782-800), decompose64 of the pairs,
+// twist, top DIF radix-R per level -> the next group's top-stage spectra.  The accumulator stays in
+// registers: it is written to scratch only by the last group's plain large_top_inv (for the
+// extraction).  Per ciphertext and group: 384 KiB (U in, spectra out) instead of 640 KiB (top_inv's
+// accumulator write and top_fwd's read), and one launch fewer.  Same operations on the same values
+// as the two kernels, so bit-identical.  TFHE_MI355_MB_FUSED=0: the separate launches (A/B).
+template <int N, int K, int L, int G>
+__global__ void __launch_bounds__(TOPT, (top_fwd_wpe<N, L>())) large_mb_inv_fwd_kernel(LargePbsLaunch a, int ct0, int i) {
+    static_assert(G > 0, "multi-bit only (the classic CMUX rotates between the two)");
+    using S = Split<N>;
+    constexpr int R = S::R, M = S::M, BPP = 1024 / TOPT;
+    const int x = blockIdx.x & 7, m = blockIdx.x >> 3;  // XCD-aware as large_top_fwd_kernel
+    const int sub = m % ((K + 1) * BPP);
+    const int cl = x + 8 * (m / ((K + 1) * BPP));
+    if (cl >= a.chunk_count) return;  // whole workgroup
+    (void)ct0;
+    (void)i;
+    const int r = sub / BPP, t = (sub % BPP) * TOPT + threadIdx.x;  // column r of group i = row r of i + 1
+    // ---- large_top_inv of group i, column r, butterfly t ----
+    const double2 *U = a.spectra + ((size_t)cl * L * (K + 1) + r) * M + t;
+    cx wt[R], tw[R], u[R];
+    wt[0] = cx{1.0, 0.0};
+#pragma unroll
+    for (int c = 1; c < R; c++) wt[c] = gld(a.wtop + (c - 1) * 1024 + t);  // = W[t c]
+#pragma unroll
+    for (int b = 0; b < R; b++) tw[b] = gld(a.twist + t + 1024 * b);
+    u[0] = gld(U);
+#pragma unroll
+    for (int c = 1; c < R; c++) u[c] = cmulw(gld(U + 1024 * c), wt[c].re, -wt[c].im);
+    dftR_inv<R>(u);
+    const double k32 = torus_k32();
+    uint64_t lo[R], hi[R];
+#pragma unroll
+    for (int b = 0; b < R; b++) backward_convert(u[b], tw[b], lo[b], hi[b], k32);
+    // ---- large_top_fwd of group i + 1, row r, butterfly t (top_fwd_body, G > 0) ----
+    const int beta = a.base_log;
+    uint64_t pk[L > 1 ? R : 1];
+#pragma unroll
+    for (int b = 0; b < R; b++) {
+        int32_t d0[L], d1[L];
+        decompose64<L>(lo[b], beta, d0);
+        decompose64<L>(hi[b], beta, d1);
+        if constexpr (L > 1) {
+            uint64_t w = 0;
+#pragma unroll
+            for (int l = 1; l < L; l++)
+                w |= ((uint64_t)((uint32_t)d0[l] & 0xffffu) << (32 * (l - 1))) |
+                     ((uint64_t)((uint32_t)d1[l] & 0xffffu) << (32 * (l - 1) + 16));
+            pk[b] = w;
+        }
+        u[b] = cmulw(cx{(double)d0[0], (double)d1[0]}, tw[b].re, tw[b].im);
+    }
+    auto top_and_store = [&](int lvl) {
+        dftR_fwd<R>(u);
+        double2 *T = a.spectra + (((size_t)cl * L + (lvl - 1)) * (K + 1) + r) * M;
+        constexpr int AUX = LARGE_TOPF_AUX < 0 ? 16 : LARGE_TOPF_AUX;
+        auto st = [&](int c, cx y) {
+            const double2 v2 = make_double2(y.re, y.im);
+            if (AUX) buffer_st_d2p<AUX>(make_rsrc(T), 16u * (t + 1024 * c), 0, v2);
+            else T[t + 1024 * c] = v2;
+        };
+        st(0, u[0]);
+#pragma unroll
+        for (int c = 1; c < R; c++) st(c, cmulw(u[c], wt[c].re, wt[c].im));
+    };
+    top_and_store(L);
+#pragma unroll
+    for (int l = 1; l < L; l++) {
+#pragma unroll
+        for (int b = 0; b < R; b++) {
+            const int32_t e0 = (int32_t)(int16_t)((pk[b] >> (32 * (l - 1))) & 0xffffu);
+            const int32_t e1 = (int32_t)(int16_t)((pk[b] >> (32 * (l - 1) + 16)) & 0xffffu);
+            u[b] = cmulw(cx{(double)e0, (double)e1}, tw[b].re, tw[b].im);
+        }
+        top_and_store(L - l);
+    }
+}
+
+static bool mb_fused_enabled() {
+    static const bool v = [] {
+        const char *e = std::getenv("TFHE_MI355_MB_FUSED");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 template <int N, int K, int G = 0>
 __global__ void __launch_bounds__(TOPT) large_top_inv_kernel(LargePbsLaunch a, int ct0, int i) {
     constexpr int BPP = 1024 / TOPT;
@@ -1720,8 +1810,9 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
         }
         const unsigned sub_blocks = (unsigned)cnt * S::R;
         const int steps = G ? a.n / G : a.n;  // CMUXes, or multi-bit groups
+        const bool mb_fused = G > 0 && mb_fused_enabled();  // top_inv of group i + top_fwd of i + 1
         for (int i = 0; i < steps; i++) {
-            {
+            if (i == 0 || !mb_fused) {
                 TimedLaunch tl(a.timer, "large_top_fwd_kernel", s);
                 hipLaunchKernelGGL((large_top_fwd_kernel<N, K, L, G>), dim3(fwd_blocks), dim3(TOPT), 0, s, a, ct0, i);
             }
@@ -1761,6 +1852,14 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
                     TimedLaunch tl(a.timer, "large_sub_kernel", s);
                     hipLaunchKernelGGL((large_sub_kernel<N, K, L>), dim3(sub_blocks), dim3(Sub::THREADS), Sub::LDS, s,
                                        a, ct0, i);
+                }
+            }
+            if constexpr (G > 0) {
+                if (mb_fused && i + 1 < steps) {
+                    TimedLaunch tl(a.timer, "large_mb_inv_fwd_kernel", s);
+                    hipLaunchKernelGGL((large_mb_inv_fwd_kernel<N, K, L, G>), dim3(fwd_blocks), dim3(TOPT), 0, s, a,
+                                       ct0, i);
+                    continue;
                 }
             }
             TimedLaunch tl(a.timer, "large_top_inv_kernel", s);
