@@ -1262,6 +1262,25 @@ def run_mul32(args, P, workload, kname, R):
     step_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
     ok = int(np.count_nonzero(cks.decrypt(out) == (a * b) % np.uint64(1 << 32)))
     agg = aggregate(R, (hi - lo) * args.steps, wall, ok, hi - lo, lo, hi)
+    latency = None
+    if R.rank == 0 and not args.no_single_call:
+        # ONE multiply (the reference's published FheUint32 `*`: 333 ms on a 128-vCPU m6i.metal,
+        # benchmarks.md:17): eager, every layer a small batch (<= 256 PBS: the latency kernel)
+        one_a, one_b = sks.to_device(RadixSlice(ca, 1)), sks.to_device(RadixSlice(cb, 1))
+        o1 = sks.mul_parallelized(one_a, one_b)
+        torch.cuda.synchronize()
+        times = []
+        for _ in range(5):
+            t = time.perf_counter()
+            o1 = sks.mul_parallelized(one_a, one_b)
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t)
+        latency = {"ms": 1e3 * float(np.median(times)), "min_ms": 1e3 * min(times), "calls": len(times),
+                   "op": "one FheUint32 multiply (mul_parallelized DAG, eager: 11 KS+PBS layers of <= 256 "
+                         "ciphertexts on the latency kernel, plus the LWE additions)",
+                   "correct": bool(cks.decrypt(o1)[0] == (int(a[0]) * int(b[0])) % (1 << 32)),
+                   "reference_ms": 333.0,
+                   "note": "reference: FheUint32 mul, whole 128-vCPU machine (benchmarks.md:17,27)"}
     if R.rank == 0:
         pbs_rate = agg["value"] * pbs_per_mul
         units = int(round(pbs_per_mul * (hi - lo)))
@@ -1290,6 +1309,9 @@ def run_mul32(args, P, workload, kname, R):
             "check": {"decrypted_ok": agg["ok"], "of": agg["of"]},
             "setup": {"keygen_s": t_gen, "bsk_broadcast_s": t_bc, "ksk_broadcast_s": t_bc_ksk},
         }
+        if latency:
+            line["single_call_latency_ms"] = latency["ms"]
+            line["single_call_latency"] = latency
         if R.world == 1 and not args.no_cpu_baseline:
             sys.path.insert(0, ROOT)
             from oracle.oracle import OracleEngine  # oracle behind the engine API (test infrastructure)
@@ -1315,7 +1337,8 @@ def run_mul32(args, P, workload, kname, R):
 def RadixSlice(rb, n):
     from tfhe_mi355.integer import RadixBatch
 
-    return RadixBatch(rb.data[:n].copy(), list(rb.degree), list(rb.noise))
+    d = rb.data[:n]
+    return RadixBatch(d.copy() if isinstance(d, np.ndarray) else d.clone(), list(rb.degree), list(rb.noise))
 
 
 if __name__ == "__main__":
