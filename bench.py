@@ -114,7 +114,9 @@ def _split_params():
         out[tag] = (name, f"shortint apply_lookup_table (keyswitch -> PBS) at {name} (shortint/parameters/mod.rs:"
                           f"{SHORTINT_SOURCE_LINE[name]}), N={p.polynomial_size}, batch per GPU; the reference publishes "
                           + ("121 ms per KS+PBS at 3_3 (benchmarks.md:42)" if tag == "3_3" else "no number for this set"),
-                    (f"large_dsub_kernel<{p.polynomial_size}> (+ split_digits/large_top_inv per CMUX, ks_mfma_kernel)"
+                    (f"onchip_cmux_kernel<{p.polynomial_size}> (the whole blind rotation per workgroup, ks_mfma_kernel)"
+                     if p.pbs_level == 2 and p.polynomial_size == 8192 and os.environ.get("TFHE_MI355_ONCHIP", "1") != "0"
+                     else f"large_dsub_kernel<{p.polynomial_size}> (+ split_digits/large_top_inv per CMUX, ks_mfma_kernel)"
                      if p.pbs_level == 2 and p.polynomial_size <= 8192 else
                      f"large_sub_kernel<{p.polynomial_size},1,{p.pbs_level}> (+ large_top_fwd/top_inv per CMUX, "
                      "ks_mfma_kernel)"))
@@ -137,7 +139,8 @@ def _split_params():
 
 PARAMS.update(_split_params())
 SPLIT_TAGS = {t for t, v in PARAMS.items()
-              if v[2].startswith(("large_sub_kernel", "large_pair_sub_kernel", "large_mb_pair2_kernel", "large_dsub_kernel"))}
+              if v[2].startswith(("large_sub_kernel", "large_pair_sub_kernel", "large_mb_pair2_kernel", "large_dsub_kernel",
+                                  "onchip_cmux_kernel"))}
 WITH_KS = {"4_4", "2_2ks"} | SPLIT_TAGS
 
 
@@ -310,7 +313,8 @@ def roofline(tag, p, units_per_launch: int, step_ms: float, kname: str, with_ks:
     fam, pmc_name = DOMINANT.get(tag, ("pbs_classic_kernel", kname))
     steps_flop = pbs_flops(p) * units_per_launch
     fp64_step = steps_flop / (step_ms * 1e-3) / 1e12
-    large = p.polynomial_size > 2048
+    # the on-chip CMUX runs every CMUX of the batch in one launch: the whole-PBS flop model per launch
+    large = p.polynomial_size > 2048 and fam != "onchip_cmux_kernel"
     grouped = p.polynomial_size == 32768 and p.pbs_level == 2 and p.glwe_dimension == 1
     chunk = split_chunk(p, units_per_launch) if large else units_per_launch
     kt = (ktimes or {}).get(fam)

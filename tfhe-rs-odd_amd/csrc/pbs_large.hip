@@ -14,6 +14,7 @@
 // from a [c-1][a] copy of the table (coalesced); sub-blocks W_M[16 x] through an LDS table (the
 // oracle's tstride-16 reads of the same table, so bit-identical).
 #include <cstdlib>
+#include <type_traits>
 
 #include "engine.h"
 #include "pbs_common.h"
@@ -1574,6 +1575,271 @@ __global__ void __launch_bounds__(1024) split_inv_digits_kernel(LargePbsLaunch a
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// On-chip CMUX (N = 8192, k = 1, L = 2, classic).  One 512-thread workgroup per
+// ciphertext runs the WHOLE blind rotation: the accumulator (2 rows x 8192 u64 = 128 KiB) lives in
+// registers (thread t owns the pairs (j, j + M), j = t + 512 h + 1024 b, h < 2, b < 4, of both
+// rows: 64 VGPRs) and every intermediate in the 128 KiB LDS region -- no accumulator, digit or
+// spectrum traffic to HBM, one launch per batch instead of 2 per CMUX.  Per CMUX:
+//   rotation   : both rows' pairs -> LDS, ct1 = X^{a~} acc - acc gathered (ct1_pair_m's rules),
+//                decompose64<2>, 4 int16 digits per (row, pair) kept in registers
+//   level L, then level L-1 (the MAC's order):
+//     top      : every thread: twist, top DIF radix-4 of its butterflies of both rows, output c
+//                times W[a c] -> wave buffer (2 c + row) at a (natural layout)
+//     sub-FFT  : wave (q, row) = buffer 2 q + row: WaveFft<1024>::forward, spectrum published in
+//                place
+//     MAC      : wave (q, col = its row index) adds G[lvl][0][col] F_0 + G[lvl][1][col] F_1 of
+//                sub-block q (F_own from registers, F_partner from the partner's buffer) into o
+//   inverse    : wave (q, col): WaveFft<1024>::inverse(o) -> its buffer (natural layout)
+//   top inverse: every thread: top DIT radix-4 of its butterflies of both columns, backward_add
+//                into the registers
+// Then the sample extraction from registers (through LDS).  The same operations in the same order
+// as large_top_fwd + large_sub_kernel + large_top_inv (and the digits-fed path), so the outputs
+// are bit-identical.  LDS: 8 x 16 KiB wave buffers (= the rotation's 2 x M pairs) + the sub-block
+// twiddle table: 143 KiB, one workgroup (8 waves, 2 per SIMD) per CU.
+// TFHE_MI355_ONCHIP=0: the digits-fed split CMUX instead (A/B).
+// ---------------------------------------------------------------------------------------
+#ifndef ONCHIP_MAC_SB
+#define ONCHIP_MAC_SB 4  // MAC slots per scheduling region (GGSW loads in flight)
+#endif
+template <int N>
+struct OnchipCfg {
+    static constexpr int M = N / 2, R = M / 1024;
+    static constexpr int THREADS = 512;
+    static constexpr int H = 1024 / THREADS;  // top-stage butterflies per thread
+    static constexpr int BUF = SubFft::XL;    // double2 per wave buffer
+    static constexpr int S1 = 8 * BUF;        // twiddle table offset (double2 units)
+    static constexpr size_t LDS = sizeof(double2) * (S1 + SubFft::Lds::s1_len);
+    static_assert(R == 4, "8 waves = 4 sub-blocks x 2 rows");
+    static_assert(8 * BUF * sizeof(double2) == 2 * M * sizeof(acc_pair), "the rotation's pairs fill the wave buffers");
+};
+
+// MAC of level L - LI for one sub-block: both rows' spectra from their buffers F (row r at
+// F + r BUF; the own one too, so its registers are free here); o accumulates over levels L..1
+// and rows 0..k in the oracle's order (sub_cmux_body's forms)
+template <int M, int BUF, int LI>
+__device__ __forceinline__ void onchip_mac(const double2 *__restrict__ Gp, const double2 *F, cx (&o)[16]) {
+    constexpr int P0 = (1 - LI) * 2;  // polynomial (lvl - 1)(k + 1) of row 0, lvl = L - LI
+#pragma unroll
+    for (int s = 0; s < 16; s++) {
+        if (s % ONCHIP_MAC_SB == 0) __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight
+        const double2 f0 = F[s * 64], f1 = F[BUF + s * 64];
+        const double2 g0 = Gp[(size_t)P0 * 2 * M + s * 64];
+        const double2 g1 = Gp[(size_t)(P0 + 1) * 2 * M + s * 64];
+        cx x = o[s];
+        if constexpr (LI == 0) {
+            x.re = fma(g0.x, f0.x, -(g0.y * f0.y));
+            x.im = fma(g0.x, f0.y, g0.y * f0.x);
+        } else {
+            x.re = fma(g0.x, f0.x, fma(-g0.y, f0.y, x.re));
+            x.im = fma(g0.x, f0.y, fma(g0.y, f0.x, x.im));
+        }
+        x.re = fma(g1.x, f1.x, fma(-g1.y, f1.y, x.re));
+        x.im = fma(g1.x, f1.y, fma(g1.y, f1.x, x.im));
+        o[s] = x;
+    }
+}
+
+// a copy of a table pointer the compiler cannot prove loop-invariant: the twist / top-twiddle loads
+// stay where they are used instead of being hoisted out of the CMUX loop (56 VGPRs held for good)
+__device__ __forceinline__ const double2 *opaque(const double2 *p) {
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
+template <int N>
+__global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
+    using S = Split<N>;
+    using Cfg = OnchipCfg<N>;
+    constexpr int K = 1, L = 2, M = S::M, R = S::R, H = Cfg::H, BUF = Cfg::BUF;
+    constexpr size_t ggsw_len = (size_t)L * (K + 1) * (K + 1) * M;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double2 *lds = reinterpret_cast<double2 *>(smem);
+    acc_pair *pairs = reinterpret_cast<acc_pair *>(smem);  // rotation view: [row][M] pairs
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int q = wave >> 1, wr = wave & 1;  // sub-block; row (forward) = column (MAC, inverse)
+    const int ct = blockIdx.x;
+    double2 *s1 = lds + Cfg::S1;
+    // sub-block stage twiddles W_1024[lane c] = W_M[R lane c]  (oracle dif_rec tstride R)
+    for (int e = t; e < SubFft::Lds::s1_len; e += Cfg::THREADS) s1[e] = a.W[R * (e & 63) * ((e >> 6) + 1)];
+    const SubFft::Lds tw{s1, s1};
+    cx *xb = reinterpret_cast<cx *>(lds) + wave * BUF;
+    double2 *own = lds + wave * BUF;
+    WaveLocalSync wsync;
+    const uint64_t *in = a.lwe_in + (size_t)ct * (a.n + 1);
+
+    // acc = LUT / X^{b~} (large_init_kernel)
+    uint64_t lo[2][H][R], hi[2][H][R];
+    {
+        const uint32_t bt = pbs_modulus_switch<S::LOGN>(in[a.n]);
+        const uint32_t li = a.lut_indexes ? min(a.lut_indexes[ct], a.lut_count - 1u) : 0u;
+        const uint64_t *lut = a.luts + (size_t)li * (K + 1) * N;
+        const int full = bt / N, rem = bt % N;
+        auto init = [&](int r, int p) -> uint64_t {
+            const int src = p + rem;
+            const bool wrap = src >= N;
+            const uint64_t v = lut[(size_t)r * N + (wrap ? src - N : src)];
+            return (wrap != (bool)(full & 1)) ? 0 - v : v;
+        };
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int h = 0; h < H; h++)
+#pragma unroll
+                for (int b = 0; b < R; b++) {
+                    const int j = t + 512 * h + 1024 * b;
+                    lo[r][h][b] = init(r, j);
+                    hi[r][h][b] = init(r, j + M);
+                }
+    }
+    const double k32 = torus_k32();
+    const int beta = a.base_log;
+    __syncthreads();  // twiddle table
+
+    for (int i = 0; i < a.n; i++) {
+        const uint32_t at = pbs_modulus_switch<S::LOGN>(in[i]);
+        const bool full_odd = (at / N) & 1;
+        const int rem = at % N;
+        // ---- rotation + decomposition (split_digits through LDS) ----
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int h = 0; h < H; h++)
+#pragma unroll
+                for (int b = 0; b < R; b++) pairs[r * M + t + 512 * h + 1024 * b] = acc_pair{lo[r][h][b], hi[r][h][b]};
+        __syncthreads();
+        uint64_t pk[2][H][R];  // int16 digits: level L at j, j + M; level L-1 at j, j + M
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int h = 0; h < H; h++)
+#pragma unroll
+                for (int b = 0; b < R; b++) {
+                    const int j = t + 512 * h + 1024 * b;
+                    const int jj0 = j - rem;  // in (-N, M)
+                    const acc_pair rot = pairs[r * M + (jj0 & (M - 1))];
+                    const bool swap = jj0 < 0 && jj0 >= -M;
+                    const uint64_t x0 = swap ? rot.y : rot.x, x1 = swap ? rot.x : rot.y;
+                    const bool neg0 = (jj0 < 0) != full_odd, neg1 = (jj0 + M < 0) != full_odd;
+                    int32_t e0[2], e1[2];
+                    decompose64<2>((neg0 ? 0 - x0 : x0) - lo[r][h][b], beta, e0);
+                    decompose64<2>((neg1 ? 0 - x1 : x1) - hi[r][h][b], beta, e1);
+                    pk[r][h][b] = ((uint64_t)((uint32_t)e0[0] & 0xffffu)) | ((uint64_t)((uint32_t)e1[0] & 0xffffu) << 16) |
+                                  ((uint64_t)((uint32_t)e0[1] & 0xffffu) << 32) |
+                                  ((uint64_t)((uint32_t)e1[1] & 0xffffu) << 48);
+                }
+        __syncthreads();  // the pairs are read: the region becomes the wave buffers
+        const double2 *Gb = a.fbsk + (size_t)i * ggsw_len + (size_t)wr * M + 1024 * q;  // wave-uniform
+        cx o[16];
+        auto level = [&](auto LIc) {
+            constexpr int LI = decltype(LIc)::value;  // 0: level L, 1: level L-1
+            // ---- twist + top DIF radix-4 of both rows -> wave buffers (large_top_fwd) ----
+            const double2 *twist = opaque(a.twist), *wtop = opaque(a.wtop);
+#pragma unroll
+            for (int h = 0; h < H; h++) {
+                const int a0 = t + 512 * h;
+                cx tv[R], wq[R];
+#pragma unroll
+                for (int b = 0; b < R; b++) tv[b] = gld(twist + a0 + 1024 * b);
+#pragma unroll
+                for (int c = 1; c < R; c++) wq[c] = gld(wtop + (c - 1) * 1024 + a0);  // = W[a0 c]
+#pragma unroll
+                for (int r = 0; r < 2; r++) {
+                    cx u[R];
+#pragma unroll
+                    for (int b = 0; b < R; b++) {
+                        const uint64_t w = pk[r][h][b] >> (32 * LI);
+                        const int32_t d0 = (int32_t)(int16_t)(w & 0xffffu), d1 = (int32_t)(int16_t)((w >> 16) & 0xffffu);
+                        u[b] = cmulw(cx{(double)d0, (double)d1}, tv[b].re, tv[b].im);
+                    }
+                    dftR_fwd<R>(u);
+                    lds[r * BUF + a0] = make_double2(u[0].re, u[0].im);
+#pragma unroll
+                    for (int c = 1; c < R; c++) {
+                        const cx y = cmulw(u[c], wq[c].re, wq[c].im);
+                        lds[(2 * c + r) * BUF + a0] = make_double2(y.re, y.im);
+                    }
+                }
+            }
+            __syncthreads();
+            // ---- sub-block forward FFT of (q, row wr), published in place ----
+            cx v[16];
+#pragma unroll
+            for (int b = 0; b < 16; b++) {
+                const double2 x = own[lane + 64 * b];
+                v[b] = cx{x.x, x.y};
+            }
+            SubFft::forward(v, xb, tw, lane, wsync);
+            wsync();
+#pragma unroll
+            for (int s = 0; s < 16; s++) own[s * 64 + lane] = make_double2(v[s].re, v[s].im);
+            __syncthreads();
+            // ---- MAC of this level, column wr ----
+            onchip_mac<M, BUF, LI>(opaque(Gb) + lane, lds + (wave & ~1) * BUF + lane, o);
+            __syncthreads();  // the partner has read this wave's spectrum
+        };
+        level(std::integral_constant<int, 0>{});
+        level(std::integral_constant<int, 1>{});
+        // ---- inverse sub-FFT of (q, column wr) -> its buffer, natural layout ----
+        SubFft::inverse(o, xb, tw, lane, wsync);
+        wsync();
+#pragma unroll
+        for (int b = 0; b < 16; b++) own[lane + 64 * b] = make_double2(o[b].re, o[b].im);
+        __syncthreads();
+        // ---- top DIT radix-4, backward conversion, acc += (large_top_inv) ----
+        const double2 *twist = opaque(a.twist), *wtop = opaque(a.wtop);
+#pragma unroll
+        for (int h = 0; h < H; h++) {
+            const int a0 = t + 512 * h;
+            cx wq[R], tv[R];
+#pragma unroll
+            for (int c = 1; c < R; c++) wq[c] = gld(wtop + (c - 1) * 1024 + a0);
+#pragma unroll
+            for (int b = 0; b < R; b++) tv[b] = gld(twist + a0 + 1024 * b);
+#pragma unroll
+            for (int col = 0; col < 2; col++) {
+                cx u[R];
+                {
+                    const double2 x = lds[col * BUF + a0];
+                    u[0] = cx{x.x, x.y};
+                }
+#pragma unroll
+                for (int c = 1; c < R; c++) {
+                    const double2 x = lds[(2 * c + col) * BUF + a0];
+                    u[c] = cmulw(cx{x.x, x.y}, wq[c].re, -wq[c].im);
+                }
+                dftR_inv<R>(u);
+#pragma unroll
+                for (int b = 0; b < R; b++) backward_add(u[b], tv[b], lo[col][h][b], hi[col][h][b], k32);
+            }
+        }
+        __syncthreads();  // the buffers are read before the next rotation rewrites them
+    }
+    // ---- sample extract at degree 0 (large_extract_kernel) from the registers ----
+#pragma unroll
+    for (int h = 0; h < H; h++)
+#pragma unroll
+        for (int b = 0; b < R; b++) pairs[t + 512 * h + 1024 * b] = acc_pair{lo[0][h][b], hi[0][h][b]};
+    __syncthreads();
+    uint64_t *out = a.lwe_out + (size_t)ct * ((size_t)K * N + 1);
+    for (int e = t; e < N; e += Cfg::THREADS) {
+        const int p = e == 0 ? 0 : N - e;
+        const acc_pair pr = pairs[p & (M - 1)];
+        const uint64_t x = p >= M ? pr.y : pr.x;
+        out[e] = e == 0 ? x : 0 - x;
+    }
+    if (t == 0) out[N] = lo[1][0][0];  // row 1 position 0: the body
+}
+
+static bool onchip_enabled() {
+    static const bool v = [] {
+        const char *e = std::getenv("TFHE_MI355_ONCHIP");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // sample extract at degree 0 (glwe_sample_extraction.rs:91-147)
 template <int N, int K>
 __global__ void __launch_bounds__(256) large_extract_kernel(LargePbsLaunch a, int ct0, int cnt) {
@@ -1735,6 +2001,14 @@ template <int N, int K, int L, int G = 0>
 static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
     using S = Split<N>;
     if (a0.count == 0) return hipSuccess;
+    if constexpr (G == 0 && K == 1 && L == 2 && S::R == 4) {
+        if (onchip_enabled()) {  // the whole blind rotation on chip, no scratch
+            TimedLaunch tl(a0.timer, "onchip_cmux_kernel", s);
+            hipLaunchKernelGGL((onchip_cmux_kernel<N>), dim3((unsigned)a0.count), dim3(OnchipCfg<N>::THREADS),
+                               OnchipCfg<N>::LDS, s, a0);
+            return hipGetLastError();
+        }
+    }
     const size_t per_ct = large_pbs_scratch_per_ct(N, K, L);
     const int chunk = (int)std::min<size_t>((size_t)a0.count, a0.scratch_bytes / per_ct);
     if (chunk <= 0) return hipErrorInvalidValue;
