@@ -1,0 +1,20 @@
+#!/bin/bash
+# round 5: on-chip N = 8192 CMUX -- parity after the mask-prefetch change, timing-only variants
+# (ONCHIP_TSKIP: phase costs), PMC of 3_3 (onchip_cmux_kernel) and mb3_3g3 (large_mb_pair2_kernel).
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_split_gpu.py tests/test_golden.py -m gpu -v --timeout 300 --timeout-method thread \
+    -k "MESSAGE_3_CARRY_3 or chunks or split_3_3" > gpurun_out/r05_onchip_tests2.log 2>&1 || { tail -30 gpurun_out/r05_onchip_tests2.log; exit 1; }
+tail -3 gpurun_out/r05_onchip_tests2.log
+B="--params 3_3 --batch 1024 --steps 2 --warmup 1 --no-cpu-baseline --no-host-abi --no-single-call"
+for v in base ts1 ts2 ts4 ts8 ts16; do
+  lib=$PWD/tfhe-rs-odd_amd/lib/libtfhe_mi355.so; [ $v = base ] || lib=$PWD/tfhe-rs-odd_amd/build/$v/libtfhe_mi355.so
+  TFHE_MI355_LIB=$lib timeout -k 10 200 python bench.py $B > gpurun_out/r05_ts_$v.json 2> gpurun_out/r05_ts_$v.log || exit 1
+  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], round(d['value'],1), d['roofline'].get('kernel_times_ms'))" gpurun_out/r05_ts_$v.json
+done
+export ROUND=r05
+for t in 3_3 mb3_3g3; do
+  timeout -k 10 700 bash scripts/pmc_workload.sh $t > gpurun_out/r05_pmc_$t.log 2>&1 || { tail -5 gpurun_out/r05_pmc_$t.log; exit 1; }
+  find gpurun_out/pmc_$t -name '*.csv' -delete
+  echo pmc $t ok
+done

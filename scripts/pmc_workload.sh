@@ -12,7 +12,11 @@ case $tag in
   mb3)   K='pbs_multibit'; U='pbs_multibit'; UPD=4096; M='pbs_multibit'; ARGS="--params mb3" ;;
   mb2)   K='pbs_multibit'; U='pbs_multibit'; UPD=4096; M='pbs_multibit'; ARGS="--params mb2" ;;
   4_4)   K='large_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=128; M='large_group_cmux_kernel'; ARGS="--params 4_4 --batch 128" ;;
-  3_3)   K='large_|split_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=512; M='large_dsub_kernel|large_sub_kernel'; ARGS="--params 3_3 --batch 512" ;;
+  3_3)   if [ "${TFHE_MI355_ONCHIP:-1}" != 0 ]; then  # the on-chip CMUX: one launch per batch
+           K='onchip_|ks_digits|ks_mfma'; U='onchip_cmux_kernel'; UPD=512; M='onchip_cmux_kernel'
+         else
+           K='large_|split_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=512; M='large_dsub_kernel|large_sub_kernel'
+         fi; ARGS="--params 3_3 --batch 512" ;;
   mb3_3g2|mb3_3g3) K='large_|split_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=512; M='large_mb_pair2_kernel|large_pair_sub_kernel|large_sub_kernel'; ARGS="--params $tag --batch 512" ;;
   *) echo "unknown tag $tag"; exit 2 ;;
 esac

@@ -1599,6 +1599,10 @@ __global__ void __launch_bounds__(1024) split_inv_digits_kernel(LargePbsLaunch a
 // twiddle table: 143 KiB, one workgroup (8 waves, 2 per SIMD) per CU.
 // TFHE_MI355_ONCHIP=0: the digits-fed split CMUX instead (A/B).
 // ---------------------------------------------------------------------------------------
+#ifndef ONCHIP_TSKIP
+#define ONCHIP_TSKIP 0  // timing-only builds (wrong outputs): 1 no GGSW loads, 2 no forward sub-FFTs,
+                        // 4 no inverse sub-FFTs, 8 no top-stage arithmetic, 16 no rotation gather
+#endif
 #ifndef ONCHIP_MAC_SB
 #define ONCHIP_MAC_SB 4  // MAC slots per scheduling region (GGSW loads in flight)
 #endif
@@ -1618,14 +1622,14 @@ struct OnchipCfg {
 // F + r BUF; the own one too, so its registers are free here); o accumulates over levels L..1
 // and rows 0..k in the oracle's order (sub_cmux_body's forms)
 template <int M, int BUF, int LI>
-__device__ __forceinline__ void onchip_mac(const double2 *__restrict__ Gp, const double2 *F, cx (&o)[16]) {
+__device__ __forceinline__ void onchip_mac(__amdgpu_buffer_rsrc_t rg, uint32_t gvo, const double2 *F, cx (&o)[16]) {
     constexpr int P0 = (1 - LI) * 2;  // polynomial (lvl - 1)(k + 1) of row 0, lvl = L - LI
 #pragma unroll
     for (int s = 0; s < 16; s++) {
         if (s % ONCHIP_MAC_SB == 0) __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight
         const double2 f0 = F[s * 64], f1 = F[BUF + s * 64];
-        const double2 g0 = Gp[(size_t)P0 * 2 * M + s * 64];
-        const double2 g1 = Gp[(size_t)(P0 + 1) * 2 * M + s * 64];
+        const double2 g0 = (ONCHIP_TSKIP & 1) ? f1 : buffer_ld_d2(rg, gvo, 16u * (uint32_t)(P0 * 2 * M + s * 64));
+        const double2 g1 = (ONCHIP_TSKIP & 1) ? f0 : buffer_ld_d2(rg, gvo, 16u * (uint32_t)((P0 + 1) * 2 * M + s * 64));
         cx x = o[s];
         if constexpr (LI == 0) {
             x.re = fma(g0.x, f0.x, -(g0.y * f0.y));
@@ -1640,14 +1644,87 @@ __device__ __forceinline__ void onchip_mac(const double2 *__restrict__ Gp, const
     }
 }
 
-// a copy of a table pointer the compiler cannot prove loop-invariant: the twist / top-twiddle loads
-// stay where they are used instead of being hoisted out of the CMUX loop (56 VGPRs held for good)
-__device__ __forceinline__ const double2 *opaque(const double2 *p) {
-    asm volatile("" : "+s"(p));
-    return p;
+#ifndef ONCHIP_SPLIT_MAC
+#define ONCHIP_SPLIT_MAC 1
+#endif
+// ONCHIP_SPLIT_MAC: the two waves of sub-block q split the MAC by slots instead of by column:
+// wave (q, WR) computes slots 8 WR .. 8 WR + 7 of BOTH columns, its own row's spectrum from
+// registers and the partner row's half from the partner's buffer (half the publish stores, no LDS
+// reads of its own spectrum); the same fma chain per output element
+template <int M, int WR, int LI>
+__device__ __forceinline__ void onchip_mac_split(__amdgpu_buffer_rsrc_t rg, uint32_t gvo, const cx (&v)[16],
+                                                 const double2 *par, cx (&o)[2][8]) {
+    constexpr int P0 = (1 - LI) * 2;  // polynomial (lvl - 1)(k + 1) of row 0, lvl = L - LI
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const int s = 8 * WR + j;
+        if (j % (ONCHIP_MAC_SB / 2 > 0 ? ONCHIP_MAC_SB / 2 : 1) == 0) __builtin_amdgcn_sched_barrier(0);
+        const double2 pp = par[s * 64];
+        const double2 mine = make_double2(v[s].re, v[s].im);
+        const double2 f0 = WR ? pp : mine, f1 = WR ? mine : pp;
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            const double2 g0 = (ONCHIP_TSKIP & 1) ? f1 : buffer_ld_d2(rg, gvo, 16u * (uint32_t)(P0 * 2 * M + c * M + s * 64));
+            const double2 g1 =
+                (ONCHIP_TSKIP & 1) ? f0 : buffer_ld_d2(rg, gvo, 16u * (uint32_t)((P0 + 1) * 2 * M + c * M + s * 64));
+            cx x = o[c][j];
+            if constexpr (LI == 0) {
+                x.re = fma(g0.x, f0.x, -(g0.y * f0.y));
+                x.im = fma(g0.x, f0.y, g0.y * f0.x);
+            } else {
+                x.re = fma(g0.x, f0.x, fma(-g0.y, f0.y, x.re));
+                x.im = fma(g0.x, f0.y, fma(g0.y, f0.x, x.im));
+            }
+            x.re = fma(g1.x, f1.x, fma(-g1.y, f1.y, x.re));
+            x.im = fma(g1.x, f1.y, fma(g1.y, f1.x, x.im));
+            o[c][j] = x;
+        }
+    }
 }
 
-template <int N>
+// after the split MAC: column 1 - WR of this wave's slots -> the partner's buffer (which only the
+// partner reads from here on, before its inverse rewrites it); column WR of the partner's slots
+// from this wave's buffer -> o = column WR, all 16 slots
+template <int BUF, int WR>
+__device__ __forceinline__ void onchip_gather_column(const cx (&o2)[2][8], cx (&o)[16], double2 *lds, int wave, int lane) {
+    double2 *pb = lds + (wave ^ 1) * BUF + lane;
+#pragma unroll
+    for (int j = 0; j < 8; j++) pb[(8 * WR + j) * 64] = make_double2(o2[1 - WR][j].re, o2[1 - WR][j].im);
+    __syncthreads();
+    const double2 *ob = lds + wave * BUF + lane;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        o[8 * WR + j] = o2[WR][j];
+        const double2 x = ob[(8 * (1 - WR) + j) * 64];
+        o[8 * (1 - WR) + j] = cx{x.x, x.y};
+    }
+}
+
+// decompose64<2> in 32-bit registers when base_log * 2 <= 30 (pbs_common.h decomp_state32: the
+// same digits)
+template <bool D32>
+__device__ __forceinline__ void onchip_decompose(uint64_t x, int beta, int32_t (&d)[2]) {
+    if constexpr (D32) {
+        uint32_t st = decomp_state32<2>(x, beta);
+        const uint32_t mask = (1u << beta) - 1;
+        d[0] = decomp_digit32(st, beta, mask);
+        d[1] = decomp_digit32(st, beta, mask);
+    } else {
+        decompose64<2>(x, beta, d);
+    }
+}
+
+// a zero the compiler cannot see through: table pointers offset by it (the twist, the top-stage
+// twiddles, the CMUX's GGSW) are not provably loop-invariant, so their loads stay where they are
+// used instead of being hoisted out of the CMUX loop into registers held for good (an opaque
+// pointer instead would lose its address space: flat loads, counted against the LDS waits too)
+__device__ __forceinline__ int opaque_zero() {
+    int z = 0;
+    asm volatile("" : "+s"(z));
+    return z;
+}
+
+template <int N, bool D32>
 __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
     using S = Split<N>;
     using Cfg = OnchipCfg<N>;
@@ -1668,6 +1745,13 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
     double2 *own = lds + wave * BUF;
     WaveLocalSync wsync;
     const uint64_t *in = a.lwe_in + (size_t)ct * (a.n + 1);
+    // twist and top-stage twiddles through buffer loads: one VGPR offset, the rest in SGPRs
+    const __amdgpu_buffer_rsrc_t rtw = make_rsrc(a.twist), rwt = make_rsrc(a.wtop);
+    const uint32_t tvo = 16u * t;
+    auto ld_cx = [](__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
+        const double2 x = buffer_ld_d2(r, vo, so);
+        return cx{x.x, x.y};
+    };
 
     // acc = LUT / X^{b~} (large_init_kernel)
     uint64_t lo[2][H][R], hi[2][H][R];
@@ -1697,8 +1781,10 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
     const int beta = a.base_log;
     __syncthreads();  // twiddle table
 
+    uint64_t a_next = in[0];
     for (int i = 0; i < a.n; i++) {
-        const uint32_t at = pbs_modulus_switch<S::LOGN>(in[i]);
+        const uint32_t at = pbs_modulus_switch<S::LOGN>(a_next);
+        a_next = in[i + 1 < a.n ? i + 1 : i];  // next mask element: its load latency hides behind this CMUX
         const bool full_odd = (at / N) & 1;
         const int rem = at % N;
         // ---- rotation + decomposition (split_digits through LDS) ----
@@ -1718,32 +1804,38 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
                 for (int b = 0; b < R; b++) {
                     const int j = t + 512 * h + 1024 * b;
                     const int jj0 = j - rem;  // in (-N, M)
-                    const acc_pair rot = pairs[r * M + (jj0 & (M - 1))];
+                    const acc_pair rot = (ONCHIP_TSKIP & 16) ? acc_pair{lo[r][h][b] * 3, hi[r][h][b]} : pairs[r * M + (jj0 & (M - 1))];
                     const bool swap = jj0 < 0 && jj0 >= -M;
                     const uint64_t x0 = swap ? rot.y : rot.x, x1 = swap ? rot.x : rot.y;
                     const bool neg0 = (jj0 < 0) != full_odd, neg1 = (jj0 + M < 0) != full_odd;
                     int32_t e0[2], e1[2];
-                    decompose64<2>((neg0 ? 0 - x0 : x0) - lo[r][h][b], beta, e0);
-                    decompose64<2>((neg1 ? 0 - x1 : x1) - hi[r][h][b], beta, e1);
+                    onchip_decompose<D32>((neg0 ? 0 - x0 : x0) - lo[r][h][b], beta, e0);
+                    onchip_decompose<D32>((neg1 ? 0 - x1 : x1) - hi[r][h][b], beta, e1);
                     pk[r][h][b] = ((uint64_t)((uint32_t)e0[0] & 0xffffu)) | ((uint64_t)((uint32_t)e1[0] & 0xffffu) << 16) |
                                   ((uint64_t)((uint32_t)e0[1] & 0xffffu) << 32) |
                                   ((uint64_t)((uint32_t)e1[1] & 0xffffu) << 48);
                 }
         __syncthreads();  // the pairs are read: the region becomes the wave buffers
-        const double2 *Gb = a.fbsk + (size_t)i * ggsw_len + (size_t)wr * M + 1024 * q;  // wave-uniform
+#if ONCHIP_SPLIT_MAC
+        const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.fbsk + (size_t)i * ggsw_len + 1024 * q);
+        cx o2[2][8];  // MAC outputs of slots 8 wr .. 8 wr + 7, both columns
+        const double2 *par = lds + (wave ^ 1) * BUF + lane;
+#else
+        const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.fbsk + (size_t)i * ggsw_len + (size_t)wr * M + 1024 * q);
+#endif
         cx o[16];
         auto level = [&](auto LIc) {
             constexpr int LI = decltype(LIc)::value;  // 0: level L, 1: level L-1
             // ---- twist + top DIF radix-4 of both rows -> wave buffers (large_top_fwd) ----
-            const double2 *twist = opaque(a.twist), *wtop = opaque(a.wtop);
+            const uint32_t z = (uint32_t)opaque_zero();
 #pragma unroll
             for (int h = 0; h < H; h++) {
                 const int a0 = t + 512 * h;
                 cx tv[R], wq[R];
 #pragma unroll
-                for (int b = 0; b < R; b++) tv[b] = gld(twist + a0 + 1024 * b);
+                for (int b = 0; b < R; b++) tv[b] = ld_cx(rtw, tvo, z + 16u * (512 * h + 1024 * b));
 #pragma unroll
-                for (int c = 1; c < R; c++) wq[c] = gld(wtop + (c - 1) * 1024 + a0);  // = W[a0 c]
+                for (int c = 1; c < R; c++) wq[c] = ld_cx(rwt, tvo, z + 16u * ((c - 1) * 1024 + 512 * h));  // = W[a0 c]
 #pragma unroll
                 for (int r = 0; r < 2; r++) {
                     cx u[R];
@@ -1753,7 +1845,7 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
                         const int32_t d0 = (int32_t)(int16_t)(w & 0xffffu), d1 = (int32_t)(int16_t)((w >> 16) & 0xffffu);
                         u[b] = cmulw(cx{(double)d0, (double)d1}, tv[b].re, tv[b].im);
                     }
-                    dftR_fwd<R>(u);
+                    if (!(ONCHIP_TSKIP & 8)) dftR_fwd<R>(u);
                     lds[r * BUF + a0] = make_double2(u[0].re, u[0].im);
 #pragma unroll
                     for (int c = 1; c < R; c++) {
@@ -1770,33 +1862,52 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
                 const double2 x = own[lane + 64 * b];
                 v[b] = cx{x.x, x.y};
             }
-            SubFft::forward(v, xb, tw, lane, wsync);
+            if (!(ONCHIP_TSKIP & 2)) SubFft::forward(v, xb, tw, lane, wsync);
             wsync();
+#if ONCHIP_SPLIT_MAC
+            // publish the partner's half of the slots; MAC of this wave's half, both columns
+            auto publish = [&](auto WRc) {
+                constexpr int WR = decltype(WRc)::value;
+#pragma unroll
+                for (int j = 0; j < 8; j++) own[(8 * (1 - WR) + j) * 64 + lane] = make_double2(v[8 * (1 - WR) + j].re, v[8 * (1 - WR) + j].im);
+            };
+            if (wr == 0) publish(std::integral_constant<int, 0>{});
+            else publish(std::integral_constant<int, 1>{});
+            __syncthreads();
+            if (wr == 0) onchip_mac_split<M, 0, LI>(rg, 16u * lane, v, par, o2);
+            else onchip_mac_split<M, 1, LI>(rg, 16u * lane, v, par, o2);
+            if constexpr (LI == 0) __syncthreads();  // the partner has read this wave's half
+#else
 #pragma unroll
             for (int s = 0; s < 16; s++) own[s * 64 + lane] = make_double2(v[s].re, v[s].im);
             __syncthreads();
             // ---- MAC of this level, column wr ----
-            onchip_mac<M, BUF, LI>(opaque(Gb) + lane, lds + (wave & ~1) * BUF + lane, o);
+            onchip_mac<M, BUF, LI>(rg, 16u * lane, lds + (wave & ~1) * BUF + lane, o);
             __syncthreads();  // the partner has read this wave's spectrum
+#endif
         };
         level(std::integral_constant<int, 0>{});
         level(std::integral_constant<int, 1>{});
+#if ONCHIP_SPLIT_MAC
+        if (wr == 0) onchip_gather_column<BUF, 0>(o2, o, lds, wave, lane);
+        else onchip_gather_column<BUF, 1>(o2, o, lds, wave, lane);
+#endif
         // ---- inverse sub-FFT of (q, column wr) -> its buffer, natural layout ----
-        SubFft::inverse(o, xb, tw, lane, wsync);
+        if (!(ONCHIP_TSKIP & 4)) SubFft::inverse(o, xb, tw, lane, wsync);
         wsync();
 #pragma unroll
         for (int b = 0; b < 16; b++) own[lane + 64 * b] = make_double2(o[b].re, o[b].im);
         __syncthreads();
         // ---- top DIT radix-4, backward conversion, acc += (large_top_inv) ----
-        const double2 *twist = opaque(a.twist), *wtop = opaque(a.wtop);
+        const uint32_t z = (uint32_t)opaque_zero();
 #pragma unroll
         for (int h = 0; h < H; h++) {
             const int a0 = t + 512 * h;
             cx wq[R], tv[R];
 #pragma unroll
-            for (int c = 1; c < R; c++) wq[c] = gld(wtop + (c - 1) * 1024 + a0);
+            for (int c = 1; c < R; c++) wq[c] = ld_cx(rwt, tvo, z + 16u * ((c - 1) * 1024 + 512 * h));
 #pragma unroll
-            for (int b = 0; b < R; b++) tv[b] = gld(twist + a0 + 1024 * b);
+            for (int b = 0; b < R; b++) tv[b] = ld_cx(rtw, tvo, z + 16u * (512 * h + 1024 * b));
 #pragma unroll
             for (int col = 0; col < 2; col++) {
                 cx u[R];
@@ -1809,7 +1920,7 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
                     const double2 x = lds[(2 * c + col) * BUF + a0];
                     u[c] = cmulw(cx{x.x, x.y}, wq[c].re, -wq[c].im);
                 }
-                dftR_inv<R>(u);
+                if (!(ONCHIP_TSKIP & 8)) dftR_inv<R>(u);
 #pragma unroll
                 for (int b = 0; b < R; b++) backward_add(u[b], tv[b], lo[col][h][b], hi[col][h][b], k32);
             }
@@ -2004,8 +2115,12 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
     if constexpr (G == 0 && K == 1 && L == 2 && S::R == 4) {
         if (onchip_enabled()) {  // the whole blind rotation on chip, no scratch
             TimedLaunch tl(a0.timer, "onchip_cmux_kernel", s);
-            hipLaunchKernelGGL((onchip_cmux_kernel<N>), dim3((unsigned)a0.count), dim3(OnchipCfg<N>::THREADS),
-                               OnchipCfg<N>::LDS, s, a0);
+            if (a0.base_log * 2 <= 30)  // 32-bit digit extraction (every shortint set at this shape)
+                hipLaunchKernelGGL((onchip_cmux_kernel<N, true>), dim3((unsigned)a0.count), dim3(OnchipCfg<N>::THREADS),
+                                   OnchipCfg<N>::LDS, s, a0);
+            else
+                hipLaunchKernelGGL((onchip_cmux_kernel<N, false>), dim3((unsigned)a0.count),
+                                   dim3(OnchipCfg<N>::THREADS), OnchipCfg<N>::LDS, s, a0);
             return hipGetLastError();
         }
     }
