@@ -1621,15 +1621,38 @@ struct OnchipCfg {
 // MAC of level L - LI for one sub-block: both rows' spectra from their buffers F (row r at
 // F + r BUF; the own one too, so its registers are free here); o accumulates over levels L..1
 // and rows 0..k in the oracle's order (sub_cmux_body's forms)
-template <int M, int BUF, int LI>
-__device__ __forceinline__ void onchip_mac(__amdgpu_buffer_rsrc_t rg, uint32_t gvo, const double2 *F, cx (&o)[16]) {
+#ifndef ONCHIP_TPF
+#define ONCHIP_TPF 1  // top-stage twist / twiddle loads issued before the barrier preceding their use
+#endif
+#ifndef ONCHIP_PF
+#define ONCHIP_PF 4  // MAC slots whose GGSW operands are issued before the publish barrier (0: none)
+#endif
+constexpr int ONCHIP_PFS = ONCHIP_PF > 0 ? ONCHIP_PF : 1;
+// GGSW operands (rows 0 and 1 of level L - LI, column of rg) of MAC slot s
+template <int M, int LI>
+__device__ __forceinline__ void onchip_ggsw(__amdgpu_buffer_rsrc_t rg, uint32_t gvo, int s, double2 &g0, double2 &g1) {
     constexpr int P0 = (1 - LI) * 2;  // polynomial (lvl - 1)(k + 1) of row 0, lvl = L - LI
+    g0 = buffer_ld_d2(rg, gvo, 16u * (uint32_t)(P0 * 2 * M + s * 64));
+    g1 = buffer_ld_d2(rg, gvo, 16u * (uint32_t)((P0 + 1) * 2 * M + s * 64));
+}
+template <int M, int BUF, int LI>
+__device__ __forceinline__ void onchip_mac(__amdgpu_buffer_rsrc_t rg, uint32_t gvo, const double2 *F, cx (&o)[16],
+                                           const double2 (&pf)[ONCHIP_PFS][2]) {
 #pragma unroll
     for (int s = 0; s < 16; s++) {
-        if (s % ONCHIP_MAC_SB == 0) __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight
+        if (s >= ONCHIP_PF && (s - ONCHIP_PF) % ONCHIP_MAC_SB == 0) __builtin_amdgcn_sched_barrier(0);
         const double2 f0 = F[s * 64], f1 = F[BUF + s * 64];
-        const double2 g0 = (ONCHIP_TSKIP & 1) ? f1 : buffer_ld_d2(rg, gvo, 16u * (uint32_t)(P0 * 2 * M + s * 64));
-        const double2 g1 = (ONCHIP_TSKIP & 1) ? f0 : buffer_ld_d2(rg, gvo, 16u * (uint32_t)((P0 + 1) * 2 * M + s * 64));
+        double2 g0, g1;
+        if (s < ONCHIP_PF) {
+            g0 = pf[s < ONCHIP_PFS ? s : 0][0];
+            g1 = pf[s < ONCHIP_PFS ? s : 0][1];
+        } else {
+            onchip_ggsw<M, LI>(rg, gvo, s, g0, g1);
+        }
+        if (ONCHIP_TSKIP & 1) {
+            g0 = f1;
+            g1 = f0;
+        }
         cx x = o[s];
         if constexpr (LI == 0) {
             x.re = fma(g0.x, f0.x, -(g0.y * f0.y));
@@ -1641,62 +1664,6 @@ __device__ __forceinline__ void onchip_mac(__amdgpu_buffer_rsrc_t rg, uint32_t g
         x.re = fma(g1.x, f1.x, fma(-g1.y, f1.y, x.re));
         x.im = fma(g1.x, f1.y, fma(g1.y, f1.x, x.im));
         o[s] = x;
-    }
-}
-
-#ifndef ONCHIP_SPLIT_MAC
-#define ONCHIP_SPLIT_MAC 1
-#endif
-// ONCHIP_SPLIT_MAC: the two waves of sub-block q split the MAC by slots instead of by column:
-// wave (q, WR) computes slots 8 WR .. 8 WR + 7 of BOTH columns, its own row's spectrum from
-// registers and the partner row's half from the partner's buffer (half the publish stores, no LDS
-// reads of its own spectrum); the same fma chain per output element
-template <int M, int WR, int LI>
-__device__ __forceinline__ void onchip_mac_split(__amdgpu_buffer_rsrc_t rg, uint32_t gvo, const cx (&v)[16],
-                                                 const double2 *par, cx (&o)[2][8]) {
-    constexpr int P0 = (1 - LI) * 2;  // polynomial (lvl - 1)(k + 1) of row 0, lvl = L - LI
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        const int s = 8 * WR + j;
-        if (j % (ONCHIP_MAC_SB / 2 > 0 ? ONCHIP_MAC_SB / 2 : 1) == 0) __builtin_amdgcn_sched_barrier(0);
-        const double2 pp = par[s * 64];
-        const double2 mine = make_double2(v[s].re, v[s].im);
-        const double2 f0 = WR ? pp : mine, f1 = WR ? mine : pp;
-#pragma unroll
-        for (int c = 0; c < 2; c++) {
-            const double2 g0 = (ONCHIP_TSKIP & 1) ? f1 : buffer_ld_d2(rg, gvo, 16u * (uint32_t)(P0 * 2 * M + c * M + s * 64));
-            const double2 g1 =
-                (ONCHIP_TSKIP & 1) ? f0 : buffer_ld_d2(rg, gvo, 16u * (uint32_t)((P0 + 1) * 2 * M + c * M + s * 64));
-            cx x = o[c][j];
-            if constexpr (LI == 0) {
-                x.re = fma(g0.x, f0.x, -(g0.y * f0.y));
-                x.im = fma(g0.x, f0.y, g0.y * f0.x);
-            } else {
-                x.re = fma(g0.x, f0.x, fma(-g0.y, f0.y, x.re));
-                x.im = fma(g0.x, f0.y, fma(g0.y, f0.x, x.im));
-            }
-            x.re = fma(g1.x, f1.x, fma(-g1.y, f1.y, x.re));
-            x.im = fma(g1.x, f1.y, fma(g1.y, f1.x, x.im));
-            o[c][j] = x;
-        }
-    }
-}
-
-// after the split MAC: column 1 - WR of this wave's slots -> the partner's buffer (which only the
-// partner reads from here on, before its inverse rewrites it); column WR of the partner's slots
-// from this wave's buffer -> o = column WR, all 16 slots
-template <int BUF, int WR>
-__device__ __forceinline__ void onchip_gather_column(const cx (&o2)[2][8], cx (&o)[16], double2 *lds, int wave, int lane) {
-    double2 *pb = lds + (wave ^ 1) * BUF + lane;
-#pragma unroll
-    for (int j = 0; j < 8; j++) pb[(8 * WR + j) * 64] = make_double2(o2[1 - WR][j].re, o2[1 - WR][j].im);
-    __syncthreads();
-    const double2 *ob = lds + wave * BUF + lane;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        o[8 * WR + j] = o2[WR][j];
-        const double2 x = ob[(8 * (1 - WR) + j) * 64];
-        o[8 * (1 - WR) + j] = cx{x.x, x.y};
     }
 }
 
@@ -1815,27 +1782,32 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
                                   ((uint64_t)((uint32_t)e0[1] & 0xffffu) << 32) |
                                   ((uint64_t)((uint32_t)e1[1] & 0xffffu) << 48);
                 }
+        // the top stage's twist and twiddles (tv[h][b] = twist[a + 1024 b], wq[h][c] = W[a c] of
+        // butterfly a = t + 512 h): issued before the barrier that precedes their use
+        cx tv[H][R], wq[H][R];
+        auto top_loads_h = [&](int h) {
+            const uint32_t z = (uint32_t)opaque_zero();
+#pragma unroll
+            for (int b = 0; b < R; b++) tv[h][b] = ld_cx(rtw, tvo, z + 16u * (512 * h + 1024 * b));
+#pragma unroll
+            for (int c = 1; c < R; c++) wq[h][c] = ld_cx(rwt, tvo, z + 16u * ((c - 1) * 1024 + 512 * h));
+        };
+        auto top_loads = [&]() {
+#pragma unroll
+            for (int h = 0; h < H; h++) top_loads_h(h);
+        };
+        if (ONCHIP_TPF) top_loads();
         __syncthreads();  // the pairs are read: the region becomes the wave buffers
-#if ONCHIP_SPLIT_MAC
-        const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.fbsk + (size_t)i * ggsw_len + 1024 * q);
-        cx o2[2][8];  // MAC outputs of slots 8 wr .. 8 wr + 7, both columns
-        const double2 *par = lds + (wave ^ 1) * BUF + lane;
-#else
         const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.fbsk + (size_t)i * ggsw_len + (size_t)wr * M + 1024 * q);
-#endif
         cx o[16];
         auto level = [&](auto LIc) {
             constexpr int LI = decltype(LIc)::value;  // 0: level L, 1: level L-1
             // ---- twist + top DIF radix-4 of both rows -> wave buffers (large_top_fwd) ----
-            const uint32_t z = (uint32_t)opaque_zero();
+            // (level L-1: per butterfly half, where they are used -- the MAC outputs are live)
 #pragma unroll
             for (int h = 0; h < H; h++) {
                 const int a0 = t + 512 * h;
-                cx tv[R], wq[R];
-#pragma unroll
-                for (int b = 0; b < R; b++) tv[b] = ld_cx(rtw, tvo, z + 16u * (512 * h + 1024 * b));
-#pragma unroll
-                for (int c = 1; c < R; c++) wq[c] = ld_cx(rwt, tvo, z + 16u * ((c - 1) * 1024 + 512 * h));  // = W[a0 c]
+                if (!ONCHIP_TPF || LI == 1) top_loads_h(h);
 #pragma unroll
                 for (int r = 0; r < 2; r++) {
                     cx u[R];
@@ -1843,13 +1815,13 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
                     for (int b = 0; b < R; b++) {
                         const uint64_t w = pk[r][h][b] >> (32 * LI);
                         const int32_t d0 = (int32_t)(int16_t)(w & 0xffffu), d1 = (int32_t)(int16_t)((w >> 16) & 0xffffu);
-                        u[b] = cmulw(cx{(double)d0, (double)d1}, tv[b].re, tv[b].im);
+                        u[b] = cmulw(cx{(double)d0, (double)d1}, tv[h][b].re, tv[h][b].im);
                     }
                     if (!(ONCHIP_TSKIP & 8)) dftR_fwd<R>(u);
                     lds[r * BUF + a0] = make_double2(u[0].re, u[0].im);
 #pragma unroll
                     for (int c = 1; c < R; c++) {
-                        const cx y = cmulw(u[c], wq[c].re, wq[c].im);
+                        const cx y = cmulw(u[c], wq[h][c].re, wq[h][c].im);
                         lds[(2 * c + r) * BUF + a0] = make_double2(y.re, y.im);
                     }
                 }
@@ -1864,50 +1836,31 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
             }
             if (!(ONCHIP_TSKIP & 2)) SubFft::forward(v, xb, tw, lane, wsync);
             wsync();
-#if ONCHIP_SPLIT_MAC
-            // publish the partner's half of the slots; MAC of this wave's half, both columns
-            auto publish = [&](auto WRc) {
-                constexpr int WR = decltype(WRc)::value;
-#pragma unroll
-                for (int j = 0; j < 8; j++) own[(8 * (1 - WR) + j) * 64 + lane] = make_double2(v[8 * (1 - WR) + j].re, v[8 * (1 - WR) + j].im);
-            };
-            if (wr == 0) publish(std::integral_constant<int, 0>{});
-            else publish(std::integral_constant<int, 1>{});
-            __syncthreads();
-            if (wr == 0) onchip_mac_split<M, 0, LI>(rg, 16u * lane, v, par, o2);
-            else onchip_mac_split<M, 1, LI>(rg, 16u * lane, v, par, o2);
-            if constexpr (LI == 0) __syncthreads();  // the partner has read this wave's half
-#else
 #pragma unroll
             for (int s = 0; s < 16; s++) own[s * 64 + lane] = make_double2(v[s].re, v[s].im);
+            // the first slots' GGSW operands are in flight during the barrier
+            double2 pf[ONCHIP_PFS][2];
+#pragma unroll
+            for (int s = 0; s < ONCHIP_PF; s++) onchip_ggsw<M, LI>(rg, 16u * lane, s, pf[s][0], pf[s][1]);
             __syncthreads();
             // ---- MAC of this level, column wr ----
-            onchip_mac<M, BUF, LI>(rg, 16u * lane, lds + (wave & ~1) * BUF + lane, o);
+            onchip_mac<M, BUF, LI>(rg, 16u * lane, lds + (wave & ~1) * BUF + lane, o, pf);
             __syncthreads();  // the partner has read this wave's spectrum
-#endif
         };
         level(std::integral_constant<int, 0>{});
         level(std::integral_constant<int, 1>{});
-#if ONCHIP_SPLIT_MAC
-        if (wr == 0) onchip_gather_column<BUF, 0>(o2, o, lds, wave, lane);
-        else onchip_gather_column<BUF, 1>(o2, o, lds, wave, lane);
-#endif
         // ---- inverse sub-FFT of (q, column wr) -> its buffer, natural layout ----
         if (!(ONCHIP_TSKIP & 4)) SubFft::inverse(o, xb, tw, lane, wsync);
         wsync();
 #pragma unroll
         for (int b = 0; b < 16; b++) own[lane + 64 * b] = make_double2(o[b].re, o[b].im);
+        if (ONCHIP_TPF) top_loads();
         __syncthreads();
         // ---- top DIT radix-4, backward conversion, acc += (large_top_inv) ----
-        const uint32_t z = (uint32_t)opaque_zero();
+        if (!ONCHIP_TPF) top_loads();
 #pragma unroll
         for (int h = 0; h < H; h++) {
             const int a0 = t + 512 * h;
-            cx wq[R], tv[R];
-#pragma unroll
-            for (int c = 1; c < R; c++) wq[c] = ld_cx(rwt, tvo, z + 16u * ((c - 1) * 1024 + 512 * h));
-#pragma unroll
-            for (int b = 0; b < R; b++) tv[b] = ld_cx(rtw, tvo, z + 16u * (512 * h + 1024 * b));
 #pragma unroll
             for (int col = 0; col < 2; col++) {
                 cx u[R];
@@ -1918,11 +1871,11 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
 #pragma unroll
                 for (int c = 1; c < R; c++) {
                     const double2 x = lds[(2 * c + col) * BUF + a0];
-                    u[c] = cmulw(cx{x.x, x.y}, wq[c].re, -wq[c].im);
+                    u[c] = cmulw(cx{x.x, x.y}, wq[h][c].re, -wq[h][c].im);
                 }
                 if (!(ONCHIP_TSKIP & 8)) dftR_inv<R>(u);
 #pragma unroll
-                for (int b = 0; b < R; b++) backward_add(u[b], tv[b], lo[col][h][b], hi[col][h][b], k32);
+                for (int b = 0; b < R; b++) backward_add(u[b], tv[h][b], lo[col][h][b], hi[col][h][b], k32);
             }
         }
         __syncthreads();  // the buffers are read before the next rotation rewrites them
