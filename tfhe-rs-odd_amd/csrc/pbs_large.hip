@@ -1613,7 +1613,8 @@ struct OnchipCfg {
     static constexpr int H = 1024 / THREADS;  // top-stage butterflies per thread
     static constexpr int BUF = SubFft::XL;    // double2 per wave buffer
     static constexpr int S1 = 8 * BUF;        // twiddle table offset (double2 units)
-    static constexpr size_t LDS = sizeof(double2) * (S1 + SubFft::Lds::s1_len);
+    static constexpr int FLAGS = S1 + SubFft::Lds::s1_len;  // pair-sync flags (double2 offset), one word per wave
+    static constexpr size_t LDS = sizeof(double2) * FLAGS + 4 * 8;
     static_assert(R == 4, "8 waves = 4 sub-blocks x 2 rows");
     static_assert(8 * BUF * sizeof(double2) == 2 * M * sizeof(acc_pair), "the rotation's pairs fill the wave buffers");
 };
@@ -1621,6 +1622,9 @@ struct OnchipCfg {
 // MAC of level L - LI for one sub-block: both rows' spectra from their buffers F (row r at
 // F + r BUF; the own one too, so its registers are free here); o accumulates over levels L..1
 // and rows 0..k in the oracle's order (sub_cmux_body's forms)
+#ifndef ONCHIP_PAIRSYNC
+#define ONCHIP_PAIRSYNC 1  // the publish -> MAC sync through the pair's LDS flags instead of a barrier
+#endif
 #ifndef ONCHIP_TPF
 #define ONCHIP_TPF 1  // top-stage twist / twiddle loads issued before the barrier preceding their use
 #endif
@@ -1707,6 +1711,9 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
     double2 *s1 = lds + Cfg::S1;
     // sub-block stage twiddles W_1024[lane c] = W_M[R lane c]  (oracle dif_rec tstride R)
     for (int e = t; e < SubFft::Lds::s1_len; e += Cfg::THREADS) s1[e] = a.W[R * (e & 63) * ((e >> 6) + 1)];
+    if (t < 8) reinterpret_cast<uint32_t *>(lds + Cfg::FLAGS)[t] = 0;
+    GroupSync<2> ps;  // the two waves of sub-block q (flag words 2 q, 2 q + 1)
+    ps.mine = lds_addr(lds + Cfg::FLAGS) + 4u * wave;
     const SubFft::Lds tw{s1, s1};
     cx *xb = reinterpret_cast<cx *>(lds) + wave * BUF;
     double2 *own = lds + wave * BUF;
@@ -1842,7 +1849,8 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
             double2 pf[ONCHIP_PFS][2];
 #pragma unroll
             for (int s = 0; s < ONCHIP_PF; s++) onchip_ggsw<M, LI>(rg, 16u * lane, s, pf[s][0], pf[s][1]);
-            __syncthreads();
+            if (ONCHIP_PAIRSYNC) ps();  // only the partner reads this spectrum
+            else __syncthreads();
             // ---- MAC of this level, column wr ----
             onchip_mac<M, BUF, LI>(rg, 16u * lane, lds + (wave & ~1) * BUF + lane, o, pf);
             __syncthreads();  // the partner has read this wave's spectrum
