@@ -1753,7 +1753,16 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
     }
     const double k32 = torus_k32();
     const int beta = a.base_log;
-    __syncthreads();  // twiddle table
+    // accumulator pair (row r, j) <-> LDS slot (2 (j >> 10) + r) BUF + (j & 1023): the slots thread t
+    // owns, (2 b + r) BUF + t + 512 h, are exactly the top-stage / top-inverse slots of its butterflies,
+    // so the top inverse writes the updated pairs in place (no barrier between its reads and them)
+    auto pslot = [](int r, int j) { return (2 * (j >> 10) + r) * BUF + (j & 1023); };
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+#pragma unroll
+        for (int h = 0; h < H; h++)
+#pragma unroll
+            for (int b = 0; b < R; b++) pairs[(2 * b + r) * BUF + t + 512 * h] = acc_pair{lo[r][h][b], hi[r][h][b]};
 
     uint64_t a_next = in[0];
     for (int i = 0; i < a.n; i++) {
@@ -1762,13 +1771,7 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
         const bool full_odd = (at / N) & 1;
         const int rem = at % N;
         // ---- rotation + decomposition (split_digits through LDS) ----
-#pragma unroll
-        for (int r = 0; r < 2; r++)
-#pragma unroll
-            for (int h = 0; h < H; h++)
-#pragma unroll
-                for (int b = 0; b < R; b++) pairs[r * M + t + 512 * h + 1024 * b] = acc_pair{lo[r][h][b], hi[r][h][b]};
-        __syncthreads();
+        __syncthreads();  // every pair written (and, at i = 0, the twiddle table)
         uint64_t pk[2][H][R];  // int16 digits: level L at j, j + M; level L-1 at j, j + M
 #pragma unroll
         for (int r = 0; r < 2; r++)
@@ -1778,7 +1781,7 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
                 for (int b = 0; b < R; b++) {
                     const int j = t + 512 * h + 1024 * b;
                     const int jj0 = j - rem;  // in (-N, M)
-                    const acc_pair rot = (ONCHIP_TSKIP & 16) ? acc_pair{lo[r][h][b] * 3, hi[r][h][b]} : pairs[r * M + (jj0 & (M - 1))];
+                    const acc_pair rot = (ONCHIP_TSKIP & 16) ? acc_pair{lo[r][h][b] * 3, hi[r][h][b]} : pairs[pslot(r, jj0 & (M - 1))];
                     const bool swap = jj0 < 0 && jj0 >= -M;
                     const uint64_t x0 = swap ? rot.y : rot.x, x1 = swap ? rot.x : rot.y;
                     const bool neg0 = (jj0 < 0) != full_odd, neg1 = (jj0 + M < 0) != full_odd;
@@ -1883,21 +1886,19 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
                 }
                 if (!(ONCHIP_TSKIP & 8)) dftR_inv<R>(u);
 #pragma unroll
-                for (int b = 0; b < R; b++) backward_add(u[b], tv[h][b], lo[col][h][b], hi[col][h][b], k32);
+                for (int b = 0; b < R; b++) {
+                    backward_add(u[b], tv[h][b], lo[col][h][b], hi[col][h][b], k32);
+                    pairs[(2 * b + col) * BUF + a0] = acc_pair{lo[col][h][b], hi[col][h][b]};  // = slot read above
+                }
             }
         }
-        __syncthreads();  // the buffers are read before the next rotation rewrites them
     }
-    // ---- sample extract at degree 0 (large_extract_kernel) from the registers ----
-#pragma unroll
-    for (int h = 0; h < H; h++)
-#pragma unroll
-        for (int b = 0; b < R; b++) pairs[t + 512 * h + 1024 * b] = acc_pair{lo[0][h][b], hi[0][h][b]};
+    // ---- sample extract at degree 0 (large_extract_kernel) from the pairs ----
     __syncthreads();
     uint64_t *out = a.lwe_out + (size_t)ct * ((size_t)K * N + 1);
     for (int e = t; e < N; e += Cfg::THREADS) {
         const int p = e == 0 ? 0 : N - e;
-        const acc_pair pr = pairs[p & (M - 1)];
+        const acc_pair pr = pairs[pslot(0, p & (M - 1))];
         const uint64_t x = p >= M ? pr.y : pr.x;
         out[e] = e == 0 ? x : 0 - x;
     }
