@@ -38,7 +38,10 @@
  *     of at most three (classic) / two (multi-bit g = 2, 3) passes of one ciphertext per CU (768 /
  *     512 rows on 256 CUs: the measured crossovers against the throughput kernels) run the
  *     one-ciphertext-per-CU latency kernels (same outputs; TFHE_MI355_LATENCY_MAX = rows
- *     overrides, 0 = never).
+ *     overrides, 0 = never).  At N = 8192, k = 1, L = 2 (classic), batches of at least 3/8 of the
+ *     CU count (96 rows on 256 CUs) run the on-chip CMUX (the whole blind rotation in one
+ *     workgroup per ciphertext, no scratch used), smaller ones the split CMUX (same outputs;
+ *     TFHE_MI355_ONCHIP_MIN = rows overrides, TFHE_MI355_ONCHIP=0 = never).
  *     The _async calls hold no per-context mutable state: every device scratch buffer they
  *     need comes from the caller (d_scratch, sized by the matching *_scratch query; a call
  *     given less than its query fails with an error, and only a query returning 0 allows
@@ -227,6 +230,7 @@ int tfhe_mi355_programmable_bootstrap_async(TfheMi355Context *ctx, const uint64_
  *     N = 1024 k = 2 L = 3, N = 256 k = 5 L = 1 -- and 0 at the other classic shapes;
  *   - multi-bit N = 2048 / 512: 0;
  *   - N >= 4096, classic and multi-bit (N = 8192): the accumulators + spectra of one pass of
+ *     the split CMUX (also asked for where the on-chip CMUX will run: the call picks by count)
  *     min(count, chunk) ciphertexts (chunk = 128 at N = 32768; below, ~200 MiB worth in multiples
  *     of 64, at most 1024: 1024 at N = 4096, 512 at N = 8192 (3_3 and multi-bit 3_3), 256 / 192
  *     at N = 16384, L = 2 / 3; TFHE_MI355_LARGE_CHUNK overrides; e.g. 1.5 MiB per ciphertext at 4_4).  Less scratch runs smaller passes; the call fails below one

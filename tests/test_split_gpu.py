@@ -146,6 +146,30 @@ def test_split_pbs_chunks_ragged(orc):
     assert np.array_equal(got[sample], fbsk.pbs(cts[sample], acc, threads=5))
 
 
+def test_onchip_and_split_cmux_agree(orc):
+    """N = 8192, L = 2: a 130-ciphertext call runs the on-chip CMUX (onchip_cmux_kernel, >= 96 rows on
+    256 CUs: capi.cpp onchip_min), the same ciphertexts in calls of 65 the digits-fed split CMUX;
+    every row identical, a sample bit-exact against the oracle, edge masks included."""
+    from tfhe_mi355.parameters import PARAM_MESSAGE_3_CARRY_3_KS_PBS
+
+    p = PARAM_MESSAGE_3_CARRY_3_KS_PBS.with_(lwe_dimension=6)
+    lwe_sk, glwe_sk, bsk, fbsk = _keys(orc, p, 77)
+    eng = _engine(p, bsk)
+    msgs = np.random.default_rng(5).integers(0, 64, 130)
+    cts = orc.lwe_encrypt(78, lwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta), p.lwe_modular_std_dev)
+    cts[0, :-1] = 0                                   # every a~ = 0
+    cts[1, :-1] = np.uint64(1 << 63)                  # a~ = N
+    cts[2, -1] = np.uint64((1 << 64) - 1)             # b~ = 2N
+    acc = orc.fill_accumulator(p.polynomial_size, 1, 8, 8, lambda x: (x * 7 + 2) % 64)
+    whole = eng.programmable_bootstrap(cts, acc)
+    halves = np.concatenate([eng.programmable_bootstrap(cts[:65], acc), eng.programmable_bootstrap(cts[65:], acc)])
+    assert np.array_equal(whole, halves), f"{np.count_nonzero(np.any(whole != halves, axis=1))} rows differ"
+    sample = np.array([0, 1, 2, 64, 65, 129])
+    assert np.array_equal(whole[sample], fbsk.pbs(cts[sample], acc, threads=6))
+    dec = decode(orc.lwe_decrypt(glwe_sk, whole[3:]), p.delta) % 64
+    assert np.array_equal(dec, (msgs[3:] * 7 + 2) % 64)
+
+
 @pytest.mark.timeout(900)
 def test_full_3_3_keyswitch_pbs(orc):
     """Full PARAM_MESSAGE_3_CARRY_3_KS_PBS (n = 864, N = 8192, L = 2; the reference's 121 ms

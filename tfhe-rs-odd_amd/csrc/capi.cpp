@@ -368,6 +368,19 @@ size_t pbs_scratch_bytes(const TfheMi355Context *c, size_t count) {
     return per_ct * std::min(count, large_chunk(c));
 }
 
+// The on-chip N = 8192 CMUX (one ciphertext per CU for the whole blind rotation) against the
+// digits-fed split CMUX (a ciphertext's sub-blocks over several CUs): at 3_3 the split path takes
+// 16.3 / 18.8 / 23.2 / 25.4 ms for 1 / 64 / 96 / 128 ciphertexts, the on-chip one 22.9-25.1 ms
+// for any count up to one per CU (profiles/r05_sweep33_onchip{0,1}.json), so the on-chip kernel
+// from 3/8 of the CU count (96 on MI355X) on.  TFHE_MI355_ONCHIP_MIN overrides.
+size_t onchip_min(const TfheMi355Context *c) {
+    static const long env = [] {
+        const char *e = std::getenv("TFHE_MI355_ONCHIP_MIN");
+        return e && *e ? std::strtol(e, nullptr, 10) : -1L;
+    }();
+    return env >= 0 ? (size_t)env : (size_t)c->cus * 3 / 8;
+}
+
 // Batches of at most this many ciphertexts run the latency kernels (one ciphertext per CU) at the
 // shapes they support.  Chosen by predicted time: the latency kernel takes one pass per CU-full of
 // ciphertexts, the throughput kernel a time that steps with its ciphertexts per CU (<= 1024 rows:
@@ -484,6 +497,7 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
         a.scratch_bytes = std::min(scratch_bytes, per_ct * large_chunk(c));
         a.timer = c->timer_or_null();
         a.grouping = (int)c->p.grouping_factor;
+        a.onchip_min_count = (int)onchip_min(c);
         check(launch_large_pbs((int)c->N(), (int)c->k(), (int)c->p.pbs_level, a, s), "launch large pbs");
         return;
     }

@@ -185,6 +185,7 @@ struct LargePbsLaunch {
     int chunk_count;             // set by the launcher: ciphertexts in the current chunk
     KernelTimer *timer = nullptr;  // optional per-kernel timing
     int grouping = 0;              // > 0: multi-bit PBS (fbsk = [n/g][2^g][L][k+1][k+1] polys)
+    int onchip_min_count = 0;      // N = 8192, L = 2 classic: the on-chip CMUX from this many ciphertexts on
 };
 bool large_pbs_supported(int N, int k, int L);
 bool large_multibit_supported(int N, int k, int L, int g);

@@ -2075,7 +2075,7 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
     using S = Split<N>;
     if (a0.count == 0) return hipSuccess;
     if constexpr (G == 0 && K == 1 && L == 2 && S::R == 4) {
-        if (onchip_enabled()) {  // the whole blind rotation on chip, no scratch
+        if (onchip_enabled() && a0.count >= a0.onchip_min_count) {  // the whole blind rotation on chip, no scratch
             TimedLaunch tl(a0.timer, "onchip_cmux_kernel", s);
             if (a0.base_log * 2 <= 30)  // 32-bit digit extraction (every shortint set at this shape)
                 hipLaunchKernelGGL((onchip_cmux_kernel<N, true>), dim3((unsigned)a0.count), dim3(OnchipCfg<N>::THREADS),
