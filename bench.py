@@ -114,7 +114,8 @@ def _split_params():
         out[tag] = (name, f"shortint apply_lookup_table (keyswitch -> PBS) at {name} (shortint/parameters/mod.rs:"
                           f"{SHORTINT_SOURCE_LINE[name]}), N={p.polynomial_size}, batch per GPU; the reference publishes "
                           + ("121 ms per KS+PBS at 3_3 (benchmarks.md:42)" if tag == "3_3" else "no number for this set"),
-                    (f"onchip_cmux_kernel<{p.polynomial_size}> (the whole blind rotation per workgroup, ks_mfma_kernel)"
+                    (f"onchip_cmux_kernel<{p.polynomial_size},{'true' if 2 * p.pbs_base_log <= 30 else 'false'}> "
+                     "(the whole blind rotation per workgroup, ks_mfma_kernel)"
                      if p.pbs_level == 2 and p.polynomial_size == 8192 and os.environ.get("TFHE_MI355_ONCHIP", "1") != "0"
                      else f"large_dsub_kernel<{p.polynomial_size}> (+ split_digits/large_top_inv per CMUX, ks_mfma_kernel)"
                      if p.pbs_level == 2 and p.polynomial_size <= 8192 else
