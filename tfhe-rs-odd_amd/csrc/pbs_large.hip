@@ -808,6 +808,10 @@ __global__ void __launch_bounds__((PairSubCfg<K, L>::THREADS), 2) large_pair_sub
 // 0..k) are those of the kernel above, so the outputs are bit-identical.  TFHE_MI355_MB_PAIR2=0
 // selects the kernel above (A/B).
 // ---------------------------------------------------------------------------------------
+#ifndef MB2_TSKIP
+#define MB2_TSKIP 0  // timing-only builds (wrong outputs): 1 no GGSW loads, 2 no forward sub-FFTs, 4 no
+                     // inverse sub-FFTs, 8 no keybundle sums (PBS_MB_TSKIP_MONO=1: conflict-free monomials)
+#endif
 template <int N, int G>
 struct MbPair2Cfg {
     static constexpr int K = 1, L = 2, CPW = 2, PW = (K + 1) * L, WAVES = CPW * PW, THREADS = 64 * WAVES;
@@ -853,7 +857,7 @@ __global__ void __launch_bounds__((MbPair2Cfg<N, G>::THREADS), 2) large_mb_pair2
         for (int b = 0; b < 16; b++) v[b] = gld(src + 64 * b);
         __syncthreads();  // twiddle table
         cx *xb = reinterpret_cast<cx *>(lds) + wave * SubFft::XL;
-        SubFft::forward(v, xb, tw, lane, wsync);
+        if (!(MB2_TSKIP & 2)) SubFft::forward(v, xb, tw, lane, wsync);
     }
     // monomial degrees of each ciphertext's 2^g - 1 non-constant GGSWs (wave-uniform)
     uint32_t deg[CPW][NSEL];
@@ -914,7 +918,7 @@ __global__ void __launch_bounds__((MbPair2Cfg<N, G>::THREADS), 2) large_mb_pair2
                 for (int r = 0; r <= K; r++)
 #pragma unroll
                     for (int sel = 0; sel < NSEL; sel++)
-                        g[r][sel] = buffer_ld_d2(grs, gvo,
+                        g[r][sel] = (MB2_TSKIP & 1) ? make_double2(1.0 + sel, 0.5 * r) : buffer_ld_d2(grs, gvo,
                                                  (uint32_t)(16u * sel * ggsw_len) + (uint32_t)((lvl - 1) * (K + 1) + r) * rowb +
                                                      16u * (uint32_t)(col * M) + 1024u * (uint32_t)s);
 #pragma unroll
@@ -923,7 +927,7 @@ __global__ void __launch_bounds__((MbPair2Cfg<N, G>::THREADS), 2) large_mb_pair2
                     for (int r = 0; r <= K; r++) {
                         double2 kb = g[r][0];
 #pragma unroll
-                        for (int sel = 1; sel < NSEL; sel++) {
+                        for (int sel = 1; sel < ((MB2_TSKIP & 8) ? 1 : NSEL); sel++) {
                             kb.x = fma(g[r][sel].x, mono[c][sel].re, fma(-g[r][sel].y, mono[c][sel].im, kb.x));
                             kb.y = fma(g[r][sel].x, mono[c][sel].im, fma(g[r][sel].y, mono[c][sel].re, kb.y));
                         }
@@ -960,7 +964,7 @@ __global__ void __launch_bounds__((MbPair2Cfg<N, G>::THREADS), 2) large_mb_pair2
     }
     cx *xb = reinterpret_cast<cx *>(oslot(c, col, 0) - lane);  // this column's 16 KiB: its exchange block
     wsync();
-    SubFft::inverse(v, xb, tw, lane, wsync);
+    if (!(MB2_TSKIP & 4)) SubFft::inverse(v, xb, tw, lane, wsync);
     if (2 * cp + c >= cnt) return;
     double2 *dst = spectra(c) + (size_t)col * M + 1024 * q + lane;  // (lvl 1, row col) slot: this WG only
     store_sub_out<LARGE_SUB_AUX>(dst, v, lane);
