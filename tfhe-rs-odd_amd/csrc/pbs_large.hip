@@ -808,6 +808,9 @@ __global__ void __launch_bounds__((PairSubCfg<K, L>::THREADS), 2) large_pair_sub
 // 0..k) are those of the kernel above, so the outputs are bit-identical.  TFHE_MI355_MB_PAIR2=0
 // selects the kernel above (A/B).
 // ---------------------------------------------------------------------------------------
+#ifndef MB2_PIPE
+#define MB2_PIPE 1  // phase 2's GGSW operand batches software pipelined (0: one (level, column) batch at a time)
+#endif
 #ifndef MB2_TSKIP
 #define MB2_TSKIP 0  // timing-only builds (wrong outputs): 1 no GGSW loads, 2 no forward sub-FFTs, 4 no
                      // inverse sub-FFTs, 8 no keybundle sums (PBS_MB_TSKIP_MONO=1: conflict-free monomials)
@@ -892,14 +895,66 @@ __global__ void __launch_bounds__((MbPair2Cfg<N, G>::THREADS), 2) large_mb_pair2
         // ---- publish slots 8h .. 8h + 7 of this wave's spectrum ----
 #pragma unroll
         for (int sl = 0; sl < 8; sl++) *hslot(c1, p1, sl) = make_double2(v[8 * h + sl].re, v[8 * h + sl].im);
-        __syncthreads();  // (h = 0: also the twist planes)
         const int s = 8 * h + wave;  // this wave's slot in round h (wave-uniform)
+#if MB2_PIPE
+        // the round's 8 operand batches (level, column, row) of 2^g GGSW values each, software
+        // pipelined: batch k + 1 in flight while batch k is consumed (the same registers as one
+        // (level, column) batch); batch 0 is issued before the barrier
+        auto gload = [&](int st, double2 (&g)[NSEL]) {
+            const int lv = L - (st >> 2), cl = (st >> 1) & 1, rr = st & 1;
+#pragma unroll
+            for (int sel = 0; sel < NSEL; sel++)
+                g[sel] = (MB2_TSKIP & 1) ? make_double2(1.0 + sel, 0.5 * rr)
+                                         : buffer_ld_d2(grs, gvo, (uint32_t)(16u * sel * ggsw_len) +
+                                                                      (uint32_t)((lv - 1) * (K + 1) + rr) * rowb +
+                                                                      16u * (uint32_t)(cl * M) + 1024u * (uint32_t)s);
+        };
+        double2 gb[2][NSEL];
+        gload(0, gb[0]);
+#endif
+        __syncthreads();  // (h = 0: also the twist planes)
         const uint32_t f = fl + (uint32_t)R * SubFft::freq_slot(s);
         cx mono[CPW][NSEL];
 #pragma unroll
         for (int c = 0; c < CPW; c++)
 #pragma unroll
             for (int sel = 1; sel < NSEL; sel++) mono[c][sel] = Tw::mono(deg[c][sel] - 4u * deg[c][sel] * f);
+#if MB2_PIPE
+        cx ff[CPW][K + 1];
+#pragma unroll
+        for (int st = 0; st < 8; st++) {
+            const int lvl = L - (st >> 2), col = (st >> 1) & 1, r = st & 1;
+            __builtin_amdgcn_sched_barrier(0);
+            if (st + 1 < 8) gload(st + 1, gb[(st + 1) & 1]);
+            if (st % 4 == 0) {
+#pragma unroll
+                for (int c = 0; c < CPW; c++)
+#pragma unroll
+                    for (int rr = 0; rr <= K; rr++) {
+                        const double2 t = *hslot(c, (lvl - 1) * (K + 1) + rr, wave);
+                        ff[c][rr] = cx{t.x, t.y};
+                    }
+            }
+            const double2 (&g)[NSEL] = gb[st & 1];
+#pragma unroll
+            for (int c = 0; c < CPW; c++) {
+                double2 kb = g[0];
+#pragma unroll
+                for (int sel = 1; sel < ((MB2_TSKIP & 8) ? 1 : NSEL); sel++) {
+                    kb.x = fma(g[sel].x, mono[c][sel].re, fma(-g[sel].y, mono[c][sel].im, kb.x));
+                    kb.y = fma(g[sel].x, mono[c][sel].im, fma(g[sel].y, mono[c][sel].re, kb.y));
+                }
+                cx &oc = o[h][c][col];
+                if (lvl == L && r == 0) {
+                    oc.re = fma(kb.x, ff[c][r].re, -(kb.y * ff[c][r].im));
+                    oc.im = fma(kb.x, ff[c][r].im, kb.y * ff[c][r].re);
+                } else {
+                    oc.re = fma(kb.x, ff[c][r].re, fma(-kb.y, ff[c][r].im, oc.re));
+                    oc.im = fma(kb.x, ff[c][r].im, fma(kb.y, ff[c][r].re, oc.im));
+                }
+            }
+        }
+#else
 #pragma unroll
         for (int lvl = L; lvl >= 1; lvl--) {
             cx ff[CPW][K + 1];
@@ -943,6 +998,7 @@ __global__ void __launch_bounds__((MbPair2Cfg<N, G>::THREADS), 2) large_mb_pair2
                 }
             }
         }
+#endif
         __syncthreads();  // every wave has read round h's half buffer
     }
     // ---- phase 3: outputs -> the half buffer as [c][col][16 slots][64], inverse sub-FFTs ----
