@@ -269,6 +269,37 @@ def test_split_multi_bit_pbs_bit_exact_vs_oracle(orc, name):
     assert np.array_equal(eng.programmable_bootstrap(edge, luts[0]), fb.pbs(edge, luts[0], threads=3))
 
 
+@pytest.mark.parametrize("name", MB_SPLIT)
+def test_onchip_and_split_multi_bit_agree(orc, name):
+    """Multi-bit N = 8192: a 130-ciphertext call and the same ciphertexts in calls of 65 (both through
+    large_mb_pair2_kernel by default; the on-chip kernel's multi-bit instantiation when the suite runs
+    with TFHE_MI355_ONCHIP_MB=1, as profiles/r05_onchip_mb_tests.log did); every row identical, a sample
+    bit-exact against the oracle."""
+    from tfhe_mi355 import client
+    from tfhe_mi355.parameters import MULTI_BIT_ALL
+
+    p = MULTI_BIT_ALL[name].with_(lwe_dimension=6)
+    N, g = p.polynomial_size, p.grouping_factor
+    lwe_sk = client.gen_binary_key(121, 1, p.lwe_dimension)
+    glwe_sk = client.gen_binary_key(121, 2, p.big_lwe_dimension)
+    bsk = client.gen_multi_bit_bootstrap_key(122, lwe_sk, glwe_sk, 1, N, p.pbs_base_log, p.pbs_level, g,
+                                             p.glwe_modular_std_dev, threads=8)
+    fb = orc.MultiBitFourierBsk(bsk, p.lwe_dimension, 1, N, p.pbs_base_log, p.pbs_level, g)
+    eng = _engine(p, bsk)
+    msgs = np.random.default_rng(6).integers(0, 64, 130)
+    cts = orc.lwe_encrypt(123, lwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta), p.lwe_modular_std_dev)
+    cts[0, :-1] = 0
+    cts[1, :-1] = np.uint64(1 << 63)
+    cts[2, -1] = np.uint64((1 << 64) - 1)
+    acc = orc.fill_accumulator(N, 1, 8, 8, lambda x: (x * 5 + 1) % 64)
+    whole = eng.programmable_bootstrap(cts, acc)
+    halves = np.concatenate([eng.programmable_bootstrap(cts[:65], acc), eng.programmable_bootstrap(cts[65:], acc)])
+    assert np.array_equal(whole, halves), f"{np.count_nonzero(np.any(whole != halves, axis=1))} rows differ"
+    sample = np.array([0, 1, 2, 64, 129])
+    assert np.array_equal(whole[sample], fb.pbs(cts[sample], acc, threads=5))
+    assert np.array_equal(decode(orc.lwe_decrypt(glwe_sk, whole[3:]), p.delta) % 64, (msgs[3:] * 5 + 1) % 64)
+
+
 @pytest.mark.timeout(900)
 def test_full_multi_bit_3_3_group_3_decrypts(orc):
     """Full PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_3_KS_PBS (n = 972, N = 8192): KS -> PBS of 64
