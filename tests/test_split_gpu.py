@@ -271,10 +271,10 @@ def test_split_multi_bit_pbs_bit_exact_vs_oracle(orc, name):
 
 @pytest.mark.parametrize("name", MB_SPLIT)
 def test_onchip_and_split_multi_bit_agree(orc, name):
-    """Multi-bit N = 8192: a 130-ciphertext call and the same ciphertexts in calls of 65 (both through
-    large_mb_pair2_kernel by default; the on-chip kernel's multi-bit instantiation when the suite runs
-    with TFHE_MI355_ONCHIP_MB=1, as profiles/r05_onchip_mb_tests.log did); every row identical, a sample
-    bit-exact against the oracle."""
+    """Multi-bit N = 8192: a 130-ciphertext call (one 512-ciphertext chunk of the split CMUX with a
+    partial pair) and the same ciphertexts in calls of 65 (odd counts: a pair workgroup with an idle
+    slot); every row identical, a sample bit-exact against the oracle.  (Round 5 also ran it against
+    the measured-slower multi-bit on-chip CMUX: profiles/r05_onchip_mb_tests.log.)"""
     from tfhe_mi355 import client
     from tfhe_mi355.parameters import MULTI_BIT_ALL
 

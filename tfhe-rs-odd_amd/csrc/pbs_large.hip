@@ -1731,70 +1731,6 @@ __device__ __forceinline__ void onchip_mac(__amdgpu_buffer_rsrc_t rg, uint32_t g
     }
 }
 
-// a zero the compiler cannot see through: table pointers offset by it (the twist, the top-stage
-// twiddles, the CMUX's GGSW) are not provably loop-invariant, so their loads stay where they are
-// used instead of being hoisted out of the CMUX loop into registers held for good (an opaque
-// pointer instead would lose its address space: flat loads, counted against the LDS waits too)
-__device__ __forceinline__ int opaque_zero() {
-    int z = 0;
-    asm volatile("" : "+s"(z));
-    return z;
-}
-
-// Multi-bit MAC of level L - LI for one sub-block (G > 0): per slot, the keybundle of each row,
-// KB = G_0 + sum_sel X^(deg_sel) G_sel in selector order (the monomial spectra from the global
-// twist table, mono_spectrum), then the classic MAC with KB in place of the GGSW operand --
-// large_pair_sub_kernel's forms, so bit-identical
-template <int N, int BUF, int LI, int G>
-__device__ __forceinline__ void onchip_mac_mb(__amdgpu_buffer_rsrc_t rg, uint32_t gvo, const double2 *F, cx (&o)[16],
-                                              const double2 *__restrict__ twist, const uint32_t (&deg)[1 << G],
-                                              uint32_t fl) {
-    constexpr int M = N / 2, R = M / 1024, NSEL = 1 << G;
-    constexpr uint32_t sel_b = 16u * (uint32_t)(2 * 2 * 2 * M);  // bytes per GGSW of the group
-    constexpr int P0 = (1 - LI) * 2;                             // polynomial (lvl - 1)(k + 1) of row 0
-#pragma unroll
-    for (int s = 0; s < 16; s++) {
-        __builtin_amdgcn_sched_barrier(0);  // one slot's operands in flight
-        // (an opaque zero in every address of the slot: the IR passes may not hoist the next slots'
-        // loads above this one -- unrolled, that holds all 16 slots' operands and spills)
-        const int z = opaque_zero();
-        const uint32_t f = fl + (uint32_t)R * SubFft::freq_slot(s);
-        cx mono[NSEL];
-#pragma unroll
-        for (int sel = 1; sel < NSEL; sel++) {  // mono_spectrum's quadrant rule, branch-free
-            const uint32_t tt = (deg[sel] - 4u * deg[sel] * f) & (uint32_t)(2 * N - 1);
-            const uint32_t qd = tt / (uint32_t)M;
-            const double2 w = twist[z + (int)(tt % (uint32_t)M)];
-            const bool sw = qd & 1u;
-            const double re = sw ? w.y : w.x, im = sw ? w.x : w.y;
-            mono[sel] = cx{(qd == 1u || qd == 2u) ? -re : re, qd >= 2u ? -im : im};
-        }
-        const double2 fr[2] = {F[s * 64], F[BUF + s * 64]};
-        cx x = o[s];
-#pragma unroll
-        for (int r = 0; r < 2; r++) {
-            if (r) __builtin_amdgcn_sched_barrier(0);  // one row's 2^g operands in flight
-            const uint32_t so = (uint32_t)z + 16u * (uint32_t)((P0 + r) * 2 * M + s * 64);
-            double2 kb = buffer_ld_d2(rg, gvo, so);
-#pragma unroll
-            for (int sel = 1; sel < NSEL; sel++) {
-                const double2 g = buffer_ld_d2(rg, gvo, so + sel * sel_b);
-                kb.x = fma(g.x, mono[sel].re, fma(-g.y, mono[sel].im, kb.x));
-                kb.y = fma(g.x, mono[sel].im, fma(g.y, mono[sel].re, kb.y));
-            }
-            const double2 ff = fr[r];
-            if (LI == 0 && r == 0) {
-                x.re = fma(kb.x, ff.x, -(kb.y * ff.y));
-                x.im = fma(kb.x, ff.y, kb.y * ff.x);
-            } else {
-                x.re = fma(kb.x, ff.x, fma(-kb.y, ff.y, x.re));
-                x.im = fma(kb.x, ff.y, fma(kb.y, ff.x, x.im));
-            }
-        }
-        o[s] = x;
-    }
-}
-
 // decompose64<2> in 32-bit registers when base_log * 2 <= 30 (pbs_common.h decomp_state32: the
 // same digits)
 template <bool D32>
@@ -1809,17 +1745,22 @@ __device__ __forceinline__ void onchip_decompose(uint64_t x, int beta, int32_t (
     }
 }
 
-// G > 0: the multi-bit PBS (lwe_multi_bit_programmable_bootstrapping.rs:548-828) through the same
-// kernel -- one group of G mask elements per step, no rotation (the external product's input is the
-// accumulator itself), the keybundle built per slot inside the MAC (onchip_mac_mb), the top inverse
-// overwriting the accumulator (the reference's zeroed ping-pong destination)
-template <int N, bool D32, int G>
+// a zero the compiler cannot see through: table pointers offset by it (the twist, the top-stage
+// twiddles, the CMUX's GGSW) are not provably loop-invariant, so their loads stay where they are
+// used instead of being hoisted out of the CMUX loop into registers held for good (an opaque
+// pointer instead would lose its address space: flat loads, counted against the LDS waits too)
+__device__ __forceinline__ int opaque_zero() {
+    int z = 0;
+    asm volatile("" : "+s"(z));
+    return z;
+}
+
+template <int N, bool D32>
 __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
     using S = Split<N>;
     using Cfg = OnchipCfg<N>;
     constexpr int K = 1, L = 2, M = S::M, R = S::R, H = Cfg::H, BUF = Cfg::BUF;
     constexpr size_t ggsw_len = (size_t)L * (K + 1) * (K + 1) * M;
-    constexpr int NSEL = 1 << G;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double2 *lds = reinterpret_cast<double2 *>(smem);
     acc_pair *pairs = reinterpret_cast<acc_pair *>(smem);  // rotation view: [row][M] pairs
@@ -1883,57 +1824,14 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
 #pragma unroll
             for (int b = 0; b < R; b++) pairs[(2 * b + r) * BUF + t + 512 * h] = acc_pair{lo[r][h][b], hi[r][h][b]};
 
-    const int steps = G ? a.n / G : a.n;  // CMUXes, or multi-bit groups
     uint64_t a_next = in[0];
-    uint64_t g_next[G > 0 ? G : 1];  // multi-bit: the next group's mask elements
-    if constexpr (G > 0) {
-#pragma unroll
-        for (int b = 0; b < G; b++) g_next[b] = in[b];
-    }
-    // this thread's X^{a~} acc - acc (classic) or acc (multi-bit) pair of row r at j = t + 512 h + 1024 b
-    auto ct1 = [&](int r, int h, int b, int rem, bool full_odd, uint64_t &d0, uint64_t &d1) {
-        if constexpr (G > 0) {
-            d0 = lo[r][h][b];
-            d1 = hi[r][h][b];
-        } else {
-            const int j = t + 512 * h + 1024 * b;
-            const int jj0 = j - rem;  // in (-N, M)
-            const acc_pair rot = (ONCHIP_TSKIP & 16) ? acc_pair{lo[r][h][b] * 3, hi[r][h][b]} : pairs[pslot(r, jj0 & (M - 1))];
-            const bool swap = jj0 < 0 && jj0 >= -M;
-            const uint64_t x0 = swap ? rot.y : rot.x, x1 = swap ? rot.x : rot.y;
-            const bool neg0 = (jj0 < 0) != full_odd, neg1 = (jj0 + M < 0) != full_odd;
-            d0 = (neg0 ? 0 - x0 : x0) - lo[r][h][b];
-            d1 = (neg1 ? 0 - x1 : x1) - hi[r][h][b];
-        }
-    };
-    for (int i = 0; i < steps; i++) {
-        int rem = 0;
-        bool full_odd = false;
-        uint32_t deg[NSEL];  // multi-bit: monomial degrees of the group's 2^g - 1 non-constant GGSWs
-        if constexpr (G == 0) {
-            const uint32_t at = pbs_modulus_switch<S::LOGN>(a_next);
-            a_next = in[i + 1 < a.n ? i + 1 : i];  // next mask element: its load latency hides behind this CMUX
-            full_odd = (at / N) & 1;
-            rem = at % N;
-        } else {
-            uint64_t gm[G];
-#pragma unroll
-            for (int b = 0; b < G; b++) gm[b] = g_next[b];
-            const int nx = i + 1 < steps ? i + 1 : i;
-#pragma unroll
-            for (int b = 0; b < G; b++) g_next[b] = in[(size_t)nx * G + b];
-            deg[0] = 0;
-#pragma unroll
-            for (int sel = 1; sel < NSEL; sel++) {  // as large_pair_sub_kernel: the raw sum, then the switch
-                uint64_t d = 0;
-#pragma unroll
-                for (int b = 0; b < G; b++)
-                    if ((sel >> (G - 1 - b)) & 1) d += gm[b];
-                deg[sel] = pbs_modulus_switch<S::LOGN>(d);
-            }
-        }
+    for (int i = 0; i < a.n; i++) {
+        const uint32_t at = pbs_modulus_switch<S::LOGN>(a_next);
+        a_next = in[i + 1 < a.n ? i + 1 : i];  // next mask element: its load latency hides behind this CMUX
+        const bool full_odd = (at / N) & 1;
+        const int rem = at % N;
         // ---- rotation + decomposition (split_digits through LDS) ----
-        __syncthreads();  // every pair written / the buffers read (and, at i = 0, the twiddle table)
+        __syncthreads();  // every pair written (and, at i = 0, the twiddle table)
         uint64_t pk[2][H][R];  // int16 digits: level L at j, j + M; level L-1 at j, j + M
 #pragma unroll
         for (int r = 0; r < 2; r++)
@@ -1941,11 +1839,15 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
             for (int h = 0; h < H; h++)
 #pragma unroll
                 for (int b = 0; b < R; b++) {
-                    uint64_t d0, d1;
-                    ct1(r, h, b, rem, full_odd, d0, d1);
+                    const int j = t + 512 * h + 1024 * b;
+                    const int jj0 = j - rem;  // in (-N, M)
+                    const acc_pair rot = (ONCHIP_TSKIP & 16) ? acc_pair{lo[r][h][b] * 3, hi[r][h][b]} : pairs[pslot(r, jj0 & (M - 1))];
+                    const bool swap = jj0 < 0 && jj0 >= -M;
+                    const uint64_t x0 = swap ? rot.y : rot.x, x1 = swap ? rot.x : rot.y;
+                    const bool neg0 = (jj0 < 0) != full_odd, neg1 = (jj0 + M < 0) != full_odd;
                     int32_t e0[2], e1[2];
-                    onchip_decompose<D32>(d0, beta, e0);
-                    onchip_decompose<D32>(d1, beta, e1);
+                    onchip_decompose<D32>((neg0 ? 0 - x0 : x0) - lo[r][h][b], beta, e0);
+                    onchip_decompose<D32>((neg1 ? 0 - x1 : x1) - hi[r][h][b], beta, e1);
                     pk[r][h][b] = ((uint64_t)((uint32_t)e0[0] & 0xffffu)) | ((uint64_t)((uint32_t)e1[0] & 0xffffu) << 16) |
                                   ((uint64_t)((uint32_t)e0[1] & 0xffffu) << 32) |
                                   ((uint64_t)((uint32_t)e1[1] & 0xffffu) << 48);
@@ -1965,9 +1867,8 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
             for (int h = 0; h < H; h++) top_loads_h(h);
         };
         if (ONCHIP_TPF) top_loads();
-        if constexpr (G == 0) __syncthreads();  // the pairs are read: the region becomes the wave buffers
-        const __amdgpu_buffer_rsrc_t rg =
-            make_rsrc(a.fbsk + (size_t)i * NSEL * ggsw_len + (size_t)wr * M + 1024 * q);
+        __syncthreads();  // the pairs are read: the region becomes the wave buffers
+        const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.fbsk + (size_t)i * ggsw_len + (size_t)wr * M + 1024 * q);
         cx o[16];
         auto level = [&](auto LIc) {
             constexpr int LI = decltype(LIc)::value;  // 0: level L, 1: level L-1
@@ -2009,19 +1910,12 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
             for (int s = 0; s < 16; s++) own[s * 64 + lane] = make_double2(v[s].re, v[s].im);
             // the first slots' GGSW operands are in flight during the barrier
             double2 pf[ONCHIP_PFS][2];
-            if constexpr (G == 0) {
 #pragma unroll
-                for (int s = 0; s < ONCHIP_PF; s++) onchip_ggsw<M, LI>(rg, 16u * lane, s, pf[s][0], pf[s][1]);
-            }
+            for (int s = 0; s < ONCHIP_PF; s++) onchip_ggsw<M, LI>(rg, 16u * lane, s, pf[s][0], pf[s][1]);
             if (ONCHIP_PAIRSYNC) ps();  // only the partner reads this spectrum
             else __syncthreads();
             // ---- MAC of this level, column wr ----
-            if constexpr (G == 0) {
-                onchip_mac<M, BUF, LI>(rg, 16u * lane, lds + (wave & ~1) * BUF + lane, o, pf);
-            } else {
-                const uint32_t fl = (uint32_t)q + (uint32_t)R * SubFft::freq_lane(lane);
-                onchip_mac_mb<N, BUF, LI, G>(rg, 16u * lane, lds + (wave & ~1) * BUF + lane, o, a.twist, deg, fl);
-            }
+            onchip_mac<M, BUF, LI>(rg, 16u * lane, lds + (wave & ~1) * BUF + lane, o, pf);
             __syncthreads();  // the partner has read this wave's spectrum
         };
         level(std::integral_constant<int, 0>{});
@@ -2053,24 +1947,13 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
                 if (!(ONCHIP_TSKIP & 8)) dftR_inv<R>(u);
 #pragma unroll
                 for (int b = 0; b < R; b++) {
-                    if constexpr (G > 0) {
-                        backward_convert(u[b], tv[h][b], lo[col][h][b], hi[col][h][b], k32);
-                    } else {
-                        backward_add(u[b], tv[h][b], lo[col][h][b], hi[col][h][b], k32);
-                        pairs[(2 * b + col) * BUF + a0] = acc_pair{lo[col][h][b], hi[col][h][b]};  // = slot read above
-                    }
+                    backward_add(u[b], tv[h][b], lo[col][h][b], hi[col][h][b], k32);
+                    pairs[(2 * b + col) * BUF + a0] = acc_pair{lo[col][h][b], hi[col][h][b]};  // = slot read above
                 }
             }
         }
     }
     // ---- sample extract at degree 0 (large_extract_kernel) from the pairs ----
-    if constexpr (G > 0) {  // the accumulator is only in registers
-        __syncthreads();
-#pragma unroll
-        for (int h = 0; h < H; h++)
-#pragma unroll
-            for (int b = 0; b < R; b++) pairs[(2 * b) * BUF + t + 512 * h] = acc_pair{lo[0][h][b], hi[0][h][b]};
-    }
     __syncthreads();
     uint64_t *out = a.lwe_out + (size_t)ct * ((size_t)K * N + 1);
     for (int e = t; e < N; e += Cfg::THREADS) {
@@ -2080,18 +1963,6 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
         out[e] = e == 0 ? x : 0 - x;
     }
     if (t == 0) out[N] = lo[1][0][0];  // row 1 position 0: the body
-}
-
-// TFHE_MI355_ONCHIP_MB=1: the multi-bit N = 8192 sets through the on-chip CMUX too (A/B; off by
-// default: one ciphertext per CU streams the group's 2^g GGSWs, 4 MiB at g = 3, from L2 once per
-// ciphertext instead of once per pair and sub-block slice -- 4169 vs 12044 KS+PBS/s at g = 3, 6973
-// vs 10120 at g = 2, bit-identical; profiles/r05_onchipmb_*.json)
-static bool onchip_mb_enabled() {
-    static const bool v = [] {
-        const char *e = std::getenv("TFHE_MI355_ONCHIP_MB");
-        return e && e[0] == '1';
-    }();
-    return v;
 }
 
 static bool onchip_enabled() {
@@ -2263,15 +2134,14 @@ template <int N, int K, int L, int G = 0>
 static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
     using S = Split<N>;
     if (a0.count == 0) return hipSuccess;
-    if constexpr (K == 1 && L == 2 && S::R == 4) {
-        if (onchip_enabled() && a0.count >= a0.onchip_min_count && (G == 0 || onchip_mb_enabled())) {
-            // the whole blind rotation on chip, no scratch
+    if constexpr (G == 0 && K == 1 && L == 2 && S::R == 4) {
+        if (onchip_enabled() && a0.count >= a0.onchip_min_count) {  // the whole blind rotation on chip, no scratch
             TimedLaunch tl(a0.timer, "onchip_cmux_kernel", s);
             if (a0.base_log * 2 <= 30)  // 32-bit digit extraction (every shortint set at this shape)
-                hipLaunchKernelGGL((onchip_cmux_kernel<N, true, G>), dim3((unsigned)a0.count),
-                                   dim3(OnchipCfg<N>::THREADS), OnchipCfg<N>::LDS, s, a0);
+                hipLaunchKernelGGL((onchip_cmux_kernel<N, true>), dim3((unsigned)a0.count), dim3(OnchipCfg<N>::THREADS),
+                                   OnchipCfg<N>::LDS, s, a0);
             else
-                hipLaunchKernelGGL((onchip_cmux_kernel<N, false, G>), dim3((unsigned)a0.count),
+                hipLaunchKernelGGL((onchip_cmux_kernel<N, false>), dim3((unsigned)a0.count),
                                    dim3(OnchipCfg<N>::THREADS), OnchipCfg<N>::LDS, s, a0);
             return hipGetLastError();
         }
