@@ -160,14 +160,17 @@ def test_onchip_and_split_cmux_agree(orc):
     cts[0, :-1] = 0                                   # every a~ = 0
     cts[1, :-1] = np.uint64(1 << 63)                  # a~ = N
     cts[2, -1] = np.uint64((1 << 64) - 1)             # b~ = 2N
-    acc = orc.fill_accumulator(p.polynomial_size, 1, 8, 8, lambda x: (x * 7 + 2) % 64)
-    whole = eng.programmable_bootstrap(cts, acc)
-    halves = np.concatenate([eng.programmable_bootstrap(cts[:65], acc), eng.programmable_bootstrap(cts[65:], acc)])
+    fs = [lambda x: (x * 7 + 2) % 64, lambda x: (x + 33) % 64]
+    luts = np.stack([orc.fill_accumulator(p.polynomial_size, 1, 8, 8, f) for f in fs])
+    idx = (np.arange(130) % 3 == 1).astype(np.uint32)  # per-ciphertext LUTs
+    whole = eng.programmable_bootstrap(cts, luts, lut_indexes=idx)
+    halves = np.concatenate([eng.programmable_bootstrap(cts[:65], luts, lut_indexes=idx[:65]),
+                             eng.programmable_bootstrap(cts[65:], luts, lut_indexes=idx[65:])])
     assert np.array_equal(whole, halves), f"{np.count_nonzero(np.any(whole != halves, axis=1))} rows differ"
     sample = np.array([0, 1, 2, 64, 65, 129])
-    assert np.array_equal(whole[sample], fbsk.pbs(cts[sample], acc, threads=6))
+    assert np.array_equal(whole[sample], fbsk.pbs(cts[sample], luts, lut_idx=idx[sample], threads=6))
     dec = decode(orc.lwe_decrypt(glwe_sk, whole[3:]), p.delta) % 64
-    assert np.array_equal(dec, (msgs[3:] * 7 + 2) % 64)
+    assert np.array_equal(dec, [fs[i](m) for i, m in zip(idx[3:], msgs[3:])])
 
 
 @pytest.mark.timeout(900)
