@@ -146,13 +146,16 @@ def test_split_pbs_chunks_ragged(orc):
     assert np.array_equal(got[sample], fbsk.pbs(cts[sample], acc, threads=5))
 
 
-def test_onchip_and_split_cmux_agree(orc):
-    """N = 8192, L = 2: a 130-ciphertext call runs the on-chip CMUX (onchip_cmux_kernel, >= 96 rows on
-    256 CUs: capi.cpp onchip_min), the same ciphertexts in calls of 65 the digits-fed split CMUX;
-    every row identical, a sample bit-exact against the oracle, edge masks included."""
-    from tfhe_mi355.parameters import PARAM_MESSAGE_3_CARRY_3_KS_PBS
+@pytest.mark.parametrize("name", ["PARAM_MESSAGE_3_CARRY_3_KS_PBS",    # L = 2, base 2^15
+                                  "PARAM_MESSAGE_6_CARRY_0_KS_PBS"])   # L = 1, base 2^22
+def test_onchip_and_split_cmux_agree(orc, name):
+    """N = 8192, L = 2 and L = 1: a 130-ciphertext call runs the on-chip CMUX (onchip_cmux_kernel, >= 96
+    rows on 256 CUs: capi.cpp onchip_min), the same ciphertexts in calls of 65 the split CMUX (digits-fed
+    at L = 2, three launches at L = 1); every row identical, a sample bit-exact against the oracle, edge
+    masks and per-ciphertext LUTs included."""
+    from tfhe_mi355.parameters import SHORTINT_ALL
 
-    p = PARAM_MESSAGE_3_CARRY_3_KS_PBS.with_(lwe_dimension=6)
+    p = SHORTINT_ALL[name].with_(lwe_dimension=6)
     lwe_sk, glwe_sk, bsk, fbsk = _keys(orc, p, 77)
     eng = _engine(p, bsk)
     msgs = np.random.default_rng(5).integers(0, 64, 130)

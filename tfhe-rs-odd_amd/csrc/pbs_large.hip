@@ -1693,13 +1693,13 @@ struct OnchipCfg {
 #endif
 constexpr int ONCHIP_PFS = ONCHIP_PF > 0 ? ONCHIP_PF : 1;
 // GGSW operands (rows 0 and 1 of level L - LI, column of rg) of MAC slot s
-template <int M, int LI>
+template <int M, int LI, int L = 2>
 __device__ __forceinline__ void onchip_ggsw(__amdgpu_buffer_rsrc_t rg, uint32_t gvo, int s, double2 &g0, double2 &g1) {
-    constexpr int P0 = (1 - LI) * 2;  // polynomial (lvl - 1)(k + 1) of row 0, lvl = L - LI
+    constexpr int P0 = (L - 1 - LI) * 2;  // polynomial (lvl - 1)(k + 1) of row 0, lvl = L - LI
     g0 = buffer_ld_d2(rg, gvo, 16u * (uint32_t)(P0 * 2 * M + s * 64));
     g1 = buffer_ld_d2(rg, gvo, 16u * (uint32_t)((P0 + 1) * 2 * M + s * 64));
 }
-template <int M, int BUF, int LI>
+template <int M, int BUF, int LI, int L = 2>
 __device__ __forceinline__ void onchip_mac(__amdgpu_buffer_rsrc_t rg, uint32_t gvo, const double2 *F, cx (&o)[16],
                                            const double2 (&pf)[ONCHIP_PFS][2]) {
 #pragma unroll
@@ -1711,7 +1711,7 @@ __device__ __forceinline__ void onchip_mac(__amdgpu_buffer_rsrc_t rg, uint32_t g
             g0 = pf[s < ONCHIP_PFS ? s : 0][0];
             g1 = pf[s < ONCHIP_PFS ? s : 0][1];
         } else {
-            onchip_ggsw<M, LI>(rg, gvo, s, g0, g1);
+            onchip_ggsw<M, LI, L>(rg, gvo, s, g0, g1);
         }
         if (ONCHIP_TSKIP & 1) {
             g0 = f1;
@@ -1745,6 +1745,19 @@ __device__ __forceinline__ void onchip_decompose(uint64_t x, int beta, int32_t (
     }
 }
 
+// L = 1: the one signed digit (decompose64<1>; 32-bit when base_log <= 30)
+template <bool D32>
+__device__ __forceinline__ int32_t onchip_decompose1(uint64_t x, int beta) {
+    if constexpr (D32) {
+        uint32_t st = decomp_state32<1>(x, beta);
+        return decomp_digit32(st, beta, (1u << beta) - 1);
+    } else {
+        int32_t d[1];
+        decompose64<1>(x, beta, d);
+        return d[0];
+    }
+}
+
 // a zero the compiler cannot see through: table pointers offset by it (the twist, the top-stage
 // twiddles, the CMUX's GGSW) are not provably loop-invariant, so their loads stay where they are
 // used instead of being hoisted out of the CMUX loop into registers held for good (an opaque
@@ -1755,11 +1768,12 @@ __device__ __forceinline__ int opaque_zero() {
     return z;
 }
 
-template <int N, bool D32>
+template <int N, bool D32, int L = 2>
 __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
     using S = Split<N>;
     using Cfg = OnchipCfg<N>;
-    constexpr int K = 1, L = 2, M = S::M, R = S::R, H = Cfg::H, BUF = Cfg::BUF;
+    static_assert(L == 1 || L == 2, "one or two decomposition levels");
+    constexpr int K = 1, M = S::M, R = S::R, H = Cfg::H, BUF = Cfg::BUF;
     constexpr size_t ggsw_len = (size_t)L * (K + 1) * (K + 1) * M;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double2 *lds = reinterpret_cast<double2 *>(smem);
@@ -1845,12 +1859,18 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
                     const bool swap = jj0 < 0 && jj0 >= -M;
                     const uint64_t x0 = swap ? rot.y : rot.x, x1 = swap ? rot.x : rot.y;
                     const bool neg0 = (jj0 < 0) != full_odd, neg1 = (jj0 + M < 0) != full_odd;
-                    int32_t e0[2], e1[2];
-                    onchip_decompose<D32>((neg0 ? 0 - x0 : x0) - lo[r][h][b], beta, e0);
-                    onchip_decompose<D32>((neg1 ? 0 - x1 : x1) - hi[r][h][b], beta, e1);
-                    pk[r][h][b] = ((uint64_t)((uint32_t)e0[0] & 0xffffu)) | ((uint64_t)((uint32_t)e1[0] & 0xffffu) << 16) |
-                                  ((uint64_t)((uint32_t)e0[1] & 0xffffu) << 32) |
-                                  ((uint64_t)((uint32_t)e1[1] & 0xffffu) << 48);
+                    if constexpr (L == 2) {
+                        int32_t e0[2], e1[2];
+                        onchip_decompose<D32>((neg0 ? 0 - x0 : x0) - lo[r][h][b], beta, e0);
+                        onchip_decompose<D32>((neg1 ? 0 - x1 : x1) - hi[r][h][b], beta, e1);
+                        pk[r][h][b] = ((uint64_t)((uint32_t)e0[0] & 0xffffu)) | ((uint64_t)((uint32_t)e1[0] & 0xffffu) << 16) |
+                                      ((uint64_t)((uint32_t)e0[1] & 0xffffu) << 32) |
+                                      ((uint64_t)((uint32_t)e1[1] & 0xffffu) << 48);
+                    } else {  // one level: |digit| <= 2^(beta - 1) (2^21 at base 2^22) -- two int32 fields
+                        const int32_t e0 = onchip_decompose1<D32>((neg0 ? 0 - x0 : x0) - lo[r][h][b], beta);
+                        const int32_t e1 = onchip_decompose1<D32>((neg1 ? 0 - x1 : x1) - hi[r][h][b], beta);
+                        pk[r][h][b] = (uint64_t)(uint32_t)e0 | ((uint64_t)(uint32_t)e1 << 32);
+                    }
                 }
         // the top stage's twist and twiddles (tv[h][b] = twist[a + 1024 b], wq[h][c] = W[a c] of
         // butterfly a = t + 512 h): issued before the barrier that precedes their use
@@ -1883,8 +1903,15 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
                     cx u[R];
 #pragma unroll
                     for (int b = 0; b < R; b++) {
-                        const uint64_t w = pk[r][h][b] >> (32 * LI);
-                        const int32_t d0 = (int32_t)(int16_t)(w & 0xffffu), d1 = (int32_t)(int16_t)((w >> 16) & 0xffffu);
+                        int32_t d0, d1;
+                        if constexpr (L == 2) {
+                            const uint64_t w = pk[r][h][b] >> (32 * LI);
+                            d0 = (int32_t)(int16_t)(w & 0xffffu);
+                            d1 = (int32_t)(int16_t)((w >> 16) & 0xffffu);
+                        } else {
+                            d0 = (int32_t)(uint32_t)pk[r][h][b];
+                            d1 = (int32_t)(uint32_t)(pk[r][h][b] >> 32);
+                        }
                         u[b] = cmulw(cx{(double)d0, (double)d1}, tv[h][b].re, tv[h][b].im);
                     }
                     if (!(ONCHIP_TSKIP & 8)) dftR_fwd<R>(u);
@@ -1911,15 +1938,15 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
             // the first slots' GGSW operands are in flight during the barrier
             double2 pf[ONCHIP_PFS][2];
 #pragma unroll
-            for (int s = 0; s < ONCHIP_PF; s++) onchip_ggsw<M, LI>(rg, 16u * lane, s, pf[s][0], pf[s][1]);
+            for (int s = 0; s < ONCHIP_PF; s++) onchip_ggsw<M, LI, L>(rg, 16u * lane, s, pf[s][0], pf[s][1]);
             if (ONCHIP_PAIRSYNC) ps();  // only the partner reads this spectrum
             else __syncthreads();
             // ---- MAC of this level, column wr ----
-            onchip_mac<M, BUF, LI>(rg, 16u * lane, lds + (wave & ~1) * BUF + lane, o, pf);
+            onchip_mac<M, BUF, LI, L>(rg, 16u * lane, lds + (wave & ~1) * BUF + lane, o, pf);
             __syncthreads();  // the partner has read this wave's spectrum
         };
         level(std::integral_constant<int, 0>{});
-        level(std::integral_constant<int, 1>{});
+        if constexpr (L == 2) level(std::integral_constant<int, 1>{});
         // ---- inverse sub-FFT of (q, column wr) -> its buffer, natural layout ----
         if (!(ONCHIP_TSKIP & 4)) SubFft::inverse(o, xb, tw, lane, wsync);
         wsync();
@@ -2134,15 +2161,14 @@ template <int N, int K, int L, int G = 0>
 static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
     using S = Split<N>;
     if (a0.count == 0) return hipSuccess;
-    if constexpr (G == 0 && K == 1 && L == 2 && S::R == 4) {
+    if constexpr (G == 0 && K == 1 && (L == 2 || L == 1) && S::R == 4) {
         if (onchip_enabled() && a0.count >= a0.onchip_min_count) {  // the whole blind rotation on chip, no scratch
             TimedLaunch tl(a0.timer, "onchip_cmux_kernel", s);
-            if (a0.base_log * 2 <= 30)  // 32-bit digit extraction (every shortint set at this shape)
-                hipLaunchKernelGGL((onchip_cmux_kernel<N, true>), dim3((unsigned)a0.count), dim3(OnchipCfg<N>::THREADS),
-                                   OnchipCfg<N>::LDS, s, a0);
+            const dim3 grid((unsigned)a0.count), block(OnchipCfg<N>::THREADS);
+            if (a0.base_log * L <= 30)  // 32-bit digit extraction (every shortint set at these shapes)
+                hipLaunchKernelGGL((onchip_cmux_kernel<N, true, L>), grid, block, OnchipCfg<N>::LDS, s, a0);
             else
-                hipLaunchKernelGGL((onchip_cmux_kernel<N, false>), dim3((unsigned)a0.count),
-                                   dim3(OnchipCfg<N>::THREADS), OnchipCfg<N>::LDS, s, a0);
+                hipLaunchKernelGGL((onchip_cmux_kernel<N, false, L>), grid, block, OnchipCfg<N>::LDS, s, a0);
             return hipGetLastError();
         }
     }
