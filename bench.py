@@ -117,7 +117,7 @@ def _split_params():
                     (f"onchip_cmux_kernel<{p.polynomial_size},"
                      f"{'true' if p.pbs_level * p.pbs_base_log <= 30 else 'false'},{p.pbs_level}> "
                      "(the whole blind rotation per workgroup, ks_mfma_kernel)"
-                     if p.pbs_level <= 2 and p.polynomial_size == 8192 and os.environ.get("TFHE_MI355_ONCHIP", "1") != "0"
+                     if p.pbs_level <= 2 and p.polynomial_size in (4096, 8192) and os.environ.get("TFHE_MI355_ONCHIP", "1") != "0"
                      else f"large_dsub_kernel<{p.polynomial_size}> (+ split_digits/large_top_inv per CMUX, ks_mfma_kernel)"
                      if p.pbs_level == 2 and p.polynomial_size <= 8192 else
                      f"large_sub_kernel<{p.polynomial_size},1,{p.pbs_level}> (+ large_top_fwd/top_inv per CMUX, "

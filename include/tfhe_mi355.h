@@ -38,10 +38,11 @@
  *     of at most three (classic) / two (multi-bit g = 2, 3) passes of one ciphertext per CU (768 /
  *     512 rows on 256 CUs: the measured crossovers against the throughput kernels) run the
  *     one-ciphertext-per-CU latency kernels (same outputs; TFHE_MI355_LATENCY_MAX = rows
- *     overrides, 0 = never).  At N = 8192, k = 1, L = 2 (classic), batches of at least 3/8 of the
- *     CU count (96 rows on 256 CUs) run the on-chip CMUX (the whole blind rotation in one
- *     workgroup per ciphertext, no scratch used), smaller ones the split CMUX (same outputs;
- *     TFHE_MI355_ONCHIP_MIN = rows overrides, TFHE_MI355_ONCHIP=0 = never).
+ *     overrides, 0 = never).  At N = 8192 / 4096, k = 1, L = 1 or 2 (classic), batches of at least
+ *     3/8 / 5/8 of the CU count (96 / 160 rows on 256 CUs) run the on-chip CMUX (the whole blind
+ *     rotation in one workgroup per ciphertext or pair of ciphertexts, no scratch used), smaller
+ *     ones the split CMUX (same outputs; TFHE_MI355_ONCHIP_MIN = rows overrides,
+ *     TFHE_MI355_ONCHIP=0 = never).
  *     The _async calls hold no per-context mutable state: every device scratch buffer they
  *     need comes from the caller (d_scratch, sized by the matching *_scratch query; a call
  *     given less than its query fails with an error, and only a query returning 0 allows

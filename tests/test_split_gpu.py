@@ -146,33 +146,37 @@ def test_split_pbs_chunks_ragged(orc):
     assert np.array_equal(got[sample], fbsk.pbs(cts[sample], acc, threads=5))
 
 
-@pytest.mark.parametrize("name", ["PARAM_MESSAGE_3_CARRY_3_KS_PBS",    # L = 2, base 2^15
-                                  "PARAM_MESSAGE_6_CARRY_0_KS_PBS"])   # L = 1, base 2^22
+@pytest.mark.parametrize("name", ["PARAM_MESSAGE_3_CARRY_3_KS_PBS",    # N = 8192, L = 2, base 2^15
+                                  "PARAM_MESSAGE_6_CARRY_0_KS_PBS",    # N = 8192, L = 1, base 2^22
+                                  "PARAM_MESSAGE_1_CARRY_4_KS_PBS",    # N = 4096, L = 2 (two ciphertexts per workgroup)
+                                  "PARAM_MESSAGE_2_CARRY_3_KS_PBS"])   # N = 4096, L = 1
 def test_onchip_and_split_cmux_agree(orc, name):
-    """N = 8192, L = 2 and L = 1: a 130-ciphertext call runs the on-chip CMUX (onchip_cmux_kernel, >= 96
-    rows on 256 CUs: capi.cpp onchip_min), the same ciphertexts in calls of 65 the split CMUX (digits-fed
-    at L = 2, three launches at L = 1); every row identical, a sample bit-exact against the oracle, edge
-    masks and per-ciphertext LUTs included."""
+    """N = 8192 and 4096, L = 2 and 1: a 131-ciphertext call runs the on-chip CMUX (onchip_cmux_kernel,
+    >= 96 rows on 256 CUs: capi.cpp onchip_min; at N = 4096 two ciphertexts per workgroup, the odd count
+    leaving a padding slot), the same ciphertexts in calls of 65 / 66 the split CMUX (digits-fed at L = 2,
+    three launches at L = 1); every row identical, a sample bit-exact against the oracle, edge masks and
+    per-ciphertext LUTs included."""
     from tfhe_mi355.parameters import SHORTINT_ALL
 
     p = SHORTINT_ALL[name].with_(lwe_dimension=6)
+    space = p.message_modulus * p.carry_modulus
     lwe_sk, glwe_sk, bsk, fbsk = _keys(orc, p, 77)
     eng = _engine(p, bsk)
-    msgs = np.random.default_rng(5).integers(0, 64, 130)
+    msgs = np.random.default_rng(5).integers(0, space, 131)
     cts = orc.lwe_encrypt(78, lwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta), p.lwe_modular_std_dev)
     cts[0, :-1] = 0                                   # every a~ = 0
     cts[1, :-1] = np.uint64(1 << 63)                  # a~ = N
     cts[2, -1] = np.uint64((1 << 64) - 1)             # b~ = 2N
-    fs = [lambda x: (x * 7 + 2) % 64, lambda x: (x + 33) % 64]
-    luts = np.stack([orc.fill_accumulator(p.polynomial_size, 1, 8, 8, f) for f in fs])
-    idx = (np.arange(130) % 3 == 1).astype(np.uint32)  # per-ciphertext LUTs
+    fs = [lambda x: (x * 7 + 2) % space, lambda x: (x + space // 2 + 1) % space]
+    luts = np.stack([orc.fill_accumulator(p.polynomial_size, 1, p.message_modulus, p.carry_modulus, f) for f in fs])
+    idx = (np.arange(131) % 3 == 1).astype(np.uint32)  # per-ciphertext LUTs
     whole = eng.programmable_bootstrap(cts, luts, lut_indexes=idx)
     halves = np.concatenate([eng.programmable_bootstrap(cts[:65], luts, lut_indexes=idx[:65]),
                              eng.programmable_bootstrap(cts[65:], luts, lut_indexes=idx[65:])])
     assert np.array_equal(whole, halves), f"{np.count_nonzero(np.any(whole != halves, axis=1))} rows differ"
-    sample = np.array([0, 1, 2, 64, 65, 129])
+    sample = np.array([0, 1, 2, 64, 65, 130])
     assert np.array_equal(whole[sample], fbsk.pbs(cts[sample], luts, lut_idx=idx[sample], threads=6))
-    dec = decode(orc.lwe_decrypt(glwe_sk, whole[3:]), p.delta) % 64
+    dec = decode(orc.lwe_decrypt(glwe_sk, whole[3:]), p.delta) % space
     assert np.array_equal(dec, [fs[i](m) for i, m in zip(idx[3:], msgs[3:])])
 
 

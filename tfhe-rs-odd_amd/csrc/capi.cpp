@@ -368,17 +368,21 @@ size_t pbs_scratch_bytes(const TfheMi355Context *c, size_t count) {
     return per_ct * std::min(count, large_chunk(c));
 }
 
-// The on-chip N = 8192 CMUX (one ciphertext per CU for the whole blind rotation) against the
-// digits-fed split CMUX (a ciphertext's sub-blocks over several CUs): at 3_3 the split path takes
-// 16.3 / 18.8 / 23.2 / 25.4 ms for 1 / 64 / 96 / 128 ciphertexts, the on-chip one 22.9-25.1 ms
-// for any count up to one per CU (profiles/r05_sweep33_onchip{0,1}.json), so the on-chip kernel
-// from 3/8 of the CU count (96 on MI355X) on.  TFHE_MI355_ONCHIP_MIN overrides.
+// The on-chip CMUX (the whole blind rotation in one workgroup: one ciphertext per CU at N = 8192,
+// two at N = 4096) against the split CMUX (a ciphertext's sub-blocks over several CUs, in several
+// launches per CMUX): at 3_3 the split path takes 16.3 / 18.8 / 23.2 / 25.4 ms for 1 / 64 / 96 / 128
+// ciphertexts, the on-chip one 22.9-25.1 ms for any count up to one per CU
+// (profiles/r05_sweep33_onchip{0,1}.json); at 1_4 (N = 4096) split 11.0 / 13.3 / 14.0 / 19.3 ms for
+// 1 / 96 / 128 / 192, on-chip 18.6-18.9 ms up to two per CU (r05_sweep14_onchip{0,1}.json).  So the
+// on-chip kernel from 3/8 (N = 8192) / 5/8 (N = 4096) of the CU count on: 96 / 160 on MI355X.
+// TFHE_MI355_ONCHIP_MIN overrides.
 size_t onchip_min(const TfheMi355Context *c) {
     static const long env = [] {
         const char *e = std::getenv("TFHE_MI355_ONCHIP_MIN");
         return e && *e ? std::strtol(e, nullptr, 10) : -1L;
     }();
-    return env >= 0 ? (size_t)env : (size_t)c->cus * 3 / 8;
+    if (env >= 0) return (size_t)env;
+    return c->N() == 4096 ? (size_t)c->cus * 5 / 8 : (size_t)c->cus * 3 / 8;
 }
 
 // Batches of at most this many ciphertexts run the latency kernels (one ciphertext per CU) at the

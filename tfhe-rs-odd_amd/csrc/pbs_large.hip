@@ -1670,13 +1670,15 @@ template <int N>
 struct OnchipCfg {
     static constexpr int M = N / 2, R = M / 1024;
     static constexpr int THREADS = 512;
-    static constexpr int H = 1024 / THREADS;  // top-stage butterflies per thread
+    static constexpr int CPW = 4 / R;          // ciphertexts per workgroup (N = 4096: two, 4 waves each)
+    static constexpr int TPC = THREADS / CPW;  // threads per ciphertext
+    static constexpr int H = 1024 / TPC;       // top-stage butterflies per thread
     static constexpr int BUF = SubFft::XL;    // double2 per wave buffer
     static constexpr int S1 = 8 * BUF;        // twiddle table offset (double2 units)
     static constexpr int FLAGS = S1 + SubFft::Lds::s1_len;  // pair-sync flags (double2 offset), one word per wave
     static constexpr size_t LDS = sizeof(double2) * FLAGS + 4 * 8;
-    static_assert(R == 4, "8 waves = 4 sub-blocks x 2 rows");
-    static_assert(8 * BUF * sizeof(double2) == 2 * M * sizeof(acc_pair), "the rotation's pairs fill the wave buffers");
+    static_assert(R == 4 || R == 2, "8 waves = CPW ciphertexts x R sub-blocks x 2 rows");
+    static_assert(8 * BUF * sizeof(double2) == CPW * 2 * M * sizeof(acc_pair), "the rotation's pairs fill the wave buffers");
 };
 
 // MAC of level L - LI for one sub-block: both rows' spectra from their buffers F (row r at
@@ -1773,15 +1775,20 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
     using S = Split<N>;
     using Cfg = OnchipCfg<N>;
     static_assert(L == 1 || L == 2, "one or two decomposition levels");
-    constexpr int K = 1, M = S::M, R = S::R, H = Cfg::H, BUF = Cfg::BUF;
+    constexpr int K = 1, M = S::M, R = S::R, H = Cfg::H, BUF = Cfg::BUF, CPW = Cfg::CPW, TPC = Cfg::TPC;
     constexpr size_t ggsw_len = (size_t)L * (K + 1) * (K + 1) * M;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double2 *lds = reinterpret_cast<double2 *>(smem);
     acc_pair *pairs = reinterpret_cast<acc_pair *>(smem);  // rotation view: [row][M] pairs
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int q = wave >> 1, wr = wave & 1;  // sub-block; row (forward) = column (MAC, inverse)
-    const int ct = blockIdx.x;
+    // wave = 2 R c + 2 q + wr: ciphertext c of the workgroup, sub-block q, row (forward) = column
+    // (MAC, inverse) wr; thread t works for ciphertext ctl = t / TPC as thread tc = t mod TPC
+    const int q = CPW == 1 ? wave >> 1 : (wave >> 1) & (R - 1), wr = wave & 1;
+    const int ctl = CPW == 1 ? 0 : t / TPC, tc = CPW == 1 ? t : t % TPC;
+    const int cb = 2 * R * ctl;  // this thread's ciphertext's first wave buffer
+    const int ct_raw = CPW == 1 ? (int)blockIdx.x : (int)blockIdx.x * CPW + ctl;
+    const int ct = CPW == 1 ? ct_raw : min(ct_raw, a.count - 1);  // a padding slot repeats the last ciphertext
     double2 *s1 = lds + Cfg::S1;
     // sub-block stage twiddles W_1024[lane c] = W_M[R lane c]  (oracle dif_rec tstride R)
     for (int e = t; e < SubFft::Lds::s1_len; e += Cfg::THREADS) s1[e] = a.W[R * (e & 63) * ((e >> 6) + 1)];
@@ -1795,7 +1802,7 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
     const uint64_t *in = a.lwe_in + (size_t)ct * (a.n + 1);
     // twist and top-stage twiddles through buffer loads: one VGPR offset, the rest in SGPRs
     const __amdgpu_buffer_rsrc_t rtw = make_rsrc(a.twist), rwt = make_rsrc(a.wtop);
-    const uint32_t tvo = 16u * t;
+    const uint32_t tvo = 16u * tc;
     auto ld_cx = [](__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
         const double2 x = buffer_ld_d2(r, vo, so);
         return cx{x.x, x.y};
@@ -1820,7 +1827,7 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
             for (int h = 0; h < H; h++)
 #pragma unroll
                 for (int b = 0; b < R; b++) {
-                    const int j = t + 512 * h + 1024 * b;
+                    const int j = tc + TPC * h + 1024 * b;
                     lo[r][h][b] = init(r, j);
                     hi[r][h][b] = init(r, j + M);
                 }
@@ -1830,13 +1837,13 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
     // accumulator pair (row r, j) <-> LDS slot (2 (j >> 10) + r) BUF + (j & 1023): the slots thread t
     // owns, (2 b + r) BUF + t + 512 h, are exactly the top-stage / top-inverse slots of its butterflies,
     // so the top inverse writes the updated pairs in place (no barrier between its reads and them)
-    auto pslot = [](int r, int j) { return (2 * (j >> 10) + r) * BUF + (j & 1023); };
+    auto pslot = [&](int r, int j) { return (cb + 2 * (j >> 10) + r) * BUF + (j & 1023); };
 #pragma unroll
     for (int r = 0; r < 2; r++)
 #pragma unroll
         for (int h = 0; h < H; h++)
 #pragma unroll
-            for (int b = 0; b < R; b++) pairs[(2 * b + r) * BUF + t + 512 * h] = acc_pair{lo[r][h][b], hi[r][h][b]};
+            for (int b = 0; b < R; b++) pairs[(cb + 2 * b + r) * BUF + tc + TPC * h] = acc_pair{lo[r][h][b], hi[r][h][b]};
 
     uint64_t a_next = in[0];
     for (int i = 0; i < a.n; i++) {
@@ -1853,7 +1860,7 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
             for (int h = 0; h < H; h++)
 #pragma unroll
                 for (int b = 0; b < R; b++) {
-                    const int j = t + 512 * h + 1024 * b;
+                    const int j = tc + TPC * h + 1024 * b;
                     const int jj0 = j - rem;  // in (-N, M)
                     const acc_pair rot = (ONCHIP_TSKIP & 16) ? acc_pair{lo[r][h][b] * 3, hi[r][h][b]} : pairs[pslot(r, jj0 & (M - 1))];
                     const bool swap = jj0 < 0 && jj0 >= -M;
@@ -1878,9 +1885,9 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
         auto top_loads_h = [&](int h) {
             const uint32_t z = (uint32_t)opaque_zero();
 #pragma unroll
-            for (int b = 0; b < R; b++) tv[h][b] = ld_cx(rtw, tvo, z + 16u * (512 * h + 1024 * b));
+            for (int b = 0; b < R; b++) tv[h][b] = ld_cx(rtw, tvo, z + 16u * (TPC * h + 1024 * b));
 #pragma unroll
-            for (int c = 1; c < R; c++) wq[h][c] = ld_cx(rwt, tvo, z + 16u * ((c - 1) * 1024 + 512 * h));
+            for (int c = 1; c < R; c++) wq[h][c] = ld_cx(rwt, tvo, z + 16u * ((c - 1) * 1024 + TPC * h));
         };
         auto top_loads = [&]() {
 #pragma unroll
@@ -1896,7 +1903,7 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
             // (level L-1: per butterfly half, where they are used -- the MAC outputs are live)
 #pragma unroll
             for (int h = 0; h < H; h++) {
-                const int a0 = t + 512 * h;
+                const int a0 = tc + TPC * h;
                 if (!ONCHIP_TPF || LI == 1) top_loads_h(h);
 #pragma unroll
                 for (int r = 0; r < 2; r++) {
@@ -1915,11 +1922,11 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
                         u[b] = cmulw(cx{(double)d0, (double)d1}, tv[h][b].re, tv[h][b].im);
                     }
                     if (!(ONCHIP_TSKIP & 8)) dftR_fwd<R>(u);
-                    lds[r * BUF + a0] = make_double2(u[0].re, u[0].im);
+                    lds[(cb + r) * BUF + a0] = make_double2(u[0].re, u[0].im);
 #pragma unroll
                     for (int c = 1; c < R; c++) {
                         const cx y = cmulw(u[c], wq[h][c].re, wq[h][c].im);
-                        lds[(2 * c + r) * BUF + a0] = make_double2(y.re, y.im);
+                        lds[(cb + 2 * c + r) * BUF + a0] = make_double2(y.re, y.im);
                     }
                 }
             }
@@ -1958,24 +1965,24 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
         if (!ONCHIP_TPF) top_loads();
 #pragma unroll
         for (int h = 0; h < H; h++) {
-            const int a0 = t + 512 * h;
+            const int a0 = tc + TPC * h;
 #pragma unroll
             for (int col = 0; col < 2; col++) {
                 cx u[R];
                 {
-                    const double2 x = lds[col * BUF + a0];
+                    const double2 x = lds[(cb + col) * BUF + a0];
                     u[0] = cx{x.x, x.y};
                 }
 #pragma unroll
                 for (int c = 1; c < R; c++) {
-                    const double2 x = lds[(2 * c + col) * BUF + a0];
+                    const double2 x = lds[(cb + 2 * c + col) * BUF + a0];
                     u[c] = cmulw(cx{x.x, x.y}, wq[h][c].re, -wq[h][c].im);
                 }
                 if (!(ONCHIP_TSKIP & 8)) dftR_inv<R>(u);
 #pragma unroll
                 for (int b = 0; b < R; b++) {
                     backward_add(u[b], tv[h][b], lo[col][h][b], hi[col][h][b], k32);
-                    pairs[(2 * b + col) * BUF + a0] = acc_pair{lo[col][h][b], hi[col][h][b]};  // = slot read above
+                    pairs[(cb + 2 * b + col) * BUF + a0] = acc_pair{lo[col][h][b], hi[col][h][b]};  // = slot read above
                 }
             }
         }
@@ -1983,13 +1990,14 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
     // ---- sample extract at degree 0 (large_extract_kernel) from the pairs ----
     __syncthreads();
     uint64_t *out = a.lwe_out + (size_t)ct * ((size_t)K * N + 1);
-    for (int e = t; e < N; e += Cfg::THREADS) {
+    if (CPW > 1 && ct_raw >= a.count) return;  // padding slot: nothing to store (no barrier follows)
+    for (int e = tc; e < N; e += TPC) {
         const int p = e == 0 ? 0 : N - e;
         const acc_pair pr = pairs[pslot(0, p & (M - 1))];
         const uint64_t x = p >= M ? pr.y : pr.x;
         out[e] = e == 0 ? x : 0 - x;
     }
-    if (t == 0) out[N] = lo[1][0][0];  // row 1 position 0: the body
+    if (tc == 0) out[N] = lo[1][0][0];  // row 1 position 0: the body
 }
 
 static bool onchip_enabled() {
@@ -2161,10 +2169,10 @@ template <int N, int K, int L, int G = 0>
 static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
     using S = Split<N>;
     if (a0.count == 0) return hipSuccess;
-    if constexpr (G == 0 && K == 1 && (L == 2 || L == 1) && S::R == 4) {
+    if constexpr (G == 0 && K == 1 && (L == 2 || L == 1) && (S::R == 4 || S::R == 2)) {
         if (onchip_enabled() && a0.count >= a0.onchip_min_count) {  // the whole blind rotation on chip, no scratch
             TimedLaunch tl(a0.timer, "onchip_cmux_kernel", s);
-            const dim3 grid((unsigned)a0.count), block(OnchipCfg<N>::THREADS);
+            const dim3 grid((unsigned)((a0.count + OnchipCfg<N>::CPW - 1) / OnchipCfg<N>::CPW)), block(OnchipCfg<N>::THREADS);
             if (a0.base_log * L <= 30)  // 32-bit digit extraction (every shortint set at these shapes)
                 hipLaunchKernelGGL((onchip_cmux_kernel<N, true, L>), grid, block, OnchipCfg<N>::LDS, s, a0);
             else
