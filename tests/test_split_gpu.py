@@ -151,30 +151,32 @@ def test_split_pbs_chunks_ragged(orc):
                                   "PARAM_MESSAGE_1_CARRY_4_KS_PBS",    # N = 4096, L = 2 (two ciphertexts per workgroup)
                                   "PARAM_MESSAGE_2_CARRY_3_KS_PBS"])   # N = 4096, L = 1
 def test_onchip_and_split_cmux_agree(orc, name):
-    """N = 8192 and 4096, L = 2 and 1: a 131-ciphertext call runs the on-chip CMUX (onchip_cmux_kernel,
-    >= 96 rows on 256 CUs: capi.cpp onchip_min; at N = 4096 two ciphertexts per workgroup, the odd count
-    leaving a padding slot), the same ciphertexts in calls of 65 / 66 the split CMUX (digits-fed at L = 2,
-    three launches at L = 1); every row identical, a sample bit-exact against the oracle, edge masks and
-    per-ciphertext LUTs included."""
+    """N = 8192 and 4096, L = 2 and 1: one call of C ciphertexts runs the on-chip CMUX (onchip_cmux_kernel;
+    capi.cpp onchip_min: >= 96 rows at N = 8192, >= 160 at N = 4096 on 256 CUs; at N = 4096 two
+    ciphertexts per workgroup, the odd count leaving a padding slot), the same ciphertexts in two calls
+    below the threshold the split CMUX (digits-fed at L = 2, three launches at L = 1); every row
+    identical, a sample bit-exact against the oracle, edge masks and per-ciphertext LUTs included."""
     from tfhe_mi355.parameters import SHORTINT_ALL
 
     p = SHORTINT_ALL[name].with_(lwe_dimension=6)
     space = p.message_modulus * p.carry_modulus
     lwe_sk, glwe_sk, bsk, fbsk = _keys(orc, p, 77)
     eng = _engine(p, bsk)
-    msgs = np.random.default_rng(5).integers(0, space, 131)
+    C = 131 if p.polynomial_size == 8192 else 171
+    h = C // 2
+    msgs = np.random.default_rng(5).integers(0, space, C)
     cts = orc.lwe_encrypt(78, lwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta), p.lwe_modular_std_dev)
     cts[0, :-1] = 0                                   # every a~ = 0
     cts[1, :-1] = np.uint64(1 << 63)                  # a~ = N
     cts[2, -1] = np.uint64((1 << 64) - 1)             # b~ = 2N
     fs = [lambda x: (x * 7 + 2) % space, lambda x: (x + space // 2 + 1) % space]
     luts = np.stack([orc.fill_accumulator(p.polynomial_size, 1, p.message_modulus, p.carry_modulus, f) for f in fs])
-    idx = (np.arange(131) % 3 == 1).astype(np.uint32)  # per-ciphertext LUTs
+    idx = (np.arange(C) % 3 == 1).astype(np.uint32)  # per-ciphertext LUTs
     whole = eng.programmable_bootstrap(cts, luts, lut_indexes=idx)
-    halves = np.concatenate([eng.programmable_bootstrap(cts[:65], luts, lut_indexes=idx[:65]),
-                             eng.programmable_bootstrap(cts[65:], luts, lut_indexes=idx[65:])])
+    halves = np.concatenate([eng.programmable_bootstrap(cts[:h], luts, lut_indexes=idx[:h]),
+                             eng.programmable_bootstrap(cts[h:], luts, lut_indexes=idx[h:])])
     assert np.array_equal(whole, halves), f"{np.count_nonzero(np.any(whole != halves, axis=1))} rows differ"
-    sample = np.array([0, 1, 2, 64, 65, 130])
+    sample = np.array([0, 1, 2, h - 1, h, C - 1])
     assert np.array_equal(whole[sample], fbsk.pbs(cts[sample], luts, lut_idx=idx[sample], threads=6))
     dec = decode(orc.lwe_decrypt(glwe_sk, whole[3:]), p.delta) % space
     assert np.array_equal(dec, [fs[i](m) for i, m in zip(idx[3:], msgs[3:])])
