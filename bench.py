@@ -527,6 +527,10 @@ OTHER_WORKLOADS = (
     ("4_4_full", "4_4", {"steps": 1, "global_batch": 65536, "warmup_batch": 1024}),
     ("3_3", "3_3", {"steps": 3, "callers": True}),
     ("mb3_3g3", "mb3_3g3", {"steps": 3, "callers": True}),
+    # the other on-chip CMUX shapes: N = 4096 L = 2 (two ciphertexts per workgroup)
+    # and N = 8192 L = 1
+    ("1_4", "1_4", {"steps": 3}),
+    ("6_0", "6_0", {"steps": 3}),
 )
 # Wall-clock budget of one such workload (keys, warm-up, steps, checks).  N = 1: the child's
 # subprocess timeout; N > 1: a per-rank watchdog (below).  BENCH_WORKLOAD_BUDGET_S overrides.
