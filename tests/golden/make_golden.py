@@ -26,6 +26,9 @@ CASES = [
     ("split_3_3_n8", "PARAM_MESSAGE_3_CARRY_3_KS_PBS", 104, 8, [5, 60], (3, 7)),
     ("split_1_6_n6", "PARAM_MESSAGE_1_CARRY_6_KS_PBS", 105, 6, [1, 100], (1, 1)),
     ("multibit_3_3_g3_n6", "PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_3_KS_PBS", 106, 6, [3, 44], (2, 5)),
+    # round 5: the on-chip CMUX's other shapes, N = 4096 L = 2 and N = 8192 L = 1 (base 2^22)
+    ("split_1_4_n8", "PARAM_MESSAGE_1_CARRY_4_KS_PBS", 107, 8, [3, 30], (5, 2)),
+    ("split_6_0_n8", "PARAM_MESSAGE_6_CARRY_0_KS_PBS", 108, 8, [9, 50], (3, 4)),
 ]
 
 
