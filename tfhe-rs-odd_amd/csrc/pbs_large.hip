@@ -1666,19 +1666,27 @@ __global__ void __launch_bounds__(1024) split_inv_digits_kernel(LargePbsLaunch a
 #ifndef ONCHIP_MAC_SB
 #define ONCHIP_MAC_SB 4  // MAC slots per scheduling region (GGSW loads in flight)
 #endif
+#ifndef ONCHIP_4096_CPW
+#define ONCHIP_4096_CPW 1  // N = 4096: 1 = one ciphertext per 256-thread workgroup (two workgroups per CU,
+                           // independent barriers); 2 = two ciphertexts per 512-thread workgroup
+#endif
 template <int N>
 struct OnchipCfg {
     static constexpr int M = N / 2, R = M / 1024;
-    static constexpr int THREADS = 512;
-    static constexpr int CPW = 4 / R;          // ciphertexts per workgroup (N = 4096: two, 4 waves each)
+    static constexpr int CPW = R == 4 ? 1 : ONCHIP_4096_CPW;  // ciphertexts per workgroup
+    static constexpr int THREADS = 256 * R / 2 * CPW;         // 2 R waves per ciphertext
+    static constexpr int WAVES = THREADS / 64;
+    static constexpr int WPS = THREADS / 256;                 // waves per SIMD of one workgroup
+    static constexpr int MIN_WPS = 2;                         // 2 waves per SIMD per CU: 256 VGPRs
     static constexpr int TPC = THREADS / CPW;  // threads per ciphertext
     static constexpr int H = 1024 / TPC;       // top-stage butterflies per thread
     static constexpr int BUF = SubFft::XL;    // double2 per wave buffer
-    static constexpr int S1 = 8 * BUF;        // twiddle table offset (double2 units)
+    static constexpr int S1 = WAVES * BUF;    // twiddle table offset (double2 units)
     static constexpr int FLAGS = S1 + SubFft::Lds::s1_len;  // pair-sync flags (double2 offset), one word per wave
-    static constexpr size_t LDS = sizeof(double2) * FLAGS + 4 * 8;
-    static_assert(R == 4 || R == 2, "8 waves = CPW ciphertexts x R sub-blocks x 2 rows");
-    static_assert(8 * BUF * sizeof(double2) == CPW * 2 * M * sizeof(acc_pair), "the rotation's pairs fill the wave buffers");
+    static constexpr size_t LDS = sizeof(double2) * FLAGS + 4 * WAVES;
+    static_assert(R == 4 || R == 2, "CPW ciphertexts x R sub-blocks x 2 rows of waves");
+    static_assert(WAVES * BUF * sizeof(double2) == CPW * 2 * M * sizeof(acc_pair), "the rotation's pairs fill the wave buffers");
+    static_assert(LDS <= 160 * 1024 / (MIN_WPS / WPS), "LDS of the workgroups one CU holds");
 };
 
 // MAC of level L - LI for one sub-block: both rows' spectra from their buffers F (row r at
@@ -1771,7 +1779,7 @@ __device__ __forceinline__ int opaque_zero() {
 }
 
 template <int N, bool D32, int L = 2>
-__global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
+__global__ void __launch_bounds__(OnchipCfg<N>::THREADS, OnchipCfg<N>::MIN_WPS / OnchipCfg<N>::WPS) onchip_cmux_kernel(LargePbsLaunch a) {
     using S = Split<N>;
     using Cfg = OnchipCfg<N>;
     static_assert(L == 1 || L == 2, "one or two decomposition levels");
@@ -1792,7 +1800,7 @@ __global__ void __launch_bounds__(512, 1) onchip_cmux_kernel(LargePbsLaunch a) {
     double2 *s1 = lds + Cfg::S1;
     // sub-block stage twiddles W_1024[lane c] = W_M[R lane c]  (oracle dif_rec tstride R)
     for (int e = t; e < SubFft::Lds::s1_len; e += Cfg::THREADS) s1[e] = a.W[R * (e & 63) * ((e >> 6) + 1)];
-    if (t < 8) reinterpret_cast<uint32_t *>(lds + Cfg::FLAGS)[t] = 0;
+    if (t < Cfg::WAVES) reinterpret_cast<uint32_t *>(lds + Cfg::FLAGS)[t] = 0;
     GroupSync<2> ps;  // the two waves of sub-block q (flag words 2 q, 2 q + 1)
     ps.mine = lds_addr(lds + Cfg::FLAGS) + 4u * wave;
     const SubFft::Lds tw{s1, s1};
