@@ -40,7 +40,7 @@
  *     one-ciphertext-per-CU latency kernels (same outputs; TFHE_MI355_LATENCY_MAX = rows
  *     overrides, 0 = never).  At N = 8192 / 4096, k = 1, L = 1 or 2 (classic), batches of at least
  *     3/8 / 5/8 of the CU count (96 / 160 rows on 256 CUs) run the on-chip CMUX (the whole blind
- *     rotation in one workgroup per ciphertext or pair of ciphertexts, no scratch used), smaller
+ *     rotation in one workgroup per ciphertext, two per CU at N = 4096, no scratch used), smaller
  *     ones the split CMUX (same outputs; TFHE_MI355_ONCHIP_MIN = rows overrides,
  *     TFHE_MI355_ONCHIP=0 = never).
  *     The _async calls hold no per-context mutable state: every device scratch buffer they

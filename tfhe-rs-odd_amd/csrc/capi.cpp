@@ -369,7 +369,7 @@ size_t pbs_scratch_bytes(const TfheMi355Context *c, size_t count) {
 }
 
 // The on-chip CMUX (the whole blind rotation in one workgroup: one ciphertext per CU at N = 8192,
-// two at N = 4096) against the split CMUX (a ciphertext's sub-blocks over several CUs, in several
+// two per CU at N = 4096) against the split CMUX (a ciphertext's sub-blocks over several CUs, in several
 // launches per CMUX): at 3_3 the split path takes 16.3 / 18.8 / 23.2 / 25.4 ms for 1 / 64 / 96 / 128
 // ciphertexts, the on-chip one 22.9-25.1 ms for any count up to one per CU
 // (profiles/r05_sweep33_onchip{0,1}.json); at 1_4 (N = 4096) split 11.0 / 13.3 / 14.0 / 19.3 ms for
