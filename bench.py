@@ -292,6 +292,8 @@ def split_chunk(p, units: int) -> int:
     """Ciphertexts per pass of the split CMUX (capi.cpp large_chunk)."""
     if p.polynomial_size >= 32768:
         return min(units, 128)
+    if p.grouping_factor:
+        return min(units, 1024)
     M, k1 = p.polynomial_size // 2, p.glwe_dimension + 1
     per = k1 * p.polynomial_size * 8 + p.pbs_level * k1 * M * 16
     return min(units, min(1024, max(64, (200 << 20) // per // 64 * 64)))

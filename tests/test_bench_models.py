@@ -63,13 +63,14 @@ def test_flop_models():
 
 def test_split_chunk_matches_the_engine_rule():
     """bench.split_chunk mirrors capi.cpp large_chunk: 200 MiB of (acc + spectra) per pass, a
-    multiple of 64 in [64, 1024], 128 at N = 32768."""
+    multiple of 64 in [64, 1024], 128 at N = 32768, 1024 for multi-bit."""
     from tfhe_mi355.parameters import ALL
 
     assert bench.split_chunk(ALL["PARAM_MESSAGE_3_CARRY_3_KS_PBS"], 4096) == 512
     assert bench.split_chunk(ALL["PARAM_MESSAGE_4_CARRY_4_KS_PBS"], 4096) == 128
     assert bench.split_chunk(ALL["PARAM_MESSAGE_1_CARRY_4_KS_PBS"], 4096) == 1024
     assert bench.split_chunk(ALL["PARAM_MESSAGE_2_CARRY_5_KS_PBS"], 4096) == 256
+    assert bench.split_chunk(ALL["PARAM_MULTI_BIT_MESSAGE_3_CARRY_3_GROUP_3_KS_PBS"], 4096) == 1024
 
 
 def test_mall_ceiling_is_the_committed_probe():

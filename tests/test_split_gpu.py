@@ -283,7 +283,7 @@ def test_split_multi_bit_pbs_bit_exact_vs_oracle(orc, name):
 
 @pytest.mark.parametrize("name", MB_SPLIT)
 def test_onchip_and_split_multi_bit_agree(orc, name):
-    """Multi-bit N = 8192: a 130-ciphertext call (one 512-ciphertext chunk of the split CMUX with a
+    """Multi-bit N = 8192: a 130-ciphertext call (one chunk of the split CMUX with a
     partial pair) and the same ciphertexts in calls of 65 (odd counts: a pair workgroup with an idle
     slot); every row identical, a sample bit-exact against the oracle.  (Round 5 also ran it against
     the measured-slower multi-bit on-chip CMUX: profiles/r05_onchip_mb_tests.log.)"""

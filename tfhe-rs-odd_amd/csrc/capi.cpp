@@ -349,6 +349,10 @@ bool is_large(const TfheMi355Context *c) {
 // round 4 sweeps (profiles/r04_chunk_sweep.log): 3_3 384 / 512 / 768 -> 5.94k / 6.17k / 5.55k,
 // 2_5 192 / 256 -> 2268 / 2307, 1_4 832 / 1024 -> 13.5k / 14.3k KS+PBS/s (160 MiB gave 384 / 192 / 832);
 // multi-bit mb3_3g3 (512 here) 384 / 512 / 768 / 1024 -> 9.11k / 9.30k / 8.59k / 8.19k (r04_mbchunk_*.log).
+// Round 5, after the paired multi-bit kernel (large_mb_pair2_kernel) and the fused top_inv/top_fwd
+// made the chunk's spectra traffic the smaller share: 512 / 768 / 1024 / 1280 / 2048 ->
+// mb3_3g3 12.04k / 12.24k / 12.18k / 11.52k / 11.54k, mb3_3g2 10.21k / 10.44k / 10.63k / 9.65k /
+// 9.65k (profiles/r05_mbchunk_*.json), so multi-bit takes 1024 (400 MiB of scratch).
 size_t large_chunk(const TfheMi355Context *c) {
     static const size_t forced = [] {
         const char *e = std::getenv("TFHE_MI355_LARGE_CHUNK");
@@ -357,6 +361,7 @@ size_t large_chunk(const TfheMi355Context *c) {
     }();
     if (forced) return forced;
     if (c->N() >= 32768) return 128;
+    if (c->p.grouping_factor) return 1024;
     const size_t per = large_pbs_scratch_per_ct((int)c->N(), (int)c->k(), (int)c->p.pbs_level);
     return std::min<size_t>(1024, std::max<size_t>(64, ((size_t)200 << 20) / per / 64 * 64));
 }
