@@ -18,7 +18,7 @@ case $tag in
            K='large_|split_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=512; M='large_dsub_kernel|large_sub_kernel'
          fi; ARGS="--params 3_3 --batch 512" ;;
   1_4|6_0|2_3) K='onchip_|ks_digits|ks_mfma'; U='onchip_cmux_kernel'; UPD=512; M='onchip_cmux_kernel'; ARGS="--params $tag --batch 512" ;;
-  mb3_3g2|mb3_3g3) K='large_|split_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=512; M='large_mb_pair2_kernel|large_pair_sub_kernel|large_sub_kernel'; ARGS="--params $tag --batch 512" ;;
+  mb3_3g2|mb3_3g3) K='large_|split_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=1024; M='large_mb_pair2_kernel|large_pair_sub_kernel|large_sub_kernel'; ARGS="--params $tag --batch 1024" ;;
   *) echo "unknown tag $tag"; exit 2 ;;
 esac
 B="$ARGS --steps 2 --warmup 1 --no-cpu-baseline --no-host-abi --no-single-call"
