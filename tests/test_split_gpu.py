@@ -285,7 +285,8 @@ def test_split_multi_bit_pbs_bit_exact_vs_oracle(orc, name):
 def test_onchip_and_split_multi_bit_agree(orc, name):
     """Multi-bit N = 8192: a 130-ciphertext call (one chunk of the split CMUX with a
     partial pair) and the same ciphertexts in calls of 65 (odd counts: a pair workgroup with an idle
-    slot); every row identical, a sample bit-exact against the oracle.  (Round 5 also ran it against
+    slot) and in 47-ciphertext passes through the async entry; every row identical, a sample bit-exact
+    against the oracle.  (Round 5 also ran it against
     the measured-slower multi-bit on-chip CMUX: profiles/r05_onchip_mb_tests.log.)"""
     from tfhe_mi355 import client
     from tfhe_mi355.parameters import MULTI_BIT_ALL
@@ -307,6 +308,18 @@ def test_onchip_and_split_multi_bit_agree(orc, name):
     whole = eng.programmable_bootstrap(cts, acc)
     halves = np.concatenate([eng.programmable_bootstrap(cts[:65], acc), eng.programmable_bootstrap(cts[65:], acc)])
     assert np.array_equal(whole, halves), f"{np.count_nonzero(np.any(whole != halves, axis=1))} rows differ"
+    # several passes of the split CMUX: the async entry with scratch for 47 ciphertexts (chunks of
+    # 47, 47, 36: odd chunks end on a half-used pair workgroup)
+    import torch
+
+    dev = torch.device("cuda", 0)
+    d_in = torch.from_numpy(cts.view(np.int64)).to(dev)
+    d_out = torch.zeros((130, p.big_lwe_dimension + 1), dtype=torch.int64, device=dev)
+    d_lut = torch.from_numpy(acc.view(np.int64)).to(dev)
+    scratch = torch.empty(eng.pbs_scratch_bytes(1) * 47, dtype=torch.uint8, device=dev)
+    eng.programmable_bootstrap_async(d_in, d_out, d_lut, 1, 130, d_scratch=scratch)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_out.cpu().numpy().view(np.uint64), whole)
     sample = np.array([0, 1, 2, 64, 129])
     assert np.array_equal(whole[sample], fb.pbs(cts[sample], acc, threads=5))
     assert np.array_equal(decode(orc.lwe_decrypt(glwe_sk, whole[3:]), p.delta) % 64, (msgs[3:] * 5 + 1) % 64)
