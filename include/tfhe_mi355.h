@@ -232,10 +232,11 @@ int tfhe_mi355_programmable_bootstrap_async(TfheMi355Context *ctx, const uint64_
  *   - multi-bit N = 2048 / 512: 0;
  *   - N >= 4096, classic and multi-bit (N = 8192): the accumulators + spectra of one pass of
  *     the split CMUX (also asked for where the on-chip CMUX will run: the call picks by count)
- *     min(count, chunk) ciphertexts (chunk = 128 at N = 32768; below, ~200 MiB worth in multiples
- *     of 64, at most 1024: 1024 at N = 4096, 512 at N = 8192 (3_3 and multi-bit 3_3), 256 / 192
- *     at N = 16384, L = 2 / 3; TFHE_MI355_LARGE_CHUNK overrides; e.g. 1.5 MiB per ciphertext at 4_4).  Less scratch runs smaller passes; the call fails below one
- *     ciphertext's worth.
+ *     min(count, chunk) ciphertexts (chunk = 128 at N = 32768, 1024 for multi-bit (N = 8192,
+ *     400 MiB); otherwise ~200 MiB worth in multiples of 64, at most 1024: 1024 at N = 4096, 512
+ *     at N = 8192 (3_3), 256 / 192 at N = 16384, L = 2 / 3; TFHE_MI355_LARGE_CHUNK overrides;
+ *     e.g. 1.5 MiB per ciphertext at 4_4).  Less scratch runs smaller passes; the call fails below
+ *     one ciphertext's worth.
  * tfhe_mi355_programmable_bootstrap_async fails when given less than this (N <= 2048) -- it never
  * falls back silently.  tfhe_mi355_blind_rotate_async takes no scratch and runs the one-pass grid. */
 int tfhe_mi355_programmable_bootstrap_scratch(TfheMi355Context *ctx, size_t count, size_t *bytes);
