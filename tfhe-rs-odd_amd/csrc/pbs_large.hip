@@ -811,6 +811,9 @@ __global__ void __launch_bounds__((PairSubCfg<K, L>::THREADS), 2) large_pair_sub
 #ifndef MB2_PIPE
 #define MB2_PIPE 1  // phase 2's GGSW operand batches software pipelined (0: one (level, column) batch at a time)
 #endif
+#ifndef MB2_SROT
+#define MB2_SROT 1  // MAC slot of wave w rotated per workgroup (0: slot 8 h + w everywhere)
+#endif
 #ifndef MB2_TSKIP
 #define MB2_TSKIP 0  // timing-only builds (wrong outputs): 1 no GGSW loads, 2 no forward sub-FFTs, 4 no
                      // inverse sub-FFTs, 8 no keybundle sums (PBS_MB_TSKIP_MONO=1: conflict-free monomials)
@@ -844,6 +847,9 @@ __global__ void __launch_bounds__((MbPair2Cfg<N, G>::THREADS), 2) large_mb_pair2
     pair_sub_block_of<R>(blockIdx.x, q, cp);
     const int cnt = a.chunk_count;
     if (2 * cp >= cnt) return;  // whole workgroup
+    // the slot of wave w in each MAC round: 8 h + ws, rotated by the workgroup's index among those
+    // of its XCD (MB2_SROT) so that its CUs do not all stream the same GGSW slot at once
+    const int ws = (wave + (MB2_SROT ? (int)(blockIdx.x >> 3) : 0)) & 7;
     double2 *s1 = lds + Cfg::S1;
     for (int e = threadIdx.x; e < SubFft::Lds::s1_len; e += Cfg::THREADS) s1[e] = a.W[R * (e & 63) * ((e >> 6) + 1)];
     const SubFft::Lds tw{s1, s1};
@@ -895,7 +901,7 @@ __global__ void __launch_bounds__((MbPair2Cfg<N, G>::THREADS), 2) large_mb_pair2
         // ---- publish slots 8h .. 8h + 7 of this wave's spectrum ----
 #pragma unroll
         for (int sl = 0; sl < 8; sl++) *hslot(c1, p1, sl) = make_double2(v[8 * h + sl].re, v[8 * h + sl].im);
-        const int s = 8 * h + wave;  // this wave's slot in round h (wave-uniform)
+        const int s = 8 * h + ws;  // this wave's slot in round h (wave-uniform)
 #if MB2_PIPE
         // the round's 8 operand batches (level, column, row) of 2^g GGSW values each, software
         // pipelined: batch k + 1 in flight while batch k is consumed (the same registers as one
@@ -931,7 +937,7 @@ __global__ void __launch_bounds__((MbPair2Cfg<N, G>::THREADS), 2) large_mb_pair2
                 for (int c = 0; c < CPW; c++)
 #pragma unroll
                     for (int rr = 0; rr <= K; rr++) {
-                        const double2 t = *hslot(c, (lvl - 1) * (K + 1) + rr, wave);
+                        const double2 t = *hslot(c, (lvl - 1) * (K + 1) + rr, ws);
                         ff[c][rr] = cx{t.x, t.y};
                     }
             }
@@ -962,7 +968,7 @@ __global__ void __launch_bounds__((MbPair2Cfg<N, G>::THREADS), 2) large_mb_pair2
             for (int c = 0; c < CPW; c++)
 #pragma unroll
                 for (int r = 0; r <= K; r++) {
-                    const double2 t = *hslot(c, (lvl - 1) * (K + 1) + r, wave);
+                    const double2 t = *hslot(c, (lvl - 1) * (K + 1) + r, ws);
                     ff[c][r] = cx{t.x, t.y};
                 }
 #pragma unroll
@@ -1009,7 +1015,7 @@ __global__ void __launch_bounds__((MbPair2Cfg<N, G>::THREADS), 2) large_mb_pair2
         for (int c = 0; c < CPW; c++)
 #pragma unroll
             for (int col = 0; col <= K; col++)
-                *oslot(c, col, 8 * h + wave) = make_double2(o[h][c][col].re, o[h][c][col].im);
+                *oslot(c, col, 8 * h + ws) = make_double2(o[h][c][col].re, o[h][c][col].im);
     __syncthreads();
     if (wave >= CPW * (K + 1)) return;
     const int c = wave / (K + 1), col = wave % (K + 1);
@@ -1666,6 +1672,9 @@ __global__ void __launch_bounds__(1024) split_inv_digits_kernel(LargePbsLaunch a
 #ifndef ONCHIP_MAC_SB
 #define ONCHIP_MAC_SB 4  // MAC slots per scheduling region (GGSW loads in flight)
 #endif
+#ifndef ONCHIP_QROT
+#define ONCHIP_QROT 1  // wave pair -> sub-block rotated per workgroup (0: pair p on sub-block p)
+#endif
 #ifndef ONCHIP_4096_CPW
 #define ONCHIP_4096_CPW 1  // N = 4096: 1 = one ciphertext per 256-thread workgroup (two workgroups per CU,
                            // independent barriers); 2 = two ciphertexts per 512-thread workgroup
@@ -1792,9 +1801,12 @@ __global__ void __launch_bounds__(OnchipCfg<N>::THREADS, OnchipCfg<N>::MIN_WPS /
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     // wave = 2 R c + 2 q + wr: ciphertext c of the workgroup, sub-block q, row (forward) = column
     // (MAC, inverse) wr; thread t works for ciphertext ctl = t / TPC as thread tc = t mod TPC
-    const int q = CPW == 1 ? wave >> 1 : (wave >> 1) & (R - 1), wr = wave & 1;
+    // sub-block of the wave pair, rotated by the workgroup's index among those of its XCD
+    // (ONCHIP_QROT) so that the CUs of an XCD do not all stream the same GGSW slice at once
+    const int q = ((wave >> 1) + (ONCHIP_QROT ? (int)(blockIdx.x >> 3) : 0)) & (R - 1), wr = wave & 1;
     const int ctl = CPW == 1 ? 0 : t / TPC, tc = CPW == 1 ? t : t % TPC;
     const int cb = 2 * R * ctl;  // this thread's ciphertext's first wave buffer
+    const int wbuf = cb + 2 * q + wr;  // this wave's buffer: sub-block q, row / column wr
     const int ct_raw = CPW == 1 ? (int)blockIdx.x : (int)blockIdx.x * CPW + ctl;
     const int ct = CPW == 1 ? ct_raw : min(ct_raw, a.count - 1);  // a padding slot repeats the last ciphertext
     double2 *s1 = lds + Cfg::S1;
@@ -1804,8 +1816,8 @@ __global__ void __launch_bounds__(OnchipCfg<N>::THREADS, OnchipCfg<N>::MIN_WPS /
     GroupSync<2> ps;  // the two waves of sub-block q (flag words 2 q, 2 q + 1)
     ps.mine = lds_addr(lds + Cfg::FLAGS) + 4u * wave;
     const SubFft::Lds tw{s1, s1};
-    cx *xb = reinterpret_cast<cx *>(lds) + wave * BUF;
-    double2 *own = lds + wave * BUF;
+    cx *xb = reinterpret_cast<cx *>(lds) + wbuf * BUF;
+    double2 *own = lds + wbuf * BUF;
     WaveLocalSync wsync;
     const uint64_t *in = a.lwe_in + (size_t)ct * (a.n + 1);
     // twist and top-stage twiddles through buffer loads: one VGPR offset, the rest in SGPRs
@@ -1957,7 +1969,7 @@ __global__ void __launch_bounds__(OnchipCfg<N>::THREADS, OnchipCfg<N>::MIN_WPS /
             if (ONCHIP_PAIRSYNC) ps();  // only the partner reads this spectrum
             else __syncthreads();
             // ---- MAC of this level, column wr ----
-            onchip_mac<M, BUF, LI, L>(rg, 16u * lane, lds + (wave & ~1) * BUF + lane, o, pf);
+            onchip_mac<M, BUF, LI, L>(rg, 16u * lane, lds + (wbuf & ~1) * BUF + lane, o, pf);
             __syncthreads();  // the partner has read this wave's spectrum
         };
         level(std::integral_constant<int, 0>{});
