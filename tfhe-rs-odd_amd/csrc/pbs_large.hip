@@ -1094,6 +1094,9 @@ __device__ __forceinline__ cx r4_out(cx x0, cx x1, cx x2, cx x3) {
 #ifndef LARGE_GRP_WMAP
 #define LARGE_GRP_WMAP 1
 #endif
+#ifndef LARGE_GRP_QROT
+#define LARGE_GRP_QROT 1  // group kernel: wave pair -> sub-block rotated per ciphertext (0: pair k on G + 4k)
+#endif
 template <int KW>
 __device__ __forceinline__ constexpr int grp_wave(int li, int k) { return LARGE_GRP_WMAP ? 2 * k + li : li * KW + k; }
 
@@ -1195,7 +1198,8 @@ __device__ __forceinline__ void group_compute_dg2(const GroupDg2 &d, cx (&y)[2][
 }
 
 template <int KW, int G>
-__device__ __forceinline__ void group_phase1(const LargePbsLaunch &a, int cl, int part, int ap, int h, double2 *lds) {
+__device__ __forceinline__ void group_phase1(const LargePbsLaunch &a, int cl, int part, int ap, int h, double2 *lds,
+                                             int rot) {
     const __amdgpu_buffer_rsrc_t rdig = make_rsrc(group_digits(a, cl)), rtw = make_rsrc(a.twist);
 #if LARGE_GRP_TW_SHARED
     cx yy[2][2][4];  // [row][li][A]
@@ -1251,7 +1255,8 @@ __device__ __forceinline__ void group_phase1(const LargePbsLaunch &a, int cl, in
                 const int kg = KW * part + k;  // uniform: part is per workgroup
                 const cx x = KW == 4 ? y[l][k] : (part ? y[l][2 + k] : y[l][k]);
                 const cx v = (G + 4 * kg) ? cmulw(x, wt[k].re, wt[k].im) : x;
-                lds[(grp_wave<KW>(l, k) * 2 + r) * 512 + (ap - 512 * h)] = make_double2(v.re, v.im);
+                // sub-block k goes to wave pair (k - rot) mod KW (LARGE_GRP_QROT)
+                lds[(grp_wave<KW>(l, (k - rot) & (KW - 1)) * 2 + r) * 512 + (ap - 512 * h)] = make_double2(v.re, v.im);
             }
         }
     }
@@ -1325,13 +1330,13 @@ __device__ __forceinline__ void group_mac_pair(cx (&f)[2][16], cx (&v)[16], doub
 }
 
 template <int KW, int G>
-__device__ __forceinline__ void group_cmux_body(const LargePbsLaunch &a, int i, int cl, int part, double2 *lds) {
+__device__ __forceinline__ void group_cmux_body(const LargePbsLaunch &a, int i, int cl, int part, double2 *lds, int rot) {
     constexpr int K = 1, L = 2;
     using Cfg = LargeGroupCfg<KW>;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = LARGE_GRP_WMAP ? wave & 1 : wave / KW, k = LARGE_GRP_WMAP ? wave >> 1 : wave % KW;
-    const int sblk = G + 4 * (KW * part + k);
+    const int sblk = G + 4 * (KW * part + ((k + rot) & (KW - 1)));  // wave pair k runs sub-block k + rot
     double2 *s1 = lds + Cfg::REGION;
     // sub-block stage twiddles W_1024[lane c] = W_M[16 lane c]  (oracle dif_rec tstride 16)
     for (int e = tid; e < SubFft::Lds::s1_len; e += Cfg::THREADS) s1[e] = a.W[16 * (e & 63) * ((e >> 6) + 1)];
@@ -1346,7 +1351,7 @@ __device__ __forceinline__ void group_cmux_body(const LargePbsLaunch &a, int i, 
         if (h) __syncthreads();  // every wave has picked up half 0
 #pragma unroll
         for (int q = 0; q < 512 / Cfg::THREADS; q++)
-            if (!(LARGE_TSKIP & 1)) group_phase1<KW, G>(a, cl, part, 512 * h + Cfg::THREADS * q + tid, h, lds);
+            if (!(LARGE_TSKIP & 1)) group_phase1<KW, G>(a, cl, part, 512 * h + Cfg::THREADS * q + tid, h, lds, rot);
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < 2; r++)
@@ -1423,11 +1428,13 @@ __global__ void __launch_bounds__(GroupCfg::THREADS, 2) large_group_cmux_kernel(
     if (cl >= a.chunk_count) return;  // whole workgroup
     const int part = (m >> 2) % PARTS;
     (void)ct0;
+    // wave pair -> sub-block rotated per ciphertext (LARGE_GRP_QROT, as ONCHIP_QROT)
+    const int rot = (LARGE_GRP_QROT && KW == 4) ? (m >> 2) & 3 : 0;
     switch (m & 3) {
-        case 0: group_cmux_body<KW, 0>(a, i, cl, part, lds); break;
-        case 1: group_cmux_body<KW, 1>(a, i, cl, part, lds); break;
-        case 2: group_cmux_body<KW, 2>(a, i, cl, part, lds); break;
-        default: group_cmux_body<KW, 3>(a, i, cl, part, lds); break;
+        case 0: group_cmux_body<KW, 0>(a, i, cl, part, lds, rot); break;
+        case 1: group_cmux_body<KW, 1>(a, i, cl, part, lds, rot); break;
+        case 2: group_cmux_body<KW, 2>(a, i, cl, part, lds, rot); break;
+        default: group_cmux_body<KW, 3>(a, i, cl, part, lds, rot); break;
     }
 }
 
