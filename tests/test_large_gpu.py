@@ -171,5 +171,6 @@ def test_large_pbs_two_chunks_ragged(orc, small_n_4_4):
     got = eng.programmable_bootstrap(cts, acc)
     dec = decode(orc.lwe_decrypt(keys.glwe_sk, got), p.delta) % 256
     assert np.array_equal(dec, (msgs * 5 + 1) % 256)
-    sample = np.array([0, 127, 128, 199])
-    assert np.array_equal(got[sample], keys.fbsk.pbs(cts[sample], acc, threads=4))
+    # one sample per sub-block rotation of the group kernel (rotation (cl / 8) mod 4: 0, 1, 2, 3)
+    sample = np.array([0, 40, 80, 127, 128, 199])
+    assert np.array_equal(got[sample], keys.fbsk.pbs(cts[sample], acc, threads=6))
