@@ -19,10 +19,10 @@ def test_programmable_bootstrap_every_message(orc, keys_2_2):
     fbsk = cc.convert_standard_lwe_bootstrap_key_to_fourier(k.bsk, P)
     assert (fbsk.input_lwe_dimension, fbsk.output_lwe_dimension, fbsk.glwe_size) == (742, 2048, 2)
     acc = orc.fill_accumulator(P.polynomial_size, 1, 4, 4, lambda x: (7 * x + 3) % 16)
-    msgs = np.arange(16, dtype=np.uint64)
+    msgs = np.repeat(np.arange(15, -1, -1, dtype=np.uint64), 4)  # msg = 15 .. 0, several encryptions each
     cts = orc.lwe_encrypt(31, k.lwe_sk, msgs * np.uint64(P.delta), P.lwe_modular_std_dev)
-    outs = np.zeros((16, P.big_lwe_dimension + 1), dtype=np.uint64)
-    for i in range(16):   # one ciphertext per call, as the reference's loop
+    outs = np.zeros((msgs.size, P.big_lwe_dimension + 1), dtype=np.uint64)
+    for i in range(msgs.size):   # one ciphertext per call, as the reference's loop
         cc.programmable_bootstrap_lwe_ciphertext(cts[i], outs[i], acc, fbsk)
     assert np.array_equal(decode(orc.lwe_decrypt(k.glwe_sk, outs), P.delta) % 16, (7 * msgs + 3) % 16)
     assert np.array_equal(outs, k.fbsk.pbs(cts, acc, threads=16))
@@ -44,8 +44,11 @@ def test_multi_bit_programmable_bootstrap(orc, keys_mb):
     msgs = np.arange(16, dtype=np.uint64)
     cts = orc.lwe_encrypt(32, k.lwe_sk, msgs * np.uint64(P.delta), P.lwe_modular_std_dev)
     outs = np.zeros((16, P.big_lwe_dimension + 1), dtype=np.uint64)
-    for i in range(16):
+    again = np.zeros_like(outs)
+    for i in range(16):  # run twice for determinism, as lwe_multi_bit_programmable_bootstrapping.rs:9-10
         cc.multi_bit_programmable_bootstrap_lwe_ciphertext(cts[i], outs[i], acc, bsk, thread_count=7)
+        cc.multi_bit_programmable_bootstrap_lwe_ciphertext(cts[i], again[i], acc, bsk, thread_count=7)
+    assert np.array_equal(outs, again)
     assert np.array_equal(decode(orc.lwe_decrypt(k.glwe_sk, outs), P.delta) % 16, (msgs + 5) % 16)
     assert np.array_equal(outs, k.fbsk.pbs(cts, acc, threads=16))
 
