@@ -1717,7 +1717,20 @@ struct OnchipCfg {
 #ifndef ONCHIP_PF
 #define ONCHIP_PF 4  // MAC slots whose GGSW operands are issued before the publish barrier (0: none)
 #endif
-constexpr int ONCHIP_PFS = ONCHIP_PF > 0 ? ONCHIP_PF : 1;
+// N = 8192, L = 2 (3_3): 6 slots before the barrier, then regions of 3 -- since the sub-block
+// rotation, 10.75-10.77k -> 11.29-11.30k KS+PBS/s against 4 / 4 (profiles/r05_ab_onchip_pfsb.log)
+#ifndef ONCHIP_PF_8192_L2
+#define ONCHIP_PF_8192_L2 6
+#endif
+#ifndef ONCHIP_MAC_SB_8192_L2
+#define ONCHIP_MAC_SB_8192_L2 3
+#endif
+template <int M, int L>
+constexpr int onchip_pf() { return M == 4096 && L == 2 ? ONCHIP_PF_8192_L2 : ONCHIP_PF; }
+template <int M, int L>
+constexpr int onchip_sb() { return M == 4096 && L == 2 ? ONCHIP_MAC_SB_8192_L2 : ONCHIP_MAC_SB; }
+template <int M, int L>
+constexpr int onchip_pfs() { return onchip_pf<M, L>() > 0 ? onchip_pf<M, L>() : 1; }
 // GGSW operands (rows 0 and 1 of level L - LI, column of rg) of MAC slot s
 template <int M, int LI, int L = 2>
 __device__ __forceinline__ void onchip_ggsw(__amdgpu_buffer_rsrc_t rg, uint32_t gvo, int s, double2 &g0, double2 &g1) {
@@ -1727,15 +1740,16 @@ __device__ __forceinline__ void onchip_ggsw(__amdgpu_buffer_rsrc_t rg, uint32_t 
 }
 template <int M, int BUF, int LI, int L = 2>
 __device__ __forceinline__ void onchip_mac(__amdgpu_buffer_rsrc_t rg, uint32_t gvo, const double2 *F, cx (&o)[16],
-                                           const double2 (&pf)[ONCHIP_PFS][2]) {
+                                           const double2 (&pf)[onchip_pfs<M, L>()][2]) {
+    constexpr int PF = onchip_pf<M, L>(), PFS = onchip_pfs<M, L>(), SB = onchip_sb<M, L>();
 #pragma unroll
     for (int s = 0; s < 16; s++) {
-        if (s >= ONCHIP_PF && (s - ONCHIP_PF) % ONCHIP_MAC_SB == 0) __builtin_amdgcn_sched_barrier(0);
+        if (s >= PF && (s - PF) % SB == 0) __builtin_amdgcn_sched_barrier(0);
         const double2 f0 = F[s * 64], f1 = F[BUF + s * 64];
         double2 g0, g1;
-        if (s < ONCHIP_PF) {
-            g0 = pf[s < ONCHIP_PFS ? s : 0][0];
-            g1 = pf[s < ONCHIP_PFS ? s : 0][1];
+        if (s < PF) {
+            g0 = pf[s < PFS ? s : 0][0];
+            g1 = pf[s < PFS ? s : 0][1];
         } else {
             onchip_ggsw<M, LI, L>(rg, gvo, s, g0, g1);
         }
@@ -1970,9 +1984,9 @@ __global__ void __launch_bounds__(OnchipCfg<N>::THREADS, OnchipCfg<N>::MIN_WPS /
 #pragma unroll
             for (int s = 0; s < 16; s++) own[s * 64 + lane] = make_double2(v[s].re, v[s].im);
             // the first slots' GGSW operands are in flight during the barrier
-            double2 pf[ONCHIP_PFS][2];
+            double2 pf[onchip_pfs<M, L>()][2];
 #pragma unroll
-            for (int s = 0; s < ONCHIP_PF; s++) onchip_ggsw<M, LI, L>(rg, 16u * lane, s, pf[s][0], pf[s][1]);
+            for (int s = 0; s < onchip_pf<M, L>(); s++) onchip_ggsw<M, LI, L>(rg, 16u * lane, s, pf[s][0], pf[s][1]);
             if (ONCHIP_PAIRSYNC) ps();  // only the partner reads this spectrum
             else __syncthreads();
             // ---- MAC of this level, column wr ----
