@@ -1717,10 +1717,11 @@ struct OnchipCfg {
 #ifndef ONCHIP_PF
 #define ONCHIP_PF 4  // MAC slots whose GGSW operands are issued before the publish barrier (0: none)
 #endif
-// N = 8192, L = 2 (3_3): 6 slots before the barrier, then regions of 3 -- since the sub-block
-// rotation, 10.75-10.77k -> 11.29-11.30k KS+PBS/s against 4 / 4 (profiles/r05_ab_onchip_pfsb.log)
+// N = 8192, L = 2 (3_3): 5 slots before the barrier, then regions of 3 -- since the sub-block
+// rotation, 10.75-10.78k -> 11.34-11.37k KS+PBS/s against 4 / 4 (profiles/r05_ab_onchip_pfsb*.log;
+// the other shapes measured best at 4 / 4)
 #ifndef ONCHIP_PF_8192_L2
-#define ONCHIP_PF_8192_L2 6
+#define ONCHIP_PF_8192_L2 5
 #endif
 #ifndef ONCHIP_MAC_SB_8192_L2
 #define ONCHIP_MAC_SB_8192_L2 3
