@@ -811,6 +811,9 @@ __global__ void __launch_bounds__((PairSubCfg<K, L>::THREADS), 2) large_pair_sub
 #ifndef MB2_PIPE
 #define MB2_PIPE 1  // phase 2's GGSW operand batches software pipelined (0: one (level, column) batch at a time)
 #endif
+#ifndef MB2_DEPTH
+#define MB2_DEPTH 2  // MB2_PIPE: operand batches issued ahead of the one being consumed (1: 11.83k / 10.16-10.28k, 2: 11.88k / 10.40-10.43k KS+PBS/s at g = 3 / 2, profiles/r05_ab_mb_depth.log)
+#endif
 #ifndef MB2_SROT
 #define MB2_SROT 1  // MAC slot of wave w rotated per workgroup (0: slot 8 h + w everywhere)
 #endif
@@ -915,8 +918,10 @@ __global__ void __launch_bounds__((MbPair2Cfg<N, G>::THREADS), 2) large_mb_pair2
                                                                       (uint32_t)((lv - 1) * (K + 1) + rr) * rowb +
                                                                       16u * (uint32_t)(cl * M) + 1024u * (uint32_t)s);
         };
-        double2 gb[2][NSEL];
-        gload(0, gb[0]);
+        constexpr int NB = MB2_DEPTH + 1;  // operand batches in flight + the one consumed
+        double2 gb[NB][NSEL];
+#pragma unroll
+        for (int st = 0; st < MB2_DEPTH; st++) gload(st, gb[st]);
 #endif
         __syncthreads();  // (h = 0: also the twist planes)
         const uint32_t f = fl + (uint32_t)R * SubFft::freq_slot(s);
@@ -931,7 +936,7 @@ __global__ void __launch_bounds__((MbPair2Cfg<N, G>::THREADS), 2) large_mb_pair2
         for (int st = 0; st < 8; st++) {
             const int lvl = L - (st >> 2), col = (st >> 1) & 1, r = st & 1;
             __builtin_amdgcn_sched_barrier(0);
-            if (st + 1 < 8) gload(st + 1, gb[(st + 1) & 1]);
+            if (st + MB2_DEPTH < 8) gload(st + MB2_DEPTH, gb[(st + MB2_DEPTH) % NB]);
             if (st % 4 == 0) {
 #pragma unroll
                 for (int c = 0; c < CPW; c++)
@@ -941,7 +946,7 @@ __global__ void __launch_bounds__((MbPair2Cfg<N, G>::THREADS), 2) large_mb_pair2
                         ff[c][rr] = cx{t.x, t.y};
                     }
             }
-            const double2 (&g)[NSEL] = gb[st & 1];
+            const double2 (&g)[NSEL] = gb[st % NB];
 #pragma unroll
             for (int c = 0; c < CPW; c++) {
                 double2 kb = g[0];
