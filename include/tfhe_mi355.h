@@ -54,8 +54,9 @@
  *     starting, so uploads are not starved under load); the serialized-key uploads hold the key
  *     lock from their first key write to the ready flag; a caller that fills the buffer of
  *     tfhe_mi355_bootstrap_key_fourier / _keyswitch_key_device itself owns that window (calls made
- *     before its _set_ready see whatever the buffer holds; on a multi-device context _set_ready
- *     also replicates the buffer to the other devices); _async calls are not ordered with
+ *     before its _set_ready see whatever the buffer holds; on a multi-device context the hand-out
+ *     marks that key not uploaded on every device, so batched calls fail until _set_ready, which
+ *     replicates the buffer to the other devices); _async calls are not ordered with
  *     uploads: do not re-upload a key while _async work that reads it may still run;
  *   - _async lut index arrays are not checked on the host (they live on the device): an entry
  *     >= lut_count is clamped to lut_count - 1 by the kernels (no out-of-bounds read); the
@@ -161,7 +162,11 @@ int tfhe_mi355_context_create(const TfheMi355Parameters *params, int device,
  *     pairs) go to the first device and are replicated from its memory: RCCL ncclBroadcast among
  *     the distinct devices (one rank per device, over xGMI; librccl is opened at run time), then
  *     device-to-device copies to further shards of the same device (TFHE_MI355_REPLICATE=copy:
- *     peer copies instead of RCCL); device-pointer key inputs live on the first device;
+ *     peer copies instead of RCCL; the default "auto" also falls back to peer copies when librccl
+ *     cannot be loaded or its communicator is refused); device-pointer key inputs live on the first
+ *     device.  Peer access is enabled between the distinct devices at creation.  A failed upload
+ *     or replication leaves that key part not uploaded on EVERY device;
+ *   - the calling thread's current HIP device is left as it was by every entry point;
  *   - batched host-pointer calls (PBS, KS, KS->PBS, PBS->KS, blind rotation, packing KS,
  *     GLWE products) are split into contiguous row shares, one per device, run concurrently and
  *     joined before the call returns; outputs are bit-identical to a single-device context;
@@ -172,6 +177,15 @@ int tfhe_mi355_context_create(const TfheMi355Parameters *params, int device,
  *   - kernel timing and coalescing statistics are summed over the devices. */
 int tfhe_mi355_context_create_devices(const TfheMi355Parameters *params, const int *devices, size_t device_count,
                                       TfheMi355Context **out_ctx);
+/* How the last key replication of a context ran: TFHE_MI355_REPLICATION_NONE (a single-device
+ * context, or nothing replicated yet), _RCCL (ncclBroadcast), _PEER_COPY (hipMemcpyPeerAsync between
+ * distinct devices), _DEVICE_COPY (one distinct device: device-to-device copies only).  `note`
+ * (optional, borrowed until the next upload) says why auto mode did not use RCCL, else "". */
+#define TFHE_MI355_REPLICATION_NONE 0
+#define TFHE_MI355_REPLICATION_RCCL 1
+#define TFHE_MI355_REPLICATION_PEER_COPY 2
+#define TFHE_MI355_REPLICATION_DEVICE_COPY 3
+int tfhe_mi355_context_replication(TfheMi355Context *ctx, int *mode, const char **note);
 /* Number of devices (shards) of a context: 1 for a single-device context. */
 int tfhe_mi355_context_devices(TfheMi355Context *ctx, size_t *count);
 /* The single-device context of shard `index` and its device ordinal (borrowed: owned and destroyed

@@ -189,3 +189,103 @@ def test_two_phase_fourier_upload_replicates_on_set_ready(orc, small_2_2):
     assert np.array_equal(multi.programmable_bootstrap(small, lut), single.programmable_bootstrap(small, lut))
     multi.close()
     single.close()
+
+
+def _hip_get_device():
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    d = ctypes.c_int(-1)
+    assert hip.hipGetDevice(ctypes.byref(d)) == 0
+    return d.value
+
+
+def test_caller_device_unchanged_and_replication_reported(orc, small_2_2, monkeypatch):
+    """Every entry point leaves the calling thread's current HIP device as it found it (create_devices,
+    uploads with replication, a batched split call, a coalesced call, destroy); the context reports
+    how the keys were replicated: device copies for {0, 0} in auto mode, the (forced) one-rank RCCL
+    broadcast with TFHE_MI355_REPLICATE=rccl."""
+    keys = small_2_2
+    p = keys.params
+    from tfhe_mi355 import Engine
+
+    before = _hip_get_device()
+    for mode, want in (("auto", "device_copy"), ("rccl", "rccl"), ("copy", "device_copy")):
+        monkeypatch.setenv("TFHE_MI355_REPLICATE", mode)
+        multi = Engine(p, devices=[0, 0])
+        assert _hip_get_device() == before
+        assert multi.replication() == ("none", "")
+        _upload((multi,), keys)
+        assert _hip_get_device() == before
+        assert multi.replication()[0] == want, mode
+        lut = orc.fill_accumulator(p.polynomial_size, 1, 4, 4, lambda x: x)
+        msgs, small = _cts(orc, keys, 40, 12)
+        got = multi.programmable_bootstrap(small, lut)
+        assert np.array_equal(decode(orc.lwe_decrypt(keys.glwe_sk, got), p.delta) % 16, msgs)
+        multi.programmable_bootstrap(small[:1], lut)
+        assert _hip_get_device() == before
+        multi.close()
+        assert _hip_get_device() == before
+    assert Engine(p, 0).replication() == ("none", "")
+
+
+def test_failed_replication_leaves_every_shard_not_uploaded(orc, small_2_2, monkeypatch):
+    """a key upload whose replication fails leaves the key part not uploaded on EVERY
+    shard (shard 0 included, though it holds the new key), so batched, split, coalesced and submitted
+    calls all fail with 'not uploaded' rather than succeeding only where they land on shard 0; a
+    later successful upload restores every shard."""
+    from tfhe_mi355._lib import EngineError
+
+    keys = small_2_2
+    p = keys.params
+    single, multi = _engines(p, [0, 0, 0])
+    _upload((single,), keys)
+    lut = orc.fill_accumulator(p.polynomial_size, 1, 4, 4, lambda x: x)
+    _, small = _cts(orc, keys, 64, 13)
+    monkeypatch.setenv("TFHE_MI355_REPLICATE", "fail")
+    with pytest.raises(EngineError, match="test hook"):
+        multi.upload_bootstrap_key(keys.bsk)
+    with pytest.raises(EngineError, match="not uploaded"):
+        multi.programmable_bootstrap(small, lut)  # split over the shards
+    for i in range(3):  # round robin: every shard's coalescer refuses
+        with pytest.raises(EngineError, match="not uploaded"):
+            multi.programmable_bootstrap(small[i:i + 1], lut)
+        with pytest.raises(EngineError, match="not uploaded"):
+            multi.submit("pbs", small[i:i + 1], lut).wait()
+    monkeypatch.setenv("TFHE_MI355_REPLICATE", "auto")
+    multi.upload_bootstrap_key(keys.bsk)
+    assert np.array_equal(multi.programmable_bootstrap(small, lut), single.programmable_bootstrap(small, lut))
+    for i in range(3):
+        assert np.array_equal(multi.programmable_bootstrap(small[i:i + 1], lut)[0],
+                              single.programmable_bootstrap(small[i:i + 1], lut)[0])
+    multi.close()
+    single.close()
+
+
+def test_key_buffer_hand_out_marks_every_shard_not_ready(orc, small_2_2):
+    """handing out the first device's key buffer (bootstrap_key_fourier /
+    keyswitch_key_device) on a multi-device context marks that key part not uploaded everywhere until
+    _set_ready replicates the rewritten buffer; the other key part is unaffected."""
+    from tfhe_mi355._lib import EngineError
+
+    keys = small_2_2
+    p = keys.params
+    single, multi = _engines(p, [0, 0])
+    _upload((single, multi), keys)
+    lut = orc.fill_accumulator(p.polynomial_size, 1, 4, 4, lambda x: (x + 1) % 16)
+    _, small = _cts(orc, keys, 50, 14)
+    _, big = _cts(orc, keys, 50, 15, big=True)
+    multi.fourier_bootstrap_key()
+    with pytest.raises(EngineError, match="not uploaded"):
+        multi.programmable_bootstrap(small, lut)
+    assert np.array_equal(multi.keyswitch(big), single.keyswitch(big))  # the KSK still serves
+    multi.fourier_bootstrap_key_set_ready()  # the buffer was not changed: the old key, replicated
+    assert np.array_equal(multi.programmable_bootstrap(small, lut), single.programmable_bootstrap(small, lut))
+    multi.keyswitch_key_device()
+    with pytest.raises(EngineError, match="not uploaded"):
+        multi.keyswitch(big)
+    multi.keyswitch_key_set_ready()
+    assert np.array_equal(multi.keyswitch_programmable_bootstrap(big, lut),
+                          single.keyswitch_programmable_bootstrap(big, lut))
+    multi.close()
+    single.close()

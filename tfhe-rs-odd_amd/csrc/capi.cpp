@@ -14,6 +14,8 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <atomic>
@@ -48,8 +50,25 @@ void check(hipError_t e, const char *what) {
     if (e != hipSuccess) fail("%s: %s", what, hipGetErrorString(e));
 }
 
+// The calling thread's current HIP device is the caller's (a Rust or C caller may use HIP itself):
+// every entry point that selects another device puts the caller's back before it returns, success
+// or failure.  A thread without a device (no GPU, or HIP not initialised) keeps none.
+struct CallerDevice {
+    int d = -1;
+    CallerDevice() {
+        if (hipGetDevice(&d) != hipSuccess) d = -1;
+    }
+    ~CallerDevice() {
+        int now = -1;
+        if (d >= 0 && (hipGetDevice(&now) != hipSuccess || now != d)) (void)hipSetDevice(d);
+    }
+    CallerDevice(const CallerDevice &) = delete;
+    CallerDevice &operator=(const CallerDevice &) = delete;
+};
+
 template <class F>
 int guarded(F &&f) {
+    CallerDevice keep;
     try {
         f();
         last_error_text().clear();
@@ -142,6 +161,46 @@ struct CoalescedReq {
 
 struct RcclComms;  // communicator over a multi-device context's distinct devices (key replication)
 
+// Worker threads of a multi-device context, one per shard after the first, started with the context
+// and joined by its destroy: a batched host-pointer call hands each of them its shard's row share
+// (split_rows) instead of starting threads per call.  Each worker runs its queue in
+// order; concurrent calls queue behind each other per shard, as they would on the shard's lock.
+struct ShardWorker {
+    std::mutex m;
+    std::condition_variable cv;
+    std::deque<std::function<void()>> q;
+    bool stop = false;
+    std::thread t;
+    void post(std::function<void()> f) {
+        {
+            std::lock_guard<std::mutex> g(m);
+            q.push_back(std::move(f));
+        }
+        cv.notify_one();
+    }
+    void loop() {
+        for (;;) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> g(m);
+                cv.wait(g, [&] { return stop || !q.empty(); });
+                if (q.empty()) return;  // stop with nothing queued
+                f = std::move(q.front());
+                q.pop_front();
+            }
+            f();
+        }
+    }
+    ~ShardWorker() {
+        {
+            std::lock_guard<std::mutex> g(m);
+            stop = true;
+        }
+        cv.notify_one();
+        if (t.joinable()) t.join();
+    }
+};
+
 struct TfheMi355Context {
     TfheMi355Parameters p{};
     int device = 0;
@@ -161,7 +220,10 @@ struct TfheMi355Context {
     // Every entry point of a multi-device context dispatches to them (see "multi-device").
     std::vector<TfheMi355Context *> shards;
     std::atomic<size_t> next_shard{0};  // round robin of coalesced calls and submits
+    std::vector<std::unique_ptr<ShardWorker>> workers;  // shards 1.. (split_rows)
+    int replication = 0;  // how the last key replication ran (tfhe_mi355_context_replication)
     RcclComms *rccl = nullptr;
+    std::string replicate_note;  // why the last replication did not use RCCL in auto mode (empty: it did, or no need)
     TfheMi355Context *owner = nullptr;  // a shard: its multi-device context (destroyed with it)
     bool multi() const { return !shards.empty(); }
     hipStream_t stream = nullptr;
@@ -275,6 +337,7 @@ struct KeyWrite {
 struct KeyRead {
     std::shared_lock<std::shared_mutex> k;
     explicit KeyRead(TfheMi355Context *c) {
+        if (std::find(tl_key_writes.begin(), tl_key_writes.end(), c) != tl_key_writes.end()) return;
         while (c->key_writers.load(std::memory_order_acquire) > 0)
             std::this_thread::sleep_for(std::chrono::microseconds(20));
         k = std::shared_lock<std::shared_mutex>(c->keys_mu);
@@ -1211,7 +1274,7 @@ RcclComms &rccl_for(TfheMi355Context *m, const std::vector<int> &devices) {
     return *m->rccl;
 }
 
-// TFHE_MI355_REPLICATE: "auto" (default), "rccl", "copy"
+// TFHE_MI355_REPLICATE: "auto" (default), "rccl", "copy" ("fail": a replication failure, test hook)
 std::string replicate_mode() {
     const char *e = std::getenv("TFHE_MI355_REPLICATE");
     return e && *e ? std::string(e) : std::string("auto");
@@ -1247,7 +1310,20 @@ void replicate(TfheMi355Context *m, KeyPart part) {
     std::vector<size_t> holder(devs.size());
     for (size_t r = 0; r < devs.size(); r++) holder[r] = r == 0 && on[0].size() > 1 ? on[0][1] : on[r][0];
     const std::string mode = replicate_mode();
-    const bool use_rccl = mode == "rccl" || (mode != "copy" && devs.size() > 1);
+    m->replicate_note.clear();
+    if (mode == "fail") fail("key replication failed (TFHE_MI355_REPLICATE=fail test hook)");
+    bool use_rccl = mode == "rccl" || (mode != "copy" && devs.size() > 1);
+    RcclComms *rcp = nullptr;
+    if (use_rccl) {
+        try {
+            rcp = &rccl_for(m, devs);
+        } catch (const Failure &e) {
+            if (mode == "rccl") throw;
+            // auto: librccl missing or its communicator refused -> the peer-copy path
+            m->replicate_note = std::string("RCCL unavailable, peer copies: ") + e.what();
+            use_rccl = false;
+        }
+    }
     auto sync_all = [&] {
         for (auto *s : S) {
             check(hipSetDevice(s->device), "hipSetDevice");
@@ -1256,8 +1332,10 @@ void replicate(TfheMi355Context *m, KeyPart part) {
     };
     check(hipSetDevice(src->device), "hipSetDevice");
     check(hipStreamSynchronize(src->stream), "key source sync");
+    m->replication = use_rccl ? TFHE_MI355_REPLICATION_RCCL
+                     : devs.size() > 1 ? TFHE_MI355_REPLICATION_PEER_COPY : TFHE_MI355_REPLICATION_DEVICE_COPY;
     if (use_rccl) {
-        RcclComms &rc = rccl_for(m, devs);
+        RcclComms &rc = *rcp;
         check_nccl(rc, rc.group_start(), "ncclGroupStart");
         for (size_t r = 0; r < devs.size(); r++) {
             check(hipSetDevice(devs[r]), "hipSetDevice");
@@ -1326,21 +1404,60 @@ void set_ready_all(TfheMi355Context *m, KeyPart part, bool ready) {
 // a batched host-pointer call of a multi-device context: shard i runs rows [count i / S, count (i+1)
 // / S) through `f(shard, first, count)` (an entry point of the shard, 0 = ok), shard 0 on the calling
 // thread and the others on threads of their own; joined, then the first failure is reported
+// The whole call holds the multi-device context's key lock shared, so a concurrent key upload
+// (key_write_all: this context exclusively first) lands before or after it, never between two
+// shards' shares.
 template <class F>
 void split_rows(TfheMi355Context *m, size_t count, F &&f) {
     const size_t S = m->shards.size();
+    KeyRead keys(m);
     std::vector<std::string> errs(S);
     auto run = [&](size_t i) {
         const size_t a = count * i / S, b = count * (i + 1) / S;
         if (a == b) return;
-        if (f(m->shards[i], a, b - a) != TFHE_MI355_OK) errs[i] = tfhe_mi355_last_error();
+        try {
+            if (f(m->shards[i], a, b - a) != TFHE_MI355_OK) errs[i] = tfhe_mi355_last_error();
+        } catch (const std::exception &e) {
+            errs[i] = e.what();
+        }
     };
-    std::vector<std::thread> th;
-    for (size_t i = 1; i < S; i++) th.emplace_back(run, i);
+    std::mutex dm;
+    std::condition_variable dcv;
+    size_t left = 0;
+    for (size_t i = 1; i < S; i++) {
+        if (count * i / S == count * (i + 1) / S) continue;
+        left++;
+        m->workers[i - 1]->post([&, i] {
+            run(i);
+            std::lock_guard<std::mutex> g(dm);
+            if (--left == 0) dcv.notify_one();
+        });
+    }
     run(0);
-    for (auto &t : th) t.join();
+    {
+        std::unique_lock<std::mutex> g(dm);
+        dcv.wait(g, [&] { return left == 0; });
+    }
     for (size_t i = 0; i < S; i++)
         if (!errs[i].empty()) fail("device %d (shard %zu): %s", m->shards[i]->device, i, errs[i].c_str());
+}
+
+// peer access between every two distinct devices of a multi-device context, so that the peer-copy
+// replication (TFHE_MI355_REPLICATE=copy, or auto without RCCL) is a direct xGMI copy rather than
+// a staged one; a pair the platform cannot map keeps the staged path (not an error)
+void enable_peer_access(const std::vector<int> &devs) {
+    std::vector<int> d = devs;
+    std::sort(d.begin(), d.end());
+    d.erase(std::unique(d.begin(), d.end()), d.end());
+    for (int a : d)
+        for (int b : d) {
+            if (a == b) continue;
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) continue;
+            if (hipSetDevice(a) != hipSuccess) continue;
+            (void)hipDeviceEnablePeerAccess(b, 0);  // hipErrorPeerAccessAlreadyEnabled is fine too
+            (void)hipGetLastError();                 // ... and leaves its code behind
+        }
 }
 
 // parameter checks shared by the single- and multi-device constructors
@@ -1599,11 +1716,16 @@ int tfhe_mi355_context_create_devices(const TfheMi355Parameters *params, const i
                 m->shards.push_back(create_single(*params, d));
                 m->shards.back()->owner = m;
             }
+            for (size_t i = 1; i < devs.size(); i++) {
+                m->workers.emplace_back(new ShardWorker());
+                ShardWorker *w = m->workers.back().get();
+                w->t = std::thread([w] { w->loop(); });
+            }
+            enable_peer_access(devs);
         } catch (...) {
             tfhe_mi355_context_destroy(m);
             throw;
         }
-        check(hipSetDevice(devs[0]), "hipSetDevice");
         *out_ctx = m;
     });
 }
@@ -1612,6 +1734,14 @@ int tfhe_mi355_context_devices(TfheMi355Context *ctx, size_t *count) {
     return guarded([&] {
         if (!ctx || !count) fail("null argument");
         *count = ctx->multi() ? ctx->shards.size() : 1;
+    });
+}
+
+int tfhe_mi355_context_replication(TfheMi355Context *ctx, int *mode, const char **note) {
+    return guarded([&] {
+        if (!ctx || !mode) fail("null argument");
+        *mode = ctx->multi() ? ctx->replication : TFHE_MI355_REPLICATION_NONE;
+        if (note) *note = ctx->replicate_note.c_str();
     });
 }
 
@@ -1634,6 +1764,7 @@ int tfhe_mi355_context_destroy(TfheMi355Context *ctx) {
         if (!ctx) return;
         if (ctx->owner) fail("this context belongs to a multi-device context: destroy that one");
         if (ctx->multi()) {  // every shard (each reports its own queued requests), then the communicator
+            ctx->workers.clear();  // joins the shard workers (a split call still running finishes first)
             std::string errs;
             for (auto *s : ctx->shards) {
                 s->owner = nullptr;
@@ -1716,8 +1847,13 @@ template <class F>
 void multi_key_upload(TfheMi355Context *m, KeyPart part, F &&first) {
     auto w = key_write_all(m);
     set_ready_all(m, part, false);
-    abi(first(m->shards[0]));
-    replicate(m, part);
+    try {
+        abi(first(m->shards[0]));
+        replicate(m, part);
+    } catch (...) {  // the first shard may hold the new key already: no shard serves a half-replicated one
+        set_ready_all(m, part, false);
+        throw;
+    }
     set_ready_all(m, part, true);
 }
 }  // namespace
@@ -1880,6 +2016,9 @@ int tfhe_mi355_bootstrap_key_fourier(TfheMi355Context *ctx, void **d_ptr, size_t
         if (ctx->multi()) {  // the first device's buffer; _set_ready replicates it to the others
             auto w = key_write_all(ctx);
             abi(tfhe_mi355_bootstrap_key_fourier(ctx->shards[0], d_ptr, bytes));
+            // the caller now rewrites shard 0's copy: no device serves this key part until _set_ready
+            // (batches fail cleanly instead of mixing a half-written key with the old replicas)
+            set_ready_all(ctx, KeyPart::Fourier, false);
             return;
         }
         KeyWrite kw(ctx);  // no coalesced batch in flight, none starts until done
@@ -1951,6 +2090,9 @@ int tfhe_mi355_keyswitch_key_device(TfheMi355Context *ctx, void **d_ptr, size_t 
         if (ctx->multi()) {  // the first device's buffer; _set_ready replicates it to the others
             auto w = key_write_all(ctx);
             abi(tfhe_mi355_keyswitch_key_device(ctx->shards[0], d_ptr, bytes));
+            // the caller now rewrites shard 0's copy: no device serves this key part until _set_ready
+            // (batches fail cleanly instead of mixing a half-written key with the old replicas)
+            set_ready_all(ctx, KeyPart::Ksk, false);
             return;
         }
         KeyWrite kw(ctx);  // no coalesced batch in flight, none starts until done

@@ -213,6 +213,23 @@ __device__ __forceinline__ cx lds_ldx(const cx *xb, int p) {
 //   p = lane + 64 c        : ((X + 16 lane) ^ 16 c) + 1024 c   (one v_xor; 1024 c is the ds offset)
 //   p = 64 cc + a1 + 4 b   : (X + 1024 cc + 16 (a1 ^ cc)) ^ 64 b (one v_xor)
 // since X has no bits in 4..9 and (a1 + 4 b) ^ cc = (a1 ^ cc) ^ 4 b (a1 < 4).
+// Sync types may carry `static constexpr int launder` (WaveLocalSyncL, pbs_common.h): bit 1
+// recomputes the lane base la, bit 2 the stage-2 base qa, at every transform, so that their 15
+// XOR images are not hoisted out of the caller's loop (where a kernel at its register limit
+// spills them).  Same addresses, same values.
+template <class S, class = void>
+struct SyncLaunder {
+    static constexpr int value = 0;
+};
+template <class S>
+struct SyncLaunder<S, decltype((void)S::launder)> {
+    static constexpr int value = S::launder;
+};
+template <class S, int Bit>
+__device__ __forceinline__ uint32_t launder_addr(uint32_t a) {
+    if constexpr ((SyncLaunder<S>::value & Bit) != 0) asm volatile("" : "+v"(a));
+    return a;
+}
 typedef double lds_d2v __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) lds_d2v lds_d2;
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
@@ -367,12 +384,12 @@ struct WaveFft<1024> {
         sync();  // previous readers of xb done
         const int cc = lane & 15, a1 = lane >> 4;
         if constexpr (TM_XCHG_XOR) {
-            const uint32_t xa = lds_addr(xb), la = xa + 16u * lane;
+            const uint32_t xa = lds_addr(xb), la = launder_addr<Sync, 1>(xa + 16u * lane);
 #pragma unroll
             for (int c = 0; c < 16; c++) lds_st_at((la ^ (16u * c)) + 1024u * c, v[c]);
             sync();
             // stage 2: blocks of 64 (cc), R=16, m=4 (a1 = row)
-            const uint32_t qa = xa + 1024u * cc + 16u * (a1 ^ cc);
+            const uint32_t qa = launder_addr<Sync, 2>(xa + 1024u * cc + 16u * (a1 ^ cc));
 #pragma unroll
             for (int b = 0; b < 16; b++) v[b] = lds_ld_at(qa ^ (64u * b));
         } else {
@@ -430,11 +447,11 @@ struct WaveFft<1024> {
         sync();  // previous readers of xb done
         if constexpr (TM_XCHG_XOR) {
             const uint32_t xa = lds_addr(xb);
-            const uint32_t qa = xa + 1024u * cc + 16u * (a1 ^ cc);
+            const uint32_t qa = launder_addr<Sync, 2>(xa + 1024u * cc + 16u * (a1 ^ cc));
 #pragma unroll
             for (int b = 0; b < 16; b++) lds_st_at(qa ^ (64u * b), v[b]);
             sync();
-            const uint32_t la = xa + 16u * lane;
+            const uint32_t la = launder_addr<Sync, 1>(xa + 16u * lane);
             v[0] = lds_ld_at(la);
 #pragma unroll
             for (int c = 1; c < 16; c++) {

@@ -74,6 +74,14 @@ struct WaveLocalSync {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 };
+// The same sync, telling WaveFft<1024> to recompute its exchange addresses at every call
+// (SyncLaunder, fft_device.h) instead of letting them be hoisted out of the caller's loop: for
+// kernels at the 256-VGPR limit, where the 32 hoisted XOR addresses were spilled to scratch
+// inside the CMUX loop (onchip_cmux_kernel<N, D32, 2>).
+template <int Bits>
+struct WaveLocalSyncL : WaveLocalSync {
+    static constexpr int launder = Bits;
+};
 
 // Sync among the (k+1) waves of one ciphertext through LDS flags instead of s_barrier, so the
 // ciphertexts sharing a workgroup (and a CU) are not forced into lockstep: their LDS bursts and

@@ -1687,6 +1687,18 @@ __global__ void __launch_bounds__(1024) split_inv_digits_kernel(LargePbsLaunch a
 #ifndef ONCHIP_QROT
 #define ONCHIP_QROT 1  // wave pair -> sub-block rotated per workgroup (0: pair p on sub-block p)
 #endif
+// L = 2: WaveFft exchange bases recomputed per transform (bit 1 la, bit 2 qa).  Hoisted out of the
+// CMUX loop, their 32 XOR images were spilled to scratch inside it (<8192, true, 2>: 132 B private,
+// 15 scratch stores + 33 loads per CMUX, vmcnt(0) waits on the GGSW prefetch; <4096, true, 2>: 84 B).
+// The bits per N are the smallest that leave every L = 2 instantiation with no private segment
+// (8192: 3 -> 246 VGPRs, +66 VALU per CMUX; 4096: 1 -> 249-253 VGPRs, +21 VALU; 4096 with both bits
+// spilled again in the 64-bit-digit instantiation)
+#ifndef ONCHIP_LAUNDER_8192
+#define ONCHIP_LAUNDER_8192 3
+#endif
+#ifndef ONCHIP_LAUNDER_4096
+#define ONCHIP_LAUNDER_4096 1
+#endif
 #ifndef ONCHIP_4096_CPW
 #define ONCHIP_4096_CPW 1  // N = 4096: 1 = one ciphertext per 256-thread workgroup (two workgroups per CU,
                            // independent barriers); 2 = two ciphertexts per 512-thread workgroup
@@ -1845,7 +1857,7 @@ __global__ void __launch_bounds__(OnchipCfg<N>::THREADS, OnchipCfg<N>::MIN_WPS /
     const SubFft::Lds tw{s1, s1};
     cx *xb = reinterpret_cast<cx *>(lds) + wbuf * BUF;
     double2 *own = lds + wbuf * BUF;
-    WaveLocalSync wsync;
+    WaveLocalSyncL<L == 2 ? (N == 8192 ? ONCHIP_LAUNDER_8192 : ONCHIP_LAUNDER_4096) : 0> wsync;
     const uint64_t *in = a.lwe_in + (size_t)ct * (a.n + 1);
     // twist and top-stage twiddles through buffer loads: one VGPR offset, the rest in SGPRs
     const __amdgpu_buffer_rsrc_t rtw = make_rsrc(a.twist), rwt = make_rsrc(a.wtop);

@@ -60,6 +60,7 @@ SIGNATURES = [
     ("tfhe_mi355_context_create_devices", ctypes.c_int,
      [ctypes.POINTER(TfheMi355Parameters), ctypes.POINTER(ctypes.c_int), sz, ctypes.POINTER(vp)]),
     ("tfhe_mi355_context_devices", ctypes.c_int, [vp, ctypes.POINTER(sz)]),
+    ("tfhe_mi355_context_replication", ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_char_p)]),
     ("tfhe_mi355_context_device_context", ctypes.c_int, [vp, sz, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int)]),
     ("tfhe_mi355_context_destroy", ctypes.c_int, [vp]),
     ("tfhe_mi355_bootstrap_key_upload", ctypes.c_int, [vp, u64p, sz]),

@@ -93,8 +93,13 @@ class Engine:
             _lib.call("tfhe_mi355_context_create_devices", ctypes.byref(self._cp), arr, len(devices),
                       ctypes.byref(h))
         self._h = h
-        if devices is not None:
-            self.device = self.device_ordinals()[0]
+        self.devices = self.device_ordinals() if devices is not None else [device]
+        self.device = self.devices[0]
+
+    @property
+    def multi_device(self) -> bool:
+        """True for a context over several shards (tfhe_mi355_context_create_devices with > 1 entry)."""
+        return len(self.devices) > 1
 
     def device_ordinals(self) -> list:
         """Device ordinal of each shard (one entry for a single-device context)."""
@@ -106,6 +111,15 @@ class Engine:
             _lib.call("tfhe_mi355_context_device_context", self._h, i, ctypes.byref(sub), ctypes.byref(dev))
             out.append(dev.value)
         return out
+
+    REPLICATION = {0: "none", 1: "rccl", 2: "peer_copy", 3: "device_copy"}
+
+    def replication(self):
+        """How the last key replication ran ('none' | 'rccl' | 'peer_copy' | 'device_copy') and why auto
+        mode did not use RCCL ('' when it did or had no need)."""
+        mode, note = ctypes.c_int(), ctypes.c_char_p()
+        _lib.call("tfhe_mi355_context_replication", self._h, ctypes.byref(mode), ctypes.byref(note))
+        return self.REPLICATION.get(mode.value, str(mode.value)), (note.value or b"").decode()
 
     # -- lifetime ---------------------------------------------------------------------
     def close(self):

@@ -109,9 +109,13 @@ class _PbsLayer:
 
 
 def _is_gpu_engine(engine) -> bool:
+    """A single-device GPU engine: radix batches stay in its HBM between layers (_DeviceOps).  A
+    multi-device context (Engine(devices=[...])) takes the host path instead: every layer is ONE
+    host-pointer KS+PBS call, which the context splits over its devices -- the reference's one
+    process with its rayon pool (radix_parallel/mul.rs:347-407) on the one-process drop-in."""
     from .engine import Engine
 
-    return isinstance(engine, Engine)
+    return isinstance(engine, Engine) and not engine.multi_device
 
 
 class _HostOps:
