@@ -195,7 +195,7 @@ def pbs_flops(p) -> float:
 
 
 PMC_ALIAS = {"mul32": "2_2ks"}  # the multiply DAG runs the 2_2 KS+PBS kernels: per-PBS traffic of that workload
-PMC_ROUNDS = ("r05", "r04", "r03")  # newest committed PMC summary first (kernels unchanged since are still described by it)
+PMC_ROUNDS = ("r06", "r05", "r04", "r03")  # newest committed PMC summary first (kernels unchanged since are still described by it)
 
 # dominant kernel of each workload: (kernel-timer family, rocprofv3 name normalised as
 # scripts/pmc_workload.py does).  Its average duration comes from the engine's HIP-event timer
@@ -570,6 +570,8 @@ def summarize(line: dict) -> dict:
     cs = callers_summary(line.get("host_abi"))
     if cs:
         out["callers"] = cs
+    if "ctx_devices" in line:
+        out["ctx_devices"] = line["ctx_devices"]
     return out
 
 
@@ -624,6 +626,69 @@ def other_workloads(args) -> dict:
             res[name] = {"error": f"timeout after {budget:.0f} s"}
         res[name]["wall_s"] = time.perf_counter() - t
         print(f"bench.py: {name} done in {res[name]['wall_s']:.1f} s", file=sys.stderr, flush=True)
+    # the one-process multi-device context on this GPU listed twice (its split / replication overhead)
+    cmd = [sys.executable, os.path.abspath(__file__), "--ctx-devices", "0,0", "--steps", "3", "--warmup", "1",
+           "--seed", str(args.seed)]
+    t = time.perf_counter()
+    try:
+        cp = subprocess.run(cmd, capture_output=True, text=True, timeout=workload_budget())
+        lines = [l for l in cp.stdout.splitlines() if l.startswith("{")]
+        res["ctx_devices"] = (summarize(json.loads(lines[-1])) if cp.returncode == 0 and lines
+                              else {"error": f"rc={cp.returncode}: {cp.stderr.strip()[-300:]}"})
+    except subprocess.TimeoutExpired:
+        res["ctx_devices"] = {"error": f"timeout after {workload_budget():.0f} s"}
+    res["ctx_devices"]["wall_s"] = time.perf_counter() - t
+    print(f"bench.py: ctx_devices done in {res['ctx_devices']['wall_s']:.1f} s", file=sys.stderr, flush=True)
+    return res
+
+
+def ctx_devices_ranks(args, R, emit=None) -> dict:
+    """N > 1: after every per-rank workload, rank 0 alone runs the one-process multi-device context
+    over all the job's devices (ctx_devices_line) while the other ranks wait on the process group's
+    key-value store (no collective kernel spinning on their GPUs meanwhile).  Under the same per-rank
+    watchdog as the other entries; an error is reported in the entry, not fatal."""
+    import datetime
+    import threading
+
+    R.barrier()
+    budget = workload_budget()
+    res = {}
+    store = None
+    try:
+        store = R.dist.distributed_c10d._get_default_store()
+    except Exception:
+        store = None
+    t = time.perf_counter()
+    if R.rank == 0:
+        def over_budget():
+            res["ctx_devices"] = {"error": f"over its {budget:.0f} s budget (watchdog)", "wall_s": time.perf_counter() - t}
+            if emit is not None:
+                emit(res)
+            sys.stdout.flush()
+            os._exit(3)
+
+        dog = threading.Timer(budget, over_budget)
+        dog.daemon = True
+        dog.start()
+        try:
+            import torch
+
+            visible = max(1, torch.cuda.device_count())
+            devs = [d % visible for d in range(R.world)]  # a rehearsal with fewer GPUs lists a device twice
+            a = argparse.Namespace(**vars(args))
+            a.steps, a.warmup = 3, 1
+            res["ctx_devices"] = summarize(ctx_devices_line(a, devs))
+        except Exception as ex:  # reported, not fatal
+            res["ctx_devices"] = {"error": repr(ex)[:300]}
+        finally:
+            dog.cancel()
+        res["ctx_devices"]["wall_s"] = time.perf_counter() - t
+        print(f"bench.py: ctx_devices done in {res['ctx_devices']['wall_s']:.1f} s", file=sys.stderr, flush=True)
+        if store is not None:
+            store.set("bench_ctx_devices_done", "1")
+    elif store is not None:
+        store.wait(["bench_ctx_devices_done"], datetime.timedelta(seconds=budget + 60))
+    R.barrier()
     return res
 
 
@@ -841,7 +906,13 @@ def main():
                     help="total ciphertexts over all ranks (split into contiguous shards: strong scaling)")
     ap.add_argument("--warmup-batch", type=int, default=0,
                     help="warm-up launches use only the first N ciphertexts of the rank's batch")
+    ap.add_argument("--ctx-devices", default=None, metavar="LIST",
+                    help="only the one-process multi-device context entry over the comma-separated device "
+                         "list (the default run adds it: devices 0,0 at N = 1, 0..N-1 at N > 1)")
     args = ap.parse_args()
+    if args.ctx_devices:
+        print(json.dumps(ctx_devices_line(args, [int(d) for d in args.ctx_devices.split(",")])), flush=True)
+        return
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
@@ -875,6 +946,10 @@ def main():
         line = merge_other(line, other_workloads_ranks(args, R, lambda a: run_workload(a, R),
                                                        emit=lambda res: print(json.dumps(merge_other(line, res)),
                                                                               flush=True)))
+        prev = dict((line or {}).get("other_workloads") or {})
+        ctx = ctx_devices_ranks(args, R, emit=lambda res: print(json.dumps(merge_other(line, {**prev, **res})),
+                                                                flush=True))
+        line = merge_other(line, {**prev, **ctx})
     if R.rank == 0:
         if default_run:
             line["summary"] = compact_summary(line)
@@ -1087,6 +1162,130 @@ def single_ct_rates(eng, cts, acc, with_ks: bool, batched_rate: float, secs: flo
                    "compared with a batched call's row; T callers cannot exceed T / latency (little_bound); "
                    "the batched device rate is the headline step's")
     return res
+
+
+CTX_DEVICES_PAIRS = 32  # FheUint32 pairs per shard of the ctx_devices entry (host radix batches)
+
+
+def ctx_devices_line(args, devices: list) -> dict:
+    """The one-process multi-device drop-in (tfhe_mi355_context_create_devices):
+    ONE context over `devices`, driven the way a Rust caller drives it -- through the host-pointer C
+    ABI, with no torch in the data path.  The reference is one process whose rayon workers call
+    KS+PBS per block (shortint/engine/mod.rs:23-25, radix_parallel/mul.rs:347-407 ->
+    shortint/server_key/mod.rs:783-857).  2_2 keys are uploaded once (the first device converts the
+    BSK; the others receive it by ncclBroadcast over xGMI, or by device copies when a device repeats),
+    then
+      * `value`: classic 2_2 PBS over 4096 x S rows per call (S = shards), page-locked caller buffers
+        (tfhe_mi355_host_alloc), split into contiguous shares run concurrently -- PCIe-inclusive;
+      * `mul32`: BASELINE config 4 with CTX_DEVICES_PAIRS x S FheUint32 pairs through the integer
+        DAG's host path (each layer ONE host-pointer KS+PBS call split over the shards);
+      * sampled rows (each shard boundary, both ends) and sampled products compared bit for bit with
+        a single-device context, every output decrypted."""
+    from tfhe_mi355 import Engine, client, fill_accumulator, integer, pinned_empty, shortint
+    from tfhe_mi355.parameters import ALL
+
+    P = ALL["PARAM_MESSAGE_2_CARRY_2_KS_PBS"]
+    S = len(devices)
+    ck = shortint.ClientKey(P, args.seed)
+    t = time.perf_counter()
+    bsk = client.gen_bootstrap_key(args.seed + 100, ck.small_lwe_secret_key, ck.glwe_secret_key, P.glwe_dimension,
+                                   P.polynomial_size, P.pbs_base_log, P.pbs_level, P.glwe_modular_std_dev)
+    ksk = client.gen_keyswitch_key(args.seed + 200, ck.large_lwe_secret_key, ck.small_lwe_secret_key,
+                                   P.ks_base_log, P.ks_level, P.lwe_modular_std_dev)
+    t_gen = time.perf_counter() - t
+    single = Engine(P, devices[0])
+    t = time.perf_counter()
+    single.upload_bootstrap_key(bsk)
+    single.upload_keyswitch_key(ksk)
+    t_single = time.perf_counter() - t
+    t = time.perf_counter()
+    multi = Engine(P, devices=devices)
+    t_create = time.perf_counter() - t
+    t = time.perf_counter()
+    multi.upload_bootstrap_key(bsk)
+    t_bsk = time.perf_counter() - t
+    t = time.perf_counter()
+    multi.upload_keyswitch_key(ksk)
+    t_ksk = time.perf_counter() - t
+    mode, note = multi.replication()
+
+    # classic PBS through the host-pointer ABI, split over the shards
+    B = 4096 * S
+    msgs = np.random.default_rng(args.seed).integers(0, 16, B).astype(np.uint64)
+    cts = client.lwe_encrypt(args.seed * 1000, ck.small_lwe_secret_key, msgs * np.uint64(P.delta),
+                             P.lwe_modular_std_dev)
+    acc = fill_accumulator(P, lambda x: x)
+    p_in = pinned_empty(cts.shape)
+    p_in[...] = cts
+    p_out = pinned_empty((B, P.big_lwe_dimension + 1))
+    for _ in range(max(1, args.warmup)):
+        multi.programmable_bootstrap(p_in, acc, out=p_out)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        multi.programmable_bootstrap(p_in, acc, out=p_out)
+    wall = time.perf_counter() - t0
+    out = np.array(p_out)
+    dec = client.decode(client.lwe_decrypt(ck.glwe_secret_key, out), P.delta) % np.uint64(16)
+    ok = int(np.count_nonzero(dec == msgs))
+    bounds = sorted({min(max(B * i // S + d, 0), B - 1) for i in range(S + 1) for d in range(-16, 16)})
+    idx = np.asarray(bounds)
+    same = bool(np.array_equal(single.programmable_bootstrap(np.ascontiguousarray(cts[idx]), acc), out[idx]))
+
+    # FheUint32 multiplies: the integer DAG over the multi-device context (host radix batches)
+    K = CTX_DEVICES_PAIRS * S
+    sks_m = integer.ServerKey(shortint.ServerKey(None, engine=multi, parameters=P))
+    cks = integer.ClientKey(ck, 16)
+    rng = np.random.default_rng(args.seed + 7)
+    a = rng.integers(0, 2 ** 32, K, dtype=np.uint64)
+    b = rng.integers(0, 2 ** 32, K, dtype=np.uint64)
+    ca, cb = cks.encrypt(a), cks.encrypt(b)
+    prod = sks_m.mul_parallelized(ca, cb)   # warm-up (LUT caches)
+    t0 = time.perf_counter()
+    msteps = max(1, min(args.steps, 2))
+    for _ in range(msteps):
+        prod = sks_m.mul_parallelized(ca, cb)
+    mwall = time.perf_counter() - t0
+    mok = int(np.count_nonzero(cks.decrypt(prod) == (a * b) % np.uint64(1 << 32)))
+    sks_s = integer.ServerKey(shortint.ServerKey(None, engine=single, parameters=P))
+    pick = [0, 1, K // 2, K - 1]
+    ref = sks_s.mul_parallelized(sks_s.to_device(RadixSlice(_radix_rows(ca, pick), len(pick))),
+                                 sks_s.to_device(RadixSlice(_radix_rows(cb, pick), len(pick))))
+    msame = bool(np.array_equal(sks_s.to_host(ref).data, prod.data[pick]))
+    multi.close()
+    single.close()
+    return {
+        "metric": "programmable bootstraps/sec through ONE multi-device context (tfhe_mi355_context_create_devices), "
+                  "host-pointer C ABI, PARAM_MESSAGE_2_CARRY_2",
+        "value": B * args.steps / wall, "unit": "PBS/s", "n_gpus": len(set(devices)), "steps": args.steps,
+        "warmup": max(1, args.warmup), "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (seeded LWE encryptions of uniform messages)",
+        "config": {"workload": (f"one context over devices {devices}: 2_2 PBS of 4096 x {S} rows per host-pointer call "
+                                f"(page-locked buffers, PCIe-inclusive), and {K} FheUint32 multiplies per step "
+                                "through the integer DAG's host path"),
+                   "global_batch": B, "devices": devices, "shards": S},
+        "check": {"decrypted_ok": ok, "of": B, "sampled_rows_equal_single_device": same,
+                  "sampled_rows": len(bounds)},
+        "setup": {"keygen_s": t_gen, "context_create_s": t_create, "bsk_upload_replicate_s": t_bsk,
+                  "ksk_upload_replicate_s": t_ksk, "single_device_upload_s": t_single,
+                  "replication": mode, "replication_note": note},
+        "ctx_devices": {
+            "pbs_per_s": B * args.steps / wall,
+            "mul32": {"value": K * msteps / mwall, "unit": "mul/s", "pairs": K, "steps": msteps,
+                      "ms_per_step": mwall / msteps * 1e3, "decrypted_ok": mok, "of": K,
+                      "sampled_products_equal_single_device": msame, "sampled": len(pick)},
+            "replication": mode,
+            "note": ("one process, one context, every shard fed through the host-pointer ABI by the context's own "
+                     "per-shard workers; host radix batches for mul32 (each DAG layer crosses PCIe), so both rates "
+                     "are PCIe- and host-memory-inclusive and not comparable with the HBM-resident entries"),
+        },
+    }
+
+
+def _radix_rows(rb, rows):
+    from tfhe_mi355.integer import RadixBatch
+
+    return RadixBatch(np.ascontiguousarray(rb.data[rows]), list(rb.degree), list(rb.noise))
 
 
 def run_pbs(args, P, pname, workload, kname, R):

@@ -30,6 +30,7 @@ for s in ${STAGES:-tests smoke bench}; do
     t) step r06_tests_${T_NAME:-sel} 600 python -u -m pytest $T_FILES -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) step r06_smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step r06_bench_default${BENCH_SUFFIX} 900 python bench.py --steps 10 --warmup 2 ;;
+    ctx) step r06_ctx_devices 500 python bench.py --ctx-devices ${CTX_DEVS:-0,0} --steps 3 --warmup 1 ;;
     rehearse2) step r06_rehearse2_gloo_1gpu 1100 env BENCH_DIST_BACKEND=gloo python -u bench.py --gpus 2 --steps 5 --warmup 1 ;;
     ab) for pass in 1 2; do
           for t in ${AB_TAGS:-3_3}; do
