@@ -38,6 +38,21 @@ for s in ${STAGES:-tests smoke bench}; do
             bline $t r06_ab_${AB_NAME}_${t}_new$pass ${AB_ARGS}
           done
         done ;;
+    probe) # single_call_probe over PROBE_COUNTS at PROBE_PARAMS, once per PROBE_ENVS entry ("name:VAR=x,...")
+        for v in ${PROBE_ENVS:-base:X=0}; do
+          n=${v%%:*}; e=${v#*:}
+          step r06_probe_${PROBE_NAME:-p}_$n 300 env $(echo "$e" | tr ',' ' ') python scripts/single_call_probe.py ${PROBE_REPS:-5} ${PROBE_COUNTS:-1,8,64}
+          grep '^{' gpurun_out/r06_probe_${PROBE_NAME:-p}_$n.log
+        done ;;
+    envab) # ENV_AB="name1:VAR=x,VAR2=y name2:VAR=z" over EAB_TAGS, EAB_PASSES passes, interleaved
+        for pass in $(seq 1 ${EAB_PASSES:-2}); do
+          for t in ${EAB_TAGS:-4_4}; do
+            for v in $ENV_AB; do
+              n=${v%%:*}; e=${v#*:}
+              env $(echo "$e" | tr ',' ' ') bash -c "$(declare -f bline); bline $t r06_${EAB_NAME:-eab}_${t}_${n}_$pass ${AB_ARGS}" || exit 1
+            done
+          done
+        done ;;
     kt) for t in ${KT_TAGS:-2_2}; do
           if [ "$t" = lat ]; then
             step r06_kt_lat 300 rocprofv3 --kernel-trace --stats -d gpurun_out/kt_lat -o run --output-format csv -- \

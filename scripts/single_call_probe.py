@@ -47,6 +47,9 @@ def main():
         dec = client.decode(client.lwe_decrypt(glwe_sk, out), P.delta) % np.uint64(msg)
         res[str(cnt)] = {"median_ms": 1e3 * float(np.median(ts)), "min_ms": 1e3 * min(ts),
                          "ok": int(np.count_nonzero(dec == msgs)), "of": cnt}
+        if os.environ.get("PROBE_STAMPS") == "1":  # a QUAD_STAMPS build: phase stamps of CMUX 200
+            res[str(cnt)]["stamps_w0"] = [int(v) for v in out[0, 2:14]]
+            res[str(cnt)]["stamps_w4"] = [int(v) for v in out[0, 15:27]]
     print(json.dumps(res))
 
 

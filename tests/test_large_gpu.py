@@ -174,3 +174,33 @@ def test_large_pbs_two_chunks_ragged(orc, small_n_4_4):
     # one sample per sub-block rotation of the group kernel (rotation (cl / 8) mod 4: 0, 1, 2, 3)
     sample = np.array([0, 40, 80, 127, 128, 199])
     assert np.array_equal(got[sample], keys.fbsk.pbs(cts[sample], acc, threads=6))
+
+
+@pytest.mark.parametrize("mask", ["interleave", "block"])
+def test_large_pbs_cu_lanes_bit_exact(orc, small_n_4_4, mask, monkeypatch):
+    """The grouped N = 32768 CMUX on two CU-masked lanes (TFHE_MI355_LANES_MCUS: group kernels of one
+    chunk beside the streaming kernels of another): 220 ciphertexts in lane chunks of
+    24 (four full pairs, then a pair whose second chunk holds 4) -- identical to
+    the one-stream context row for row, every output decrypting, a sample bit-exact vs the oracle."""
+    from tfhe_mi355 import Engine
+
+    keys, single = small_n_4_4
+    p = keys.params
+    N = p.polynomial_size
+    monkeypatch.setenv("TFHE_MI355_LANES_MCUS", "8")
+    monkeypatch.setenv("TFHE_MI355_LANES_CHUNK", "24")
+    monkeypatch.setenv("TFHE_MI355_LANES_MASK", mask)
+    lanes = Engine(p, 0)
+    lanes.upload_bootstrap_key(keys.bsk)
+    msgs = np.random.default_rng(23).integers(0, 256, 220)
+    cts = keys.encrypt(orc, msgs, 323)
+    fs = [lambda x: (x * 3 + 5) % 256, lambda x: 255 - x]
+    luts = np.stack([orc.fill_accumulator(N, 1, 16, 16, f) for f in fs])
+    idx = (np.arange(220) % 2).astype(np.uint32)
+    got = lanes.programmable_bootstrap(cts, luts, lut_indexes=idx)
+    assert np.array_equal(got, single.programmable_bootstrap(cts, luts, lut_indexes=idx))
+    dec = decode(orc.lwe_decrypt(keys.glwe_sk, got), p.delta) % 256
+    assert np.array_equal(dec, np.where(idx == 1, 255 - msgs, (msgs * 3 + 5) % 256))
+    sample = np.array([0, 23, 24, 47, 200, 219])
+    assert np.array_equal(got[sample], keys.fbsk.pbs(cts[sample], luts, lut_idx=idx[sample], threads=6))
+    lanes.close()

@@ -13,6 +13,16 @@ pytestmark = pytest.mark.gpu
 SMALL, BIG = 200, 1100   # <= 3 x CUs rows: latency kernel; > 1024: throughput kernel (persistent grid)
 
 
+def _ran(eng, f):
+    """f()'s result and the kernel families it launched (the engine's kernel timer): the row counts
+    above assume a device of 200 .. 366 CUs, so every test also checks the kernel that ran."""
+    eng.kernel_timing(1)
+    out = f()
+    ran = set(eng.kernel_times())
+    eng.kernel_timing(0)
+    return out, ran
+
+
 @pytest.fixture(scope="module")
 def eng(keys_2_2):
     from tfhe_mi355 import Engine
@@ -42,8 +52,10 @@ def test_latency_equals_throughput_kernel_and_oracle(orc, keys_2_2, eng):
     luts = np.stack([orc.fill_accumulator(2048, 1, 4, 4, f) for f in fs])
     cts = _edge_batch(keys_2_2, BIG, 41)
     idx = (np.arange(BIG) * 5 % 3).astype(np.uint32)
-    thr = eng.programmable_bootstrap(cts, luts, lut_indexes=idx)               # throughput kernel
-    lat = eng.programmable_bootstrap(cts[:SMALL], luts, lut_indexes=idx[:SMALL])  # latency kernel
+    thr, ran = _ran(eng, lambda: eng.programmable_bootstrap(cts, luts, lut_indexes=idx))  # throughput kernel
+    assert ran == {"pbs_classic_kernel"}, ran
+    lat, ran = _ran(eng, lambda: eng.programmable_bootstrap(cts[:SMALL], luts, lut_indexes=idx[:SMALL]))
+    assert ran == {"pbs_latency_kernel"}, ran
     assert np.array_equal(lat, thr[:SMALL]), f"{np.count_nonzero(lat != thr[:SMALL])} words differ"
     sub = np.r_[0:8, 190:200]
     exp = keys_2_2.fbsk.pbs(cts[sub], luts, lut_idx=idx[sub], threads=16)
@@ -108,8 +120,10 @@ def test_mb_latency_equals_throughput_kernel_and_oracle(orc, mb_keys, g):
     luts = np.stack([orc.fill_accumulator(2048, 1, 4, 4, f) for f in fs])
     cts = _edge_batch(keys, BIG, 47 + g)
     idx = (np.arange(BIG) * 5 % 3).astype(np.uint32)
-    thr = e.programmable_bootstrap(cts, luts, lut_indexes=idx)
-    lat = e.programmable_bootstrap(cts[:SMALL], luts, lut_indexes=idx[:SMALL])
+    thr, ran = _ran(e, lambda: e.programmable_bootstrap(cts, luts, lut_indexes=idx))
+    assert ran == {"pbs_multibit"}, ran
+    lat, ran = _ran(e, lambda: e.programmable_bootstrap(cts[:SMALL], luts, lut_indexes=idx[:SMALL]))
+    assert ran == {"pbs_mb_latency_kernel"}, ran
     assert np.array_equal(lat, thr[:SMALL]), f"{np.count_nonzero(lat != thr[:SMALL])} words differ"
     sub = np.r_[0:7, 199:200]
     exp = keys.fbsk.pbs(cts[sub], luts, lut_idx=idx[sub], threads=16)

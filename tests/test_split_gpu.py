@@ -50,6 +50,22 @@ def _device_to_host(ptr, nbytes):
     return out
 
 
+def _cus():
+    """Compute units of device 0: the CMUX form thresholds of capi.cpp scale with it."""
+    import torch
+
+    return torch.cuda.get_device_properties(0).multi_processor_count
+
+
+def _ran(eng, f):
+    """f()'s result and the kernel families it launched (the engine's kernel timer)."""
+    eng.kernel_timing(1)
+    out = f()
+    ran = set(eng.kernel_times())
+    eng.kernel_timing(0)
+    return out, ran
+
+
 def engine_position(N):
     """FFT position of each engine-layout spectrum element: sub-block q = e // 1024 holds
     positions 1024 q + the WaveFft<1024> layout."""
@@ -162,8 +178,11 @@ def test_onchip_and_split_cmux_agree(orc, name):
     space = p.message_modulus * p.carry_modulus
     lwe_sk, glwe_sk, bsk, fbsk = _keys(orc, p, 77)
     eng = _engine(p, bsk)
-    C = 131 if p.polynomial_size == 8192 else 171
+    cus = _cus()
+    on_min = cus * 3 // 8 if p.polynomial_size == 8192 else cus * 5 // 8  # capi.cpp onchip_min
+    C = on_min + 35
     h = C // 2
+    quad = p.polynomial_size == 8192 and p.pbs_level == 2 and h <= cus // 4
     msgs = np.random.default_rng(5).integers(0, space, C)
     cts = orc.lwe_encrypt(78, lwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta), p.lwe_modular_std_dev)
     cts[0, :-1] = 0                                   # every a~ = 0
@@ -172,14 +191,62 @@ def test_onchip_and_split_cmux_agree(orc, name):
     fs = [lambda x: (x * 7 + 2) % space, lambda x: (x + space // 2 + 1) % space]
     luts = np.stack([orc.fill_accumulator(p.polynomial_size, 1, p.message_modulus, p.carry_modulus, f) for f in fs])
     idx = (np.arange(C) % 3 == 1).astype(np.uint32)  # per-ciphertext LUTs
-    whole = eng.programmable_bootstrap(cts, luts, lut_indexes=idx)
-    halves = np.concatenate([eng.programmable_bootstrap(cts[:h], luts, lut_indexes=idx[:h]),
-                             eng.programmable_bootstrap(cts[h:], luts, lut_indexes=idx[h:])])
+    whole, ran = _ran(eng, lambda: eng.programmable_bootstrap(cts, luts, lut_indexes=idx))
+    assert "onchip_cmux_kernel" in ran, ran
+    halves = []
+    for a, b in ((0, h), (h, C)):
+        out, ran = _ran(eng, lambda: eng.programmable_bootstrap(cts[a:b], luts, lut_indexes=idx[a:b]))
+        assert "onchip_cmux_kernel" not in ran and ("quad_cmux_kernel" in ran) == quad, ran
+        halves.append(out)
+    halves = np.concatenate(halves)
     assert np.array_equal(whole, halves), f"{np.count_nonzero(np.any(whole != halves, axis=1))} rows differ"
     sample = np.array([0, 1, 2, h - 1, h, C - 1])
     assert np.array_equal(whole[sample], fbsk.pbs(cts[sample], luts, lut_idx=idx[sample], threads=6))
     dec = decode(orc.lwe_decrypt(glwe_sk, whole[3:]), p.delta) % space
     assert np.array_equal(dec, [fs[i](m) for i, m in zip(idx[3:], msgs[3:])])
+
+
+@pytest.mark.parametrize("name", ["PARAM_MESSAGE_3_CARRY_3_KS_PBS", "PARAM_MESSAGE_2_CARRY_4_KS_PBS"])
+def test_quad_onchip_and_split_cmux_agree(orc, name):
+    """N = 8192, L = 2: the same ciphertexts through the three CMUX forms -- one call of 3/8 of the CU
+    count + 35 (on-chip CMUX, one ciphertext per CU), calls of 1, 7 and CUs/4 - 12 (quad CMUX: four
+    workgroups per ciphertext exchanging their sub-blocks every CMUX; capi.cpp quad_max = CUs / 4) and
+    one call of the rest (split CMUX, between the quad and the on-chip ranges), the kernel of each call
+    checked by the engine's kernel timer -- every row identical, a sample bit-exact against the oracle,
+    edge masks and per-ciphertext LUTs included."""
+    from tfhe_mi355.parameters import SHORTINT_ALL
+
+    p = SHORTINT_ALL[name].with_(lwe_dimension=6)
+    space = p.message_modulus * p.carry_modulus
+    lwe_sk, glwe_sk, bsk, fbsk = _keys(orc, p, 79)
+    eng = _engine(p, bsk)
+    cus = _cus()
+    Q, O = cus // 4, cus * 3 // 8  # capi.cpp quad_max, onchip_min
+    C = O + 35
+    msgs = np.random.default_rng(8).integers(0, space, C)
+    cts = orc.lwe_encrypt(80, lwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta), p.lwe_modular_std_dev)
+    cts[0, :-1] = 0                                   # every a~ = 0
+    cts[1, :-1] = np.uint64(1 << 63)                  # a~ = N
+    cts[2, -1] = np.uint64((1 << 64) - 1)             # b~ = 2N
+    cts[3, ::2] = np.uint64((1 << 64) - 1)
+    fs = [lambda x: (x * 5 + 1) % space, lambda x: (space - 1 - x) % space]
+    luts = np.stack([orc.fill_accumulator(p.polynomial_size, 1, p.message_modulus, p.carry_modulus, f) for f in fs])
+    idx = (np.arange(C) % 3 == 2).astype(np.uint32)
+    whole, ran = _ran(eng, lambda: eng.programmable_bootstrap(cts, luts, lut_indexes=idx))
+    assert "onchip_cmux_kernel" in ran, ran
+    parts = []
+    for a, b, kern in ((0, 1, "quad_cmux_kernel"), (1, 8, "quad_cmux_kernel"), (8, Q - 4, "quad_cmux_kernel"),
+                       (Q - 4, C, "large_dsub_kernel")):
+        assert 0 < b - a <= Q if kern.startswith("quad") else Q < b - a < O
+        out, ran = _ran(eng, lambda: eng.programmable_bootstrap(cts[a:b], luts, lut_indexes=idx[a:b]))
+        assert kern in ran and "onchip_cmux_kernel" not in ran, (a, b, ran)
+        parts.append(out)
+    got = np.concatenate(parts)
+    assert np.array_equal(whole, got), f"{np.count_nonzero(np.any(whole != got, axis=1))} rows differ"
+    sample = np.array([0, 1, 2, 3, 7, 8, Q - 5, Q - 4, C - 1])
+    assert np.array_equal(whole[sample], fbsk.pbs(cts[sample], luts, lut_idx=idx[sample], threads=9))
+    dec = decode(orc.lwe_decrypt(glwe_sk, whole[4:]), p.delta) % space
+    assert np.array_equal(dec, [fs[i](m) for i, m in zip(idx[4:], msgs[4:])])
 
 
 @pytest.mark.timeout(900)

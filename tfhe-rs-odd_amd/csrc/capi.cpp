@@ -252,6 +252,12 @@ struct TfheMi355Context {
     uint32_t pks_base_log = 0, pks_level = 0;
     bool pksk_ready = false, pksk_planes_ready = false;
     KernelTimer timer;  // per-kernel durations (tfhe_mi355_kernel_timing_*), off by default
+    // CU-masked lanes of the N = 32768 grouped CMUX (large_lanes), created at first use
+    std::mutex lanes_mu;
+    bool lanes_made = false;
+    long lanes_mcus = 0, lanes_chunk = 0;  // TFHE_MI355_LANES_MCUS / _CHUNK at creation
+    bool lanes_block = false;              // TFHE_MI355_LANES_MASK=block
+    hipStream_t lane_c = nullptr, lane_m = nullptr;
     // Request coalescing of small host-pointer calls (the reference calls the PBS one ciphertext
     // at a time from rayon workers: shortint/server_key/mod.rs:783-857, radix_parallel/mul.rs:
     // 347-407).  Concurrent calls are queued per op; dispatcher threads (one per batch slot,
@@ -416,6 +422,43 @@ bool is_large(const TfheMi355Context *c) {
 // made the chunk's spectra traffic the smaller share: 512 / 768 / 1024 / 1280 / 2048 ->
 // mb3_3g3 12.04k / 12.24k / 12.18k / 11.52k / 11.54k, mb3_3g2 10.21k / 10.44k / 10.63k / 9.65k /
 // 9.65k (profiles/r05_mbchunk_*.json), so multi-bit takes 1024 (400 MiB of scratch).
+// N = 32768 on two CU-masked lanes (pbs_large.hip launch_grouped_lanes): TFHE_MI355_LANES_MCUS =
+// CUs per XCD of the streaming lane (0 = one stream, the default until measured), the group lane takes
+// the rest; TFHE_MI355_LANES_MASK = "interleave" (CU mask bit i on XCD i mod 8, the driver's
+// symmetric mapping) or "block"; TFHE_MI355_LANES_CHUNK = ciphertexts per lane chunk (default: one
+// group-kernel round of the group lane's CUs twice over, i.e. its CUs / 2 since a ciphertext has 4
+// group workgroups)
+// (read per context at its creation, so that a process can hold contexts of both kinds)
+long env_long(const char *name, long dflt) {
+    const char *e = std::getenv(name);
+    return e && *e ? std::max(0L, std::atol(e)) : dflt;
+}
+bool large_lanes_on(const TfheMi355Context *c) {
+    return c->N() >= 32768 && c->p.pbs_level == 2 && !c->p.grouping_factor && c->lanes_mcus > 0 &&
+           c->lanes_mcus * 8 < c->cus;
+}
+size_t lanes_chunk(const TfheMi355Context *c) {
+    if (c->lanes_chunk > 0) return (size_t)c->lanes_chunk;
+    return std::max<size_t>(8, ((size_t)c->cus - (size_t)c->lanes_mcus * 8) / 2 / 8 * 8);
+}
+void make_lanes(TfheMi355Context *c) {
+    std::lock_guard<std::mutex> g(c->lanes_mu);
+    if (c->lanes_made) return;
+    const int cus = c->cus, m = (int)c->lanes_mcus * 8;
+    const bool block = c->lanes_block;
+    std::vector<uint32_t> mc((cus + 31) / 32, 0), mm((cus + 31) / 32, 0);
+    for (int i = 0; i < cus; i++) {
+        // interleave: the last m bits (bit i -> XCD i mod 8: m / 8 CUs of every XCD); block: the last
+        // m / 8 CUs of each 32-CU run of bits
+        const bool mem = block ? (i % (cus / 8)) >= (cus / 8) - m / 8 : i >= cus - m;
+        (mem ? mm : mc)[i / 32] |= 1u << (i % 32);
+    }
+    check(hipSetDevice(c->device), "hipSetDevice");
+    check(hipExtStreamCreateWithCUMask(&c->lane_c, (uint32_t)mc.size(), mc.data()), "hipExtStreamCreateWithCUMask");
+    check(hipExtStreamCreateWithCUMask(&c->lane_m, (uint32_t)mm.size(), mm.data()), "hipExtStreamCreateWithCUMask");
+    c->lanes_made = true;
+}
+
 size_t large_chunk(const TfheMi355Context *c) {
     static const size_t forced = [] {
         const char *e = std::getenv("TFHE_MI355_LARGE_CHUNK");
@@ -423,6 +466,7 @@ size_t large_chunk(const TfheMi355Context *c) {
         return x > 0 ? (size_t)x : (size_t)0;
     }();
     if (forced) return forced;
+    if (large_lanes_on(c)) return 2 * lanes_chunk(c);  // one chunk per lane
     if (c->N() >= 32768) return 128;
     if (c->p.grouping_factor) return 1024;
     const size_t per = large_pbs_scratch_per_ct((int)c->N(), (int)c->k(), (int)c->p.pbs_level);
@@ -451,6 +495,17 @@ size_t onchip_min(const TfheMi355Context *c) {
     }();
     if (env >= 0) return (size_t)env;
     return c->N() == 4096 ? (size_t)c->cus * 5 / 8 : (size_t)c->cus * 3 / 8;
+}
+
+// The quad CMUX (N = 8192, L = 2 classic, four CUs per ciphertext, pbs_large.hip) for batches of at
+// most this many ciphertexts: one pass of CUs / 4 by default; TFHE_MI355_QUAD_MAX overrides (0 = never)
+size_t quad_max(const TfheMi355Context *c) {
+    if (c->N() != 8192 || c->p.pbs_level != 2 || c->p.grouping_factor || c->k() != 1) return 0;
+    static const long env = [] {
+        const char *e = std::getenv("TFHE_MI355_QUAD_MAX");
+        return e && *e ? std::strtol(e, nullptr, 10) : -1L;
+    }();
+    return env >= 0 ? (size_t)env : (size_t)c->cus / 4;
 }
 
 // Batches of at most this many ciphertexts run the latency kernels (one ciphertext per CU) at the
@@ -570,6 +625,13 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
         a.timer = c->timer_or_null();
         a.grouping = (int)c->p.grouping_factor;
         a.onchip_min_count = (int)onchip_min(c);
+        a.quad_pass = (int)(c->cus / 4);
+        a.quad_max_count = (int)quad_max(c);
+        if (large_lanes_on(c) && count > lanes_chunk(c)) {  // two chunks in flight at once
+            make_lanes(c);
+            a.lane_c = c->lane_c;
+            a.lane_m = c->lane_m;
+        }
         check(launch_large_pbs((int)c->N(), (int)c->k(), (int)c->p.pbs_level, a, s), "launch large pbs");
         return;
     }
@@ -1498,6 +1560,12 @@ TfheMi355Context *create_single(const TfheMi355Parameters &p, int device) {
     auto *c = new TfheMi355Context();
     c->p = p;
     c->device = device;
+    c->lanes_mcus = env_long("TFHE_MI355_LANES_MCUS", 0);
+    c->lanes_chunk = env_long("TFHE_MI355_LANES_CHUNK", 0);
+    {
+        const char *e = std::getenv("TFHE_MI355_LANES_MASK");
+        c->lanes_block = e && std::strcmp(e, "block") == 0;
+    }
     try {
         check(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
         int cus = 0;
@@ -1831,6 +1899,11 @@ int tfhe_mi355_context_destroy(TfheMi355Context *ctx) {
             if (L.stream) (void)hipStreamDestroy(L.stream);
         }
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+        for (hipStream_t l : {ctx->lane_c, ctx->lane_m})
+            if (l) {
+                (void)hipStreamSynchronize(l);
+                (void)hipStreamDestroy(l);
+            }
         delete ctx;  // device and pinned buffers free themselves
         if (!orphans.empty())
             fail("context destroyed with %zu request(s) still queued: they were not run and their wait returns 1",

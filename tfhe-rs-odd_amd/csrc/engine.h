@@ -186,6 +186,14 @@ struct LargePbsLaunch {
     KernelTimer *timer = nullptr;  // optional per-kernel timing
     int grouping = 0;              // > 0: multi-bit PBS (fbsk = [n/g][2^g][L][k+1][k+1] polys)
     int onchip_min_count = 0;      // N = 8192, L = 2 classic: the on-chip CMUX from this many ciphertexts on
+    // N = 32768 grouped CMUX on two CU-masked streams: lane_c runs the
+    // FP64 group kernels of one chunk while lane_m runs the streaming kernels (top_inv, digits) of
+    // another; null: everything on the launch stream
+    hipStream_t lane_c = nullptr, lane_m = nullptr;
+    // N = 8192, L = 2 classic: the quad CMUX (R workgroups per ciphertext) for batches
+    // of at most quad_max_count ciphertexts, quad_pass ciphertexts per launch (CUs / R: one workgroup
+    // per CU, all resident at once); 0 = never
+    int quad_pass = 0, quad_max_count = 0;
 };
 bool large_pbs_supported(int N, int k, int L);
 bool large_multibit_supported(int N, int k, int L, int g);

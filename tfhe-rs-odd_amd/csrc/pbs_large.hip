@@ -14,6 +14,7 @@
 // from a [c-1][a] copy of the table (coalesced); sub-blocks W_M[16 x] through an LDS table (the
 // oracle's tstride-16 reads of the same table, so bit-identical).
 #include <cstdlib>
+#include <mutex>
 #include <type_traits>
 
 #include "engine.h"
@@ -2067,6 +2068,411 @@ static bool onchip_enabled() {
     return v;
 }
 
+// ---------------------------------------------------------------------------------------
+// Quad CMUX (N = 8192, k = 1, L = 2, classic; small batches).  The
+// on-chip CMUX runs a ciphertext's whole blind rotation on ONE CU (25 us per CMUX: 22-25 ms per
+// call whatever the count), the split CMUX spreads it over several launches per CMUX (16.3 ms for
+// one ciphertext).  Here the R = 4 sub-blocks of one ciphertext run on R CUs of one XCD at once, in
+// one launch for the whole blind rotation.  Every workgroup keeps the FULL accumulator (registers
+// as in the on-chip kernel, thread t owning the pairs (j, j + M), j = t + 512 h + 1024 b) and does
+// the cheap full-width work itself -- rotation, decomposition, the top DIT inverse + backward
+// conversion -- but the expensive part only for its sub-block q:
+//   rotation     : pairs -> LDS, ct1 = X^{a~} acc - acc gathered, digits (as the on-chip kernel)
+//   top DIF      : output q of every top radix-4 butterfly, both levels and rows -> 4 LDS buffers
+//   sub-FFTs     : waves 0-3, one polynomial (level, row) each, spectra published in place;
+//                  meanwhile waves 4-7 load the CMUX's GGSW operands of sub-block q (4 slots each)
+//   MAC          : waves 4-7, slots 4 w' .. 4 w' + 3, both columns, the oracle's level/row order
+//   inverse      : waves 0-1 (column c) -> U_q[c], stored write-through to the ciphertext's
+//                  exchange buffer (double-buffered by CMUX parity), then a flag
+//   exchange     : every workgroup waits for the R flags of CMUX i, loads U_0..U_{R-1} at its
+//                  butterflies (sc1 loads: L2 / Infinity Cache, never a stale L1 line) and runs the
+//                  top DIT radix-4 + backward_add of both columns into its registers
+// One exchange per CMUX (U: 32 KiB out, 96 KiB in per workgroup); the hand-off is the guide's
+// "sc1 payload + drained flag" form (MI355X_MICROARCH.md, inter-workgroup visibility).  Same
+// operations on the same values as the on-chip / split paths (the redundant full-width parts
+// compute identical values in every workgroup), so the outputs are bit-identical.
+// Co-residency: the R workgroups of a ciphertext wait on each other, so a launch holds at most one
+// workgroup per CU (143 KiB of LDS each) and at most CUs / R ciphertexts, and quad launches of one
+// device are serialised (launch_quad below); every flag wait is bounded (QUAD_SPIN_MAX polls).
+// ---------------------------------------------------------------------------------------
+#ifndef QUAD_SPIN_MAX
+#define QUAD_SPIN_MAX (1u << 24)
+#endif
+#ifndef QUAD_STAMPS
+#define QUAD_STAMPS 0  // diagnostic builds: s_memtime at the phase boundaries of CMUX 200 (waves 0 and 4 of
+                       // ciphertext 0's workgroup q = 0), written over that ciphertext's output words 1..26
+#endif
+#ifndef QUAD_TPF
+#define QUAD_TPF 1  // the top stages' twist / W loads issued ahead of the barrier before their use
+#endif
+#ifndef QUAD_OWNU
+#define QUAD_OWNU 1  // the workgroup's own U_q read back from LDS, not from the exchange buffer
+#endif
+#ifndef QUAD_TSKIP
+#define QUAD_TSKIP 0  // timing-only builds (wrong outputs): 1 no flag wait, 2 no forward sub-FFTs, 4 no inverse
+                      // sub-FFTs, 8 no GGSW loads, 16 no U loads, 32 no U stores
+#endif
+template <int N>
+struct QuadCfg {
+    static constexpr int M = N / 2, R = M / 1024;
+    static constexpr int THREADS = 512, TPC = THREADS, H = 1024 / THREADS;
+    static constexpr int BUF = SubFft::XL;
+    static constexpr int REGION = 2 * R * BUF;  // the rotation's 2 x M pairs; then 4 spectra + 2 columns
+    static_assert(REGION >= 6 * BUF, "spectra and column buffers fit the pair region");
+    static constexpr int S1 = REGION;
+    static constexpr size_t LDS = sizeof(double2) * (S1 + SubFft::Lds::s1_len);
+    static_assert(LDS > 80 * 1024 && LDS <= 160 * 1024, "one workgroup per CU");
+    // device scratch of a launch: flags [ct][R] (one 128-B line each), then per ciphertext the
+    // exchange U [parity 2][sub-block R][column 2][1024] double2
+    static constexpr size_t FLAG_BYTES = 128;
+    static constexpr size_t U_BYTES = (size_t)2 * R * 2 * 1024 * sizeof(double2);
+};
+
+template <int N>
+__device__ __forceinline__ double2 *quad_u(const LargePbsLaunch &a, int cnt, int ct, int par, int q, int c) {
+    using Cfg = QuadCfg<N>;
+    char *base = reinterpret_cast<char *>(a.scratch) + (size_t)cnt * Cfg::R * Cfg::FLAG_BYTES;
+    return reinterpret_cast<double2 *>(base + (size_t)ct * Cfg::U_BYTES) + ((size_t)(par * Cfg::R + q) * 2 + c) * 1024;
+}
+
+// top DIF output Q of butterfly a0 for both rows and levels -> spectra buffers p = (lvl - 1) 2 + r
+// (tv[h][b] = twist[a0 + 1024 b], wq[h] = W[a0 Q], loaded by the caller ahead of the barrier)
+template <int N, int Q, int H>
+__device__ __forceinline__ void quad_top(double2 *lds, const uint64_t (&pk)[2][H][Split<N>::R],
+                                         const cx (&tvh)[H][Split<N>::R], const cx (&wqh)[H], int t) {
+    constexpr int R = Split<N>::R, BUF = SubFft::XL;
+#pragma unroll
+    for (int h = 0; h < H; h++) {
+        const int a0 = t + 512 * h;
+        const cx *tv = tvh[h];
+        const cx wq = wqh[h];
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int li = 0; li < 2; li++) {  // li = 0: level L, 1: level L-1
+                cx u[R];
+#pragma unroll
+                for (int b = 0; b < R; b++) {
+                    const uint64_t w = pk[r][h][b] >> (32 * li);
+                    const int32_t d0 = (int32_t)(int16_t)(w & 0xffffu), d1 = (int32_t)(int16_t)((w >> 16) & 0xffffu);
+                    u[b] = cmulw(cx{(double)d0, (double)d1}, tv[b].re, tv[b].im);
+                }
+                dftR_fwd<R>(u);
+                const cx y = Q ? cmulw(u[Q], wq.re, wq.im) : u[0];
+                const int p = (1 - li) * 2 + r;  // level L -> 2, 3; level L-1 -> 0, 1
+                lds[p * BUF + a0] = make_double2(y.re, y.im);
+            }
+    }
+}
+
+template <int N, bool D32>
+__global__ void __launch_bounds__(512, 1) quad_cmux_kernel(LargePbsLaunch a, int ct0, int cnt) {
+    using S = Split<N>;
+    using Cfg = QuadCfg<N>;
+    constexpr int K = 1, L = 2, M = S::M, R = S::R, H = Cfg::H, BUF = Cfg::BUF, TPC = Cfg::TPC;
+    static_assert(R == 4, "N = 8192");
+    constexpr size_t ggsw_len = (size_t)L * (K + 1) * (K + 1) * M;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double2 *lds = reinterpret_cast<double2 *>(smem);
+    acc_pair *pairs = reinterpret_cast<acc_pair *>(smem);
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    // the R workgroups of ciphertext cl: blocks 8 m + x with the same x (one XCD), q = m mod R
+    const int x = blockIdx.x & 7, mm = blockIdx.x >> 3;
+    const int cl = x + 8 * (mm / R), q = mm % R;
+    if (cl >= cnt) return;  // all R workgroups of a padding slot
+    const int ct = ct0 + cl;
+    uint32_t *flags = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(a.scratch) + (size_t)cl * R * Cfg::FLAG_BYTES);
+    double2 *s1 = lds + Cfg::S1;
+    for (int e = t; e < SubFft::Lds::s1_len; e += TPC) s1[e] = a.W[R * (e & 63) * ((e >> 6) + 1)];
+    const SubFft::Lds tw{s1, s1};
+    const uint64_t *in = a.lwe_in + (size_t)ct * (a.n + 1);
+
+    // acc = LUT / X^{b~} (large_init_kernel), full width in every workgroup
+    uint64_t lo[2][H][R], hi[2][H][R];
+    {
+        const uint32_t bt = pbs_modulus_switch<S::LOGN>(in[a.n]);
+        const uint32_t li = a.lut_indexes ? min(a.lut_indexes[ct], a.lut_count - 1u) : 0u;
+        const uint64_t *lut = a.luts + (size_t)li * (K + 1) * N;
+        const int full = bt / N, rem = bt % N;
+        auto init = [&](int r, int p) -> uint64_t {
+            const int src = p + rem;
+            const bool wrap = src >= N;
+            const uint64_t v = lut[(size_t)r * N + (wrap ? src - N : src)];
+            return (wrap != (bool)(full & 1)) ? 0 - v : v;
+        };
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int h = 0; h < H; h++)
+#pragma unroll
+                for (int b = 0; b < R; b++) {
+                    const int j = t + TPC * h + 1024 * b;
+                    lo[r][h][b] = init(r, j);
+                    hi[r][h][b] = init(r, j + M);
+                }
+    }
+    const double k32 = torus_k32();
+    const int beta = a.base_log;
+    auto pslot = [&](int r, int j) { return (2 * (j >> 10) + r) * BUF + (j & 1023); };
+    auto store_pairs = [&]() {
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int h = 0; h < H; h++)
+#pragma unroll
+                for (int b = 0; b < R; b++) pairs[(2 * b + r) * BUF + t + TPC * h] = acc_pair{lo[r][h][b], hi[r][h][b]};
+    };
+    store_pairs();
+    WaveLocalSyncL<3> wsync;
+    const __amdgpu_buffer_rsrc_t rtw = make_rsrc(a.twist), rwt = make_rsrc(a.wtop);
+    uint64_t st[QUAD_STAMPS ? 13 : 1];
+    auto stamp = [&](int i, int k) {
+        if constexpr (QUAD_STAMPS) {
+            if (i == 200) st[k] = __builtin_amdgcn_s_memtime();
+        }
+    };
+
+    uint64_t a_next = in[0];
+    for (int i = 0; i < a.n; i++) {
+        stamp(i, 0);
+        const uint32_t at = pbs_modulus_switch<S::LOGN>(a_next);
+        a_next = in[i + 1 < a.n ? i + 1 : i];
+        const bool full_odd = (at / N) & 1;
+        const int rem = at % N;
+        const int par = i & 1;
+        // the top stage's twist and W[a0 q], issued ahead of the barrier (QUAD_TPF)
+        cx tvh[H][R], wqh[H];
+        auto top_tables = [&]() {
+            const uint32_t z = (uint32_t)opaque_zero();
+#pragma unroll
+            for (int h = 0; h < H; h++) {
+#pragma unroll
+                for (int b = 0; b < R; b++) {
+                    const double2 y = buffer_ld_d2(rtw, 16u * (t + TPC * h + 1024 * b), z);
+                    tvh[h][b] = cx{y.x, y.y};
+                }
+                const double2 y = q ? buffer_ld_d2(rwt, 16u * ((q - 1) * 1024 + t + TPC * h), z) : make_double2(1.0, 0.0);
+                wqh[h] = cx{y.x, y.y};
+            }
+        };
+        if (QUAD_TPF) top_tables();
+        __syncthreads();  // every pair written (and, at i = 0, the twiddle table)
+        stamp(i, 1);
+        // ---- rotation + decomposition (the on-chip kernel's) ----
+        uint64_t pk[2][H][R];
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int h = 0; h < H; h++)
+#pragma unroll
+                for (int b = 0; b < R; b++) {
+                    const int j = t + TPC * h + 1024 * b;
+                    const int jj0 = j - rem;
+                    const acc_pair rot = pairs[pslot(r, jj0 & (M - 1))];
+                    const bool swap = jj0 < 0 && jj0 >= -M;
+                    const uint64_t x0 = swap ? rot.y : rot.x, x1 = swap ? rot.x : rot.y;
+                    const bool neg0 = (jj0 < 0) != full_odd, neg1 = (jj0 + M < 0) != full_odd;
+                    int32_t e0[2], e1[2];
+                    onchip_decompose<D32>((neg0 ? 0 - x0 : x0) - lo[r][h][b], beta, e0);
+                    onchip_decompose<D32>((neg1 ? 0 - x1 : x1) - hi[r][h][b], beta, e1);
+                    pk[r][h][b] = ((uint64_t)((uint32_t)e0[0] & 0xffffu)) | ((uint64_t)((uint32_t)e1[0] & 0xffffu) << 16) |
+                                  ((uint64_t)((uint32_t)e0[1] & 0xffffu) << 32) |
+                                  ((uint64_t)((uint32_t)e1[1] & 0xffffu) << 48);
+                }
+        stamp(i, 2);
+        __syncthreads();  // the pairs are read: the region becomes the spectra
+        stamp(i, 3);
+        // ---- top DIF output q of both rows and levels ----
+        if (!QUAD_TPF) top_tables();
+        switch (q) {
+            case 0: quad_top<N, 0, H>(lds, pk, tvh, wqh, t); break;
+            case 1: quad_top<N, 1, H>(lds, pk, tvh, wqh, t); break;
+            case 2: quad_top<N, 2, H>(lds, pk, tvh, wqh, t); break;
+            default: quad_top<N, 3, H>(lds, pk, tvh, wqh, t); break;
+        }
+        stamp(i, 4);
+        __syncthreads();
+        stamp(i, 5);
+        const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.fbsk + (size_t)i * ggsw_len + 1024 * q);
+        if (wave < 4) {
+            // ---- sub-block forward FFT of polynomial p = wave, published in place ----
+            double2 *own = lds + wave * BUF;
+            cx v[16];
+#pragma unroll
+            for (int b = 0; b < 16; b++) {
+                const double2 y = own[lane + 64 * b];
+                v[b] = cx{y.x, y.y};
+            }
+            if (!(QUAD_TSKIP & 2)) SubFft::forward(v, reinterpret_cast<cx *>(own), tw, lane, wsync);
+            wsync();
+#pragma unroll
+            for (int sl = 0; sl < 16; sl++) own[sl * 64 + lane] = make_double2(v[sl].re, v[sl].im);
+            __syncthreads();  // spectra published
+            stamp(i, 6);
+            __syncthreads();  // MAC outputs in the column buffers
+            stamp(i, 7);
+            if (wave < 2) {
+                // ---- inverse sub-FFT of column c = wave -> U_q[c] (write-through) ----
+                double2 *colb = lds + (4 + wave) * BUF;
+#pragma unroll
+                for (int sl = 0; sl < 16; sl++) {
+                    const double2 y = colb[sl * 64 + lane];
+                    v[sl] = cx{y.x, y.y};
+                }
+                if (!(QUAD_TSKIP & 4)) SubFft::inverse(v, reinterpret_cast<cx *>(colb), tw, lane, wsync);
+                wsync();  // the inverse's own exchange reads of colb are done
+#pragma unroll
+                for (int b = 0; b < 16; b++) colb[lane + 64 * b] = make_double2(v[b].re, v[b].im);  // own U_q[c]
+                double2 *dst = quad_u<N>(a, cnt, cl, par, q, wave);
+                const __amdgpu_buffer_rsrc_t ru = make_rsrc(dst);
+                if (!(QUAD_TSKIP & 32))
+#pragma unroll
+                    for (int b = 0; b < 16; b++)
+                        buffer_st_d2p<16>(ru, 16u * (lane + 64 * b), 0, make_double2(v[b].re, v[b].im));
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            stamp(i, 8);
+        } else {
+            // ---- GGSW operands of slots 4 w' .. 4 w' + 3, both columns (in flight during the FFTs) ----
+            const int w4 = wave - 4;
+            double2 g[4][2][4];  // [slot][column][polynomial p]
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+#pragma unroll
+                for (int c = 0; c < 2; c++)
+#pragma unroll
+                    for (int p = 0; p < 4; p++)
+                        g[k][c][p] = (QUAD_TSKIP & 8) ? make_double2(p + c, k)
+                                                      : buffer_ld_d2(rg, 16u * lane, 16u * (uint32_t)((p * 2 + c) * M + (4 * w4 + k) * 64));
+            __syncthreads();  // spectra published
+            stamp(i, 6);
+            // ---- MAC: levels L..1, rows 0..k (p = 2, 3, 0, 1), the oracle's forms ----
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int sl = 4 * w4 + k;
+                double2 f[4];
+#pragma unroll
+                for (int p = 0; p < 4; p++) f[p] = lds[p * BUF + sl * 64 + lane];
+#pragma unroll
+                for (int c = 0; c < 2; c++) {
+                    cx o;
+                    {
+                        const double2 gg = g[k][c][2], ff = f[2];
+                        o.re = fma(gg.x, ff.x, -(gg.y * ff.y));
+                        o.im = fma(gg.x, ff.y, gg.y * ff.x);
+                    }
+                    constexpr int order[3] = {3, 0, 1};
+#pragma unroll
+                    for (int u = 0; u < 3; u++) {
+                        const double2 gg = g[k][c][order[u]], ff = f[order[u]];
+                        o.re = fma(gg.x, ff.x, fma(-gg.y, ff.y, o.re));
+                        o.im = fma(gg.x, ff.y, fma(gg.y, ff.x, o.im));
+                    }
+                    lds[(4 + c) * BUF + sl * 64 + lane] = make_double2(o.re, o.im);
+                }
+            }
+            stamp(i, 7);
+            __syncthreads();  // MAC outputs in the column buffers
+            stamp(i, 8);
+        }
+        // the top inverse's twist and W[a0 c], issued ahead of the exchange wait
+        cx tvd[H][R], wqd[H][R];
+        auto dit_tables = [&]() {
+            const uint32_t z = (uint32_t)opaque_zero();
+#pragma unroll
+            for (int h = 0; h < H; h++) {
+#pragma unroll
+                for (int b = 0; b < R; b++) {
+                    const double2 y = buffer_ld_d2(rtw, 16u * (t + TPC * h + 1024 * b), z);
+                    tvd[h][b] = cx{y.x, y.y};
+                }
+#pragma unroll
+                for (int c = 1; c < R; c++) {
+                    const double2 y = buffer_ld_d2(rwt, 16u * ((c - 1) * 1024 + t + TPC * h), z);
+                    wqd[h][c] = cx{y.x, y.y};
+                }
+            }
+        };
+        if (QUAD_TPF) dit_tables();
+        __syncthreads();  // U_q stored and drained by both storing waves
+        stamp(i, 9);
+        // ---- exchange: the R workgroups' U of CMUX i ----
+        if (t == 0) {
+            __hip_atomic_store(flags + q * (Cfg::FLAG_BYTES / 4), (uint32_t)(i + 1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            for (int p = 0; p < ((QUAD_TSKIP & 1) ? 0 : R); p++) {
+                const uint32_t *f = flags + p * (Cfg::FLAG_BYTES / 4);
+                for (uint32_t spin = 0; spin < QUAD_SPIN_MAX; spin++) {
+                    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (uint32_t)(i + 1)) break;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+        }
+        __syncthreads();
+        stamp(i, 10);
+        // ---- top DIT radix-4 of both columns, backward_add (large_top_inv), full width ----
+        if (!QUAD_TPF) dit_tables();
+#pragma unroll
+        for (int h = 0; h < H; h++) {
+            const int a0 = t + TPC * h;
+            const cx *tv = tvd[h], *wq = wqd[h];
+#pragma unroll
+            for (int col = 0; col < 2; col++) {
+                cx u[R];
+#pragma unroll
+                for (int c = 0; c < R; c++) {
+                    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+                    cx y;
+                    if (QUAD_OWNU && c == q) {  // this workgroup's own sub-block: kept in LDS by the inverse wave
+                        const double2 z = lds[(4 + col) * BUF + a0];
+                        y = cx{z.x, z.y};
+                    } else if (QUAD_TSKIP & 16) {
+                        const double2 z = lds[(c * 2 + col) * BUF + a0];
+                        y = cx{z.x, z.y};
+                    } else {
+                        const v4u w = __builtin_amdgcn_raw_buffer_load_b128(make_rsrc(quad_u<N>(a, cnt, cl, par, c, col)),
+                                                                             16u * a0, 0, 16);  // sc1: L2, not L1
+                        y = cx{__hiloint2double((int)w.y, (int)w.x), __hiloint2double((int)w.w, (int)w.z)};
+                    }
+                    u[c] = c == 0 ? y : cmulw(y, wq[c].re, -wq[c].im);
+                }
+                dftR_inv<R>(u);
+#pragma unroll
+                for (int b = 0; b < R; b++) backward_add(u[b], tv[b], lo[col][h][b], hi[col][h][b], k32);
+            }
+        }
+        stamp(i, 11);
+        store_pairs();  // every LDS reader of this CMUX passed the barrier above
+        stamp(i, 12);
+    }
+    // ---- sample extract at degree 0 (large_extract_kernel), workgroup 0 of the ciphertext ----
+    __syncthreads();
+    if (q != 0) return;
+    uint64_t *out = a.lwe_out + (size_t)ct * ((size_t)K * N + 1);
+    for (int e = t; e < N; e += TPC) {
+        const int p = e == 0 ? 0 : N - e;
+        const acc_pair pr = pairs[pslot(0, p & (M - 1))];
+        const uint64_t xv = p >= M ? pr.y : pr.x;
+        out[e] = e == 0 ? xv : 0 - xv;
+    }
+    if (t == 0) out[N] = lo[1][0][0];  // row 1 position 0: the body
+    if constexpr (QUAD_STAMPS) {
+        __syncthreads();
+        if (cl == 0 && lane == 0 && (wave == 0 || wave == 4))
+            for (int k = 1; k < 13; k++) out[(wave ? 14 : 1) + k] = st[k] - st[0];
+    }
+}
+
+// TFHE_MI355_QUAD=0: never the quad CMUX (A/B)
+static bool quad_enabled() {
+    static const bool v = [] {
+        const char *e = std::getenv("TFHE_MI355_QUAD");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // sample extract at degree 0 (glwe_sample_extraction.rs:91-147)
 template <int N, int K>
 __global__ void __launch_bounds__(256) large_extract_kernel(LargePbsLaunch a, int ct0, int cnt) {
@@ -2224,10 +2630,142 @@ static bool large_pair_sub_classic() {
     return v;
 }
 
+// The grouped N = 32768 CMUX on two CU-masked lanes (round 6).  Per chunk-CMUX the group kernel
+// is FP64-bound (VALU busy 0.42) and the two streaming kernels (large_top_inv, large_digits: 43 % of
+// the time) run at the Infinity-Cache streaming ceiling, one after the other on every CU.  Here two
+// chunks A and B alternate: lane_c (most CUs) runs group(A, i) while lane_m (the other CUs) runs
+// top_inv(B, i - 1) + digits(B, i), then the roles swap; cross-lane order by events.  Per lane the
+// kernel sequence and its arguments are those of the one-stream path, so outputs are identical.
+//   lane_m: init(A) digits(A,0) [dA]  init(B) digits(B,0) [dB]
+//   per CMUX i:  lane_c: <dA> group(A,i) [gA]  <dB> group(B,i) [gB]
+//                lane_m: <gA> top_inv(A,i) digits(A,i+1) [dA]  <gB> top_inv(B,i) digits(B,i+1) [dB]
+//   lane_m: extract(A) extract(B); the launch stream waits for both lanes
+static hipError_t launch_grouped_lanes(const LargePbsLaunch &a0, hipStream_t s, size_t per_ct) {
+    constexpr int N = LN, K = 1;
+    const int lchunk = (int)std::min<size_t>((size_t)a0.count, a0.scratch_bytes / per_ct / 2);
+    if (lchunk <= 0) return hipErrorInvalidValue;
+    hipStream_t C = a0.lane_c, Mst = a0.lane_m;
+    hipEvent_t ev[5] = {};
+    hipError_t e = hipSuccess;
+    for (auto &x : ev)
+        if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess) return e;
+    hipEvent_t &start = ev[0], &dA = ev[1], &dB = ev[2], &gA = ev[3], &gB = ev[4];
+    (void)hipEventRecord(start, s);  // the caller's prior work (inputs, LUTs) before either lane
+    (void)hipStreamWaitEvent(C, start, 0);
+    (void)hipStreamWaitEvent(Mst, start, 0);
+    LargePbsLaunch la[2] = {a0, a0};
+    for (int l = 0; l < 2; l++) {
+        la[l].levels = 2;
+        la[l].acc = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(a0.scratch) + (size_t)l * lchunk * per_ct);
+        la[l].spectra = reinterpret_cast<double2 *>(reinterpret_cast<char *>(la[l].acc) +
+                                                    (size_t)lchunk * (K + 1) * N * sizeof(uint64_t));
+    }
+    hipEvent_t *dev[2] = {&dA, &dB}, *gev[2] = {&gA, &gB};
+    for (int ct0 = 0; ct0 < a0.count; ct0 += 2 * lchunk) {
+        int c0[2], cnt[2];
+        for (int l = 0; l < 2; l++) {
+            c0[l] = ct0 + l * lchunk;
+            cnt[l] = std::max(0, std::min(lchunk, a0.count - c0[l]));
+            la[l].chunk_count = cnt[l];
+        }
+        const int lanes = cnt[1] > 0 ? 2 : 1;
+        auto grp_blocks = [&](int l) { return (unsigned)((cnt[l] + 7) / 8) * 8 * 4 * GroupCfg::PARTS; };
+        auto dig_blocks = [&](int l) { return (unsigned)((cnt[l] + 7) / 8) * 8 * (LM / LARGE_DIGT); };
+        auto top_blocks = [&](int l) { return (unsigned)cnt[l] * (K + 1) * (1024 / TOPT); };
+        for (int l = 0; l < lanes; l++) {
+            const size_t init_elems = (size_t)cnt[l] * (K + 1) * N;
+            hipLaunchKernelGGL((large_init_kernel<N, K>), dim3((unsigned)((init_elems + 255) / 256)), dim3(256), 0, Mst,
+                               la[l], c0[l], cnt[l]);
+            {
+                TimedLaunch tl(a0.timer, "large_digits_kernel", Mst);
+                hipLaunchKernelGGL(large_digits_kernel, dim3(dig_blocks(l)), dim3(LARGE_DIGT), 0, Mst, la[l], c0[l], 0);
+            }
+            (void)hipEventRecord(*dev[l], Mst);
+        }
+        for (int i = 0; i < a0.n; i++) {
+            for (int l = 0; l < lanes; l++) {
+                (void)hipStreamWaitEvent(C, *dev[l], 0);
+                {
+                    TimedLaunch tl(a0.timer, "large_group_cmux_kernel", C);
+                    hipLaunchKernelGGL(large_group_cmux_kernel, dim3(grp_blocks(l)), dim3(GroupCfg::THREADS), GroupCfg::LDS, C,
+                                       la[l], c0[l], i);
+                }
+                (void)hipEventRecord(*gev[l], C);
+            }
+            for (int l = 0; l < lanes; l++) {
+                (void)hipStreamWaitEvent(Mst, *gev[l], 0);
+                {
+                    TimedLaunch tl(a0.timer, "large_top_inv_kernel", Mst);
+                    hipLaunchKernelGGL((large_top_inv_kernel<N, K>), dim3(top_blocks(l)), dim3(TOPT), 0, Mst, la[l], c0[l], i);
+                }
+                if (i + 1 < a0.n) {
+                    TimedLaunch tl(a0.timer, "large_digits_kernel", Mst);
+                    hipLaunchKernelGGL(large_digits_kernel, dim3(dig_blocks(l)), dim3(LARGE_DIGT), 0, Mst, la[l], c0[l],
+                                       i + 1);
+                    (void)hipEventRecord(*dev[l], Mst);
+                }
+            }
+        }
+        for (int l = 0; l < lanes; l++) {
+            const size_t out_elems = (size_t)cnt[l] * (K * N + 1);
+            hipLaunchKernelGGL((large_extract_kernel<N, K>), dim3((unsigned)((out_elems + 255) / 256)), dim3(256), 0, Mst,
+                               la[l], c0[l], cnt[l]);
+        }
+        // the next pair reuses both lanes' scratch: its init (lane_m) must follow this pair's last
+        // group kernels (lane_c) -- lane_m already ran top_inv after them (gA / gB waits above)
+    }
+    (void)hipEventRecord(gA, C);
+    (void)hipEventRecord(dA, Mst);
+    (void)hipStreamWaitEvent(s, gA, 0);
+    (void)hipStreamWaitEvent(s, dA, 0);
+    e = hipGetLastError();
+    for (auto &x : ev) (void)hipEventDestroy(x);
+    return e;
+}
+
+// The quad CMUX over the batch in passes of quad_pass ciphertexts.  Its workgroups wait on each
+// other, so two quad launches must never share the device's CUs: every launch of a device waits
+// for the previous one (an event chained across streams under a process-wide lock).
+template <int N>
+static hipError_t launch_quad(const LargePbsLaunch &a0, hipStream_t s) {
+    using Cfg = QuadCfg<N>;
+    static std::mutex mu;
+    static hipEvent_t last[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(s, &cs);
+    const bool capturing = cs != hipStreamCaptureStatusNone;
+    const int pass = a0.quad_pass;
+    if (pass <= 0 || (size_t)std::min(pass, a0.count) * (Cfg::R * Cfg::FLAG_BYTES + Cfg::U_BYTES) > a0.scratch_bytes)
+        return hipErrorInvalidValue;
+    std::lock_guard<std::mutex> g(mu);
+    if (!capturing && last[dev]) (void)hipStreamWaitEvent(s, last[dev], 0);
+    for (int c0 = 0; c0 < a0.count; c0 += pass) {
+        const int cnt = std::min(pass, a0.count - c0);
+        hipError_t e = hipMemsetAsync(a0.scratch, 0, (size_t)cnt * Cfg::R * Cfg::FLAG_BYTES, s);  // the flags
+        if (e != hipSuccess) return e;
+        TimedLaunch tl(a0.timer, "quad_cmux_kernel", s);
+        const dim3 grid((unsigned)((cnt + 7) / 8) * 8 * Cfg::R), block(Cfg::THREADS);
+        if (a0.base_log * 2 <= 30)
+            hipLaunchKernelGGL((quad_cmux_kernel<N, true>), grid, block, Cfg::LDS, s, a0, c0, cnt);
+        else
+            hipLaunchKernelGGL((quad_cmux_kernel<N, false>), grid, block, Cfg::LDS, s, a0, c0, cnt);
+    }
+    if (!capturing) {
+        if (!last[dev]) (void)hipEventCreateWithFlags(&last[dev], hipEventDisableTiming);
+        (void)hipEventRecord(last[dev], s);
+    }
+    return hipGetLastError();
+}
+
 template <int N, int K, int L, int G = 0>
 static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
     using S = Split<N>;
     if (a0.count == 0) return hipSuccess;
+    if constexpr (G == 0 && K == 1 && L == 2 && S::R == 4) {
+        if (quad_enabled() && a0.count <= a0.quad_max_count) return launch_quad<N>(a0, s);
+    }
     if constexpr (G == 0 && K == 1 && (L == 2 || L == 1) && (S::R == 4 || S::R == 2)) {
         if (onchip_enabled() && a0.count >= a0.onchip_min_count) {  // the whole blind rotation on chip, no scratch
             TimedLaunch tl(a0.timer, "onchip_cmux_kernel", s);
@@ -2240,6 +2778,10 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
         }
     }
     const size_t per_ct = large_pbs_scratch_per_ct(N, K, L);
+    if constexpr (N == LN && K == 1 && L == 2 && G == 0) {
+        if (LARGE_GROUP_SUB && large_grouped_enabled() && a0.lane_c && a0.lane_m)
+            return launch_grouped_lanes(a0, s, per_ct);
+    }
     const int chunk = (int)std::min<size_t>((size_t)a0.count, a0.scratch_bytes / per_ct);
     if (chunk <= 0) return hipErrorInvalidValue;
     LargePbsLaunch a = a0;
