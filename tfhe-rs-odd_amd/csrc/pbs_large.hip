@@ -2106,7 +2106,9 @@ static bool onchip_enabled() {
 #define QUAD_TPF 1  // the top stages' twist / W loads issued ahead of the barrier before their use
 #endif
 #ifndef QUAD_OWNU
-#define QUAD_OWNU 1  // the workgroup's own U_q read back from LDS, not from the exchange buffer
+#define QUAD_OWNU 0  // 1: the workgroup's own U_q read back from LDS, not from the exchange buffer -- the
+                     // per-sub-block branch serialises the U loads: 13.07-13.68 vs 12.63 ms per call
+                     // (profiles/r06_quad_ab.txt)
 #endif
 #ifndef QUAD_TSKIP
 #define QUAD_TSKIP 0  // timing-only builds (wrong outputs): 1 no flag wait, 2 no forward sub-FFTs, 4 no inverse
@@ -2321,9 +2323,11 @@ __global__ void __launch_bounds__(512, 1) quad_cmux_kernel(LargePbsLaunch a, int
                     v[sl] = cx{y.x, y.y};
                 }
                 if (!(QUAD_TSKIP & 4)) SubFft::inverse(v, reinterpret_cast<cx *>(colb), tw, lane, wsync);
-                wsync();  // the inverse's own exchange reads of colb are done
+                if (QUAD_OWNU) {
+                    wsync();  // the inverse's own exchange reads of colb are done
 #pragma unroll
-                for (int b = 0; b < 16; b++) colb[lane + 64 * b] = make_double2(v[b].re, v[b].im);  // own U_q[c]
+                    for (int b = 0; b < 16; b++) colb[lane + 64 * b] = make_double2(v[b].re, v[b].im);  // own U_q[c]
+                }
                 double2 *dst = quad_u<N>(a, cnt, cl, par, q, wave);
                 const __amdgpu_buffer_rsrc_t ru = make_rsrc(dst);
                 if (!(QUAD_TSKIP & 32))
