@@ -53,7 +53,7 @@ def test_latency_equals_throughput_kernel_and_oracle(orc, keys_2_2, eng):
     cts = _edge_batch(keys_2_2, BIG, 41)
     idx = (np.arange(BIG) * 5 % 3).astype(np.uint32)
     thr, ran = _ran(eng, lambda: eng.programmable_bootstrap(cts, luts, lut_indexes=idx))  # throughput kernel
-    assert ran == {"pbs_classic_kernel"}, ran
+    assert "pbs_classic_kernel" in ran, ran  # (the host pipeline's ragged last chunk may take the latency kernel)
     lat, ran = _ran(eng, lambda: eng.programmable_bootstrap(cts[:SMALL], luts, lut_indexes=idx[:SMALL]))
     assert ran == {"pbs_latency_kernel"}, ran
     assert np.array_equal(lat, thr[:SMALL]), f"{np.count_nonzero(lat != thr[:SMALL])} words differ"
@@ -121,7 +121,7 @@ def test_mb_latency_equals_throughput_kernel_and_oracle(orc, mb_keys, g):
     cts = _edge_batch(keys, BIG, 47 + g)
     idx = (np.arange(BIG) * 5 % 3).astype(np.uint32)
     thr, ran = _ran(e, lambda: e.programmable_bootstrap(cts, luts, lut_indexes=idx))
-    assert ran == {"pbs_multibit"}, ran
+    assert "pbs_multibit" in ran, ran
     lat, ran = _ran(e, lambda: e.programmable_bootstrap(cts[:SMALL], luts, lut_indexes=idx[:SMALL]))
     assert ran == {"pbs_mb_latency_kernel"}, ran
     assert np.array_equal(lat, thr[:SMALL]), f"{np.count_nonzero(lat != thr[:SMALL])} words differ"
