@@ -42,7 +42,14 @@
  *     3/8 / 5/8 of the CU count (96 / 160 rows on 256 CUs) run the on-chip CMUX (the whole blind
  *     rotation in one workgroup per ciphertext, two per CU at N = 4096, no scratch used), smaller
  *     ones the split CMUX (same outputs; TFHE_MI355_ONCHIP_MIN = rows overrides,
- *     TFHE_MI355_ONCHIP=0 = never).
+ *     TFHE_MI355_ONCHIP=0 = never); at N = 8192, L = 2 batches of at most CUs / 4 rows run the quad
+ *     CMUX instead (four CUs per ciphertext exchanging sub-blocks every CMUX through the scratch;
+ *     same outputs; TFHE_MI355_QUAD_MAX = rows overrides, TFHE_MI355_QUAD=0 = never).  The quad
+ *     CMUX's workgroups wait on each other, so its launches are serialised per device within the
+ *     process; two PROCESSES running quad CMUX kernels on one GPU at once can starve each other's
+ *     workgroups -- the waits are bounded, and a synchronous call whose quad launch timed out
+ *     fails (rc 1, outputs invalid) instead of hanging (an _async call's failure is reported by
+ *     the context's next synchronous call); set TFHE_MI355_QUAD=0 where processes share a GPU.
  *     The _async calls hold no per-context mutable state: every device scratch buffer they
  *     need comes from the caller (d_scratch, sized by the matching *_scratch query; a call
  *     given less than its query fails with an error, and only a query returning 0 allows

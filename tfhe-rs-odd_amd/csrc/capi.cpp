@@ -256,6 +256,7 @@ struct TfheMi355Context {
     std::mutex lanes_mu;
     bool lanes_made = false;
     long lanes_mcus = 0, lanes_chunk = 0;  // TFHE_MI355_LANES_MCUS / _CHUNK at creation
+    DeviceBuffer quad_fail;  // one u32 the quad CMUX sets when a flag wait timed out (check_quad_fail)
     bool lanes_block = false;              // TFHE_MI355_LANES_MASK=block
     hipStream_t lane_c = nullptr, lane_m = nullptr;
     // Request coalescing of small host-pointer calls (the reference calls the PBS one ciphertext
@@ -627,6 +628,16 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
         a.onchip_min_count = (int)onchip_min(c);
         a.quad_pass = (int)(c->cus / 4);
         a.quad_max_count = (int)quad_max(c);
+        if (a.quad_max_count > 0 && count <= (size_t)a.quad_max_count) {
+            if (!c->quad_fail.ptr) {  // created zeroed at the first quad launch of the context
+                std::lock_guard<std::mutex> g(c->lanes_mu);
+                if (!c->quad_fail.ptr) {
+                    c->quad_fail.reserve(4);
+                    check(hipMemset(c->quad_fail.ptr, 0, 4), "quad fail word");
+                }
+            }
+            a.quad_fail = static_cast<uint32_t *>(c->quad_fail.ptr);
+        }
         if (large_lanes_on(c) && count > lanes_chunk(c)) {  // two chunks in flight at once
             make_lanes(c);
             a.lane_c = c->lane_c;
@@ -838,6 +849,20 @@ void lane_finish(TfheMi355Context::Lane &L, void *out, size_t out_words) {
         std::memcpy(static_cast<uint64_t *>(out) + L.first * out_words, L.h_out.ptr, L.count * out_words * 8);
 }
 
+// after a synchronous call's device work: a quad CMUX launch of this context whose flag wait timed
+// out (its partner workgroups never became resident -- e.g. another process's quad grid held the
+// CUs) left invalid outputs; fail the call loudly instead of returning them
+void check_quad_fail(TfheMi355Context *c) {
+    if (!c->quad_fail.ptr) return;
+    uint32_t v = 0;
+    check(hipMemcpy(&v, c->quad_fail.ptr, 4, hipMemcpyDeviceToHost), "quad fail word");
+    if (v) {
+        (void)hipMemset(c->quad_fail.ptr, 0, 4);
+        fail("quad CMUX: a workgroup waited in vain for its partners (is another process running quad CMUX "
+             "kernels on this GPU?); the outputs are invalid -- TFHE_MI355_QUAD=0 disables the quad CMUX");
+    }
+}
+
 void run_host_pipeline(TfheMi355Context *c, const uint64_t *in, size_t in_words, uint64_t *out, size_t out_words,
                        const uint64_t *luts, size_t lut_words, size_t lut_count, const uint32_t *idx, size_t count,
                        ChunkLaunch launch, ScratchSize scratch_size) {
@@ -905,6 +930,7 @@ void run_host_pipeline(TfheMi355Context *c, const uint64_t *in, size_t in_words,
             lane_finish(a, out, out_words);
             lane_finish(b, out, out_words);
         }
+        check_quad_fail(c);
     } catch (...) {
         (void)hipStreamSynchronize(cs);
         for (auto &L : c->lanes) {
@@ -1069,6 +1095,7 @@ void run_coalesced_batch(TfheMi355Context *c, TfheMi355Context::Coalescer::Slot 
              scratch ? sl.d_scratch.ptr : nullptr, scratch ? sl.d_scratch.bytes : 0, s);
     check(hipMemcpyAsync(sl.h_out.ptr, sl.d_out.ptr, total * d.out_words * 8, hipMemcpyDeviceToHost, s), "D2H batch");
     check(hipStreamSynchronize(s), "batch sync");
+    check_quad_fail(c);
     rows = 0;
     int deferred = 0;
     for (auto *r : batch) {

@@ -194,6 +194,7 @@ struct LargePbsLaunch {
     // of at most quad_max_count ciphertexts, quad_pass ciphertexts per launch (CUs / R: one workgroup
     // per CU, all resident at once); 0 = never
     int quad_pass = 0, quad_max_count = 0;
+    uint32_t *quad_fail = nullptr;  // device word set by a quad workgroup whose partners never arrived
 };
 bool large_pbs_supported(int N, int k, int L);
 bool large_multibit_supported(int N, int k, int L, int g);

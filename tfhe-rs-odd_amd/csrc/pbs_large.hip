@@ -2407,10 +2407,15 @@ __global__ void __launch_bounds__(512, 1) quad_cmux_kernel(LargePbsLaunch a, int
                                __HIP_MEMORY_SCOPE_AGENT);
             for (int p = 0; p < ((QUAD_TSKIP & 1) ? 0 : R); p++) {
                 const uint32_t *f = flags + p * (Cfg::FLAG_BYTES / 4);
-                for (uint32_t spin = 0; spin < QUAD_SPIN_MAX; spin++) {
+                uint32_t spin = 0;
+                for (; spin < QUAD_SPIN_MAX; spin++) {
                     if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (uint32_t)(i + 1)) break;
                     __builtin_amdgcn_s_sleep(1);
                 }
+                // a partner that never arrived (the device's CUs held by another process's quad grid):
+                // the outputs are invalid -- recorded for the host (tfhe_mi355 fails the call), no hang
+                if (spin == QUAD_SPIN_MAX && a.quad_fail)
+                    __hip_atomic_store(a.quad_fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         __syncthreads();
