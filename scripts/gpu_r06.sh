@@ -54,7 +54,10 @@ for s in ${STAGES:-tests smoke bench}; do
           done
         done ;;
     kt) for t in ${KT_TAGS:-2_2}; do
-          if [ "$t" = lat ]; then
+          if [ "$t" = quad ]; then  # the quad CMUX: single 3_3 KS+PBS calls of 1 and 64 rows
+            step r06_kt_quad 300 env PROBE_PARAMS=PARAM_MESSAGE_3_CARRY_3_KS_PBS rocprofv3 --kernel-trace --stats \
+              -d gpurun_out/kt_quad -o run --output-format csv -- python3 scripts/single_call_probe.py 5 1,64
+          elif [ "$t" = lat ]; then
             step r06_kt_lat 300 rocprofv3 --kernel-trace --stats -d gpurun_out/kt_lat -o run --output-format csv -- \
               python3 scripts/latency_probe.py 1,64,256
           else
