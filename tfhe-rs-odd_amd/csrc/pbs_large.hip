@@ -1735,14 +1735,16 @@ struct OnchipCfg {
 #ifndef ONCHIP_PF
 #define ONCHIP_PF 4  // MAC slots whose GGSW operands are issued before the publish barrier (0: none)
 #endif
-// N = 8192, L = 2 (3_3): 5 slots before the barrier, then regions of 3 -- since the sub-block
-// rotation, 10.75-10.78k -> 11.34-11.37k KS+PBS/s against 4 / 4 (profiles/r05_ab_onchip_pfsb*.log;
-// the other shapes measured best at 4 / 4)
+// N = 8192, L = 2 (3_3): 6 slots before the barrier, then regions of 4 -- round 5 (with the spilling
+// build) measured 5 / 3 best (10.75-10.78k -> 11.34-11.37k KS+PBS/s against 4 / 4,
+// profiles/r05_ab_onchip_pfsb*.log); re-swept after the exchange addresses stopped spilling (round 6,
+// profiles/r06_ab_onchip_pfsb.txt): 5 / 3 12.02-12.03k, 6 / 4 12.27k, 6 / 3 12.26k, 8 / 4 12.20k,
+// 7 / 3 12.18k, 5 / 4 12.10-12.11k, 4 / 4 12.08k (the other shapes measured best at 4 / 4)
 #ifndef ONCHIP_PF_8192_L2
-#define ONCHIP_PF_8192_L2 5
+#define ONCHIP_PF_8192_L2 6
 #endif
 #ifndef ONCHIP_MAC_SB_8192_L2
-#define ONCHIP_MAC_SB_8192_L2 3
+#define ONCHIP_MAC_SB_8192_L2 4
 #endif
 template <int M, int L>
 constexpr int onchip_pf() { return M == 4096 && L == 2 ? ONCHIP_PF_8192_L2 : ONCHIP_PF; }
