@@ -1806,6 +1806,26 @@ __device__ __forceinline__ void onchip_decompose(uint64_t x, int beta, int32_t (
     }
 }
 
+#ifndef ONCHIP_DIGIT2
+#define ONCHIP_DIGIT2 1  // 0: two decomp_digit32 per value (A/B of Digit2, pbs_common.h)
+#endif
+// both levels of the values at j and j + M as the int16 quad the top DIF reads: level L at j, j + M
+// in the low dword, level L-1 in the high dword
+template <bool D32>
+__device__ __forceinline__ uint64_t onchip_pack2(uint64_t v0, uint64_t v1, int beta, const Digit2 &dg2) {
+    if constexpr (D32 && ONCHIP_DIGIT2) {
+        uint32_t lv0, lv1;
+        dg2.pair((uint32_t)(v0 >> 32), (uint32_t)(v1 >> 32), lv0, lv1);
+        return (uint64_t)lv0 | ((uint64_t)lv1 << 32);
+    } else {
+        int32_t e0[2], e1[2];
+        onchip_decompose<D32>(v0, beta, e0);
+        onchip_decompose<D32>(v1, beta, e1);
+        return ((uint64_t)((uint32_t)e0[0] & 0xffffu)) | ((uint64_t)((uint32_t)e1[0] & 0xffffu) << 16) |
+               ((uint64_t)((uint32_t)e0[1] & 0xffffu) << 32) | ((uint64_t)((uint32_t)e1[1] & 0xffffu) << 48);
+    }
+}
+
 // L = 1: the one signed digit (decompose64<1>; 32-bit when base_log <= 30)
 template <bool D32>
 __device__ __forceinline__ int32_t onchip_decompose1(uint64_t x, int beta) {
@@ -1896,6 +1916,7 @@ __global__ void __launch_bounds__(OnchipCfg<N>::THREADS, OnchipCfg<N>::MIN_WPS /
     }
     const double k32 = torus_k32();
     const int beta = a.base_log;
+    const Digit2 dg2(D32 ? beta : 2);  // (unused unless D32)
     // accumulator pair (row r, j) <-> LDS slot (2 (j >> 10) + r) BUF + (j & 1023): the slots thread t
     // owns, (2 b + r) BUF + t + 512 h, are exactly the top-stage / top-inverse slots of its butterflies,
     // so the top inverse writes the updated pairs in place (no barrier between its reads and them)
@@ -1929,12 +1950,8 @@ __global__ void __launch_bounds__(OnchipCfg<N>::THREADS, OnchipCfg<N>::MIN_WPS /
                     const uint64_t x0 = swap ? rot.y : rot.x, x1 = swap ? rot.x : rot.y;
                     const bool neg0 = (jj0 < 0) != full_odd, neg1 = (jj0 + M < 0) != full_odd;
                     if constexpr (L == 2) {
-                        int32_t e0[2], e1[2];
-                        onchip_decompose<D32>((neg0 ? 0 - x0 : x0) - lo[r][h][b], beta, e0);
-                        onchip_decompose<D32>((neg1 ? 0 - x1 : x1) - hi[r][h][b], beta, e1);
-                        pk[r][h][b] = ((uint64_t)((uint32_t)e0[0] & 0xffffu)) | ((uint64_t)((uint32_t)e1[0] & 0xffffu) << 16) |
-                                      ((uint64_t)((uint32_t)e0[1] & 0xffffu) << 32) |
-                                      ((uint64_t)((uint32_t)e1[1] & 0xffffu) << 48);
+                        pk[r][h][b] = onchip_pack2<D32>((neg0 ? 0 - x0 : x0) - lo[r][h][b], (neg1 ? 0 - x1 : x1) - hi[r][h][b],
+                                                        beta, dg2);
                     } else {  // one level: |digit| <= 2^(beta - 1) (2^21 at base 2^22) -- two int32 fields
                         const int32_t e0 = onchip_decompose1<D32>((neg0 ? 0 - x0 : x0) - lo[r][h][b], beta);
                         const int32_t e1 = onchip_decompose1<D32>((neg1 ? 0 - x1 : x1) - hi[r][h][b], beta);
@@ -2112,6 +2129,9 @@ static bool onchip_enabled() {
                      // per-sub-block branch serialises the U loads: 13.07-13.68 vs 12.63 ms per call
                      // (profiles/r06_quad_ab.txt)
 #endif
+#ifndef QUAD_PKFENCE
+#define QUAD_PKFENCE 1  // the digits computed before the barrier that ends the rotation
+#endif
 #ifndef QUAD_TSKIP
 #define QUAD_TSKIP 0  // timing-only builds (wrong outputs): 1 no flag wait, 2 no forward sub-FFTs, 4 no inverse
                       // sub-FFTs, 8 no GGSW loads, 16 no U loads, 32 no U stores
@@ -2218,6 +2238,7 @@ __global__ void __launch_bounds__(512, 1) quad_cmux_kernel(LargePbsLaunch a, int
     }
     const double k32 = torus_k32();
     const int beta = a.base_log;
+    const Digit2 dg2(D32 ? beta : 2);  // (unused unless D32)
     auto pslot = [&](int r, int j) { return (2 * (j >> 10) + r) * BUF + (j & 1023); };
     auto store_pairs = [&]() {
 #pragma unroll
@@ -2277,12 +2298,10 @@ __global__ void __launch_bounds__(512, 1) quad_cmux_kernel(LargePbsLaunch a, int
                     const bool swap = jj0 < 0 && jj0 >= -M;
                     const uint64_t x0 = swap ? rot.y : rot.x, x1 = swap ? rot.x : rot.y;
                     const bool neg0 = (jj0 < 0) != full_odd, neg1 = (jj0 + M < 0) != full_odd;
-                    int32_t e0[2], e1[2];
-                    onchip_decompose<D32>((neg0 ? 0 - x0 : x0) - lo[r][h][b], beta, e0);
-                    onchip_decompose<D32>((neg1 ? 0 - x1 : x1) - hi[r][h][b], beta, e1);
-                    pk[r][h][b] = ((uint64_t)((uint32_t)e0[0] & 0xffffu)) | ((uint64_t)((uint32_t)e1[0] & 0xffffu) << 16) |
-                                  ((uint64_t)((uint32_t)e0[1] & 0xffffu) << 32) |
-                                  ((uint64_t)((uint32_t)e1[1] & 0xffffu) << 48);
+                    pk[r][h][b] = onchip_pack2<D32>((neg0 ? 0 - x0 : x0) - lo[r][h][b], (neg1 ? 0 - x1 : x1) - hi[r][h][b],
+                                                    beta, dg2);
+                    if (QUAD_PKFENCE) asm volatile("" : "+v"(pk[r][h][b]));  // digits before the barrier: 32
+                                                                            // registers live across it, not 64
                 }
         stamp(i, 2);
         __syncthreads();  // the pairs are read: the region becomes the spectra
