@@ -190,7 +190,7 @@ struct Digit2 {
             const uint32_t a = __builtin_amdgcn_ubfe(y, s0, beta);
             const uint32_t z0 = a + (y >> 31) + hm1;
             const uint32_t c = __builtin_amdgcn_ubfe(z0, beta, 1);
-            d0[e] = a + c * (uint32_t)nb;
+            d0[e] = a + (uint32_t)__mul24((int)c, nb);  // v_mad_i32_i24 (c is 0 or 1, nb = -2^beta)
             z1[e] = (y >> s1) + c + hm1;
         }
         lv0 = __builtin_amdgcn_perm(d0[1], d0[0], 0x05040100u);

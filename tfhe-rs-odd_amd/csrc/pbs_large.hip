@@ -2129,6 +2129,9 @@ static bool onchip_enabled() {
                      // per-sub-block branch serialises the U loads: 13.07-13.68 vs 12.63 ms per call
                      // (profiles/r06_quad_ab.txt)
 #endif
+#ifndef QUAD_PPOLL
+#define QUAD_PPOLL 1  // the R exchange flags polled by R lanes at once (0: lane 0 polls them in turn)
+#endif
 #ifndef QUAD_PKFENCE
 #define QUAD_PKFENCE 1  // the digits computed before the barrier that ends the rotation
 #endif
@@ -2423,7 +2426,21 @@ __global__ void __launch_bounds__(512, 1) quad_cmux_kernel(LargePbsLaunch a, int
         __syncthreads();  // U_q stored and drained by both storing waves
         stamp(i, 9);
         // ---- exchange: the R workgroups' U of CMUX i ----
-        if (t == 0) {
+        if (QUAD_PPOLL && wave == 0) {
+            // lanes 0..R-1 poll the R flags together: one L2 round trip per poll instead of R in turn
+            if (lane == 0)
+                __hip_atomic_store(flags + q * (Cfg::FLAG_BYTES / 4), (uint32_t)(i + 1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t *f = flags + (lane < R ? lane : 0) * (Cfg::FLAG_BYTES / 4);
+            uint32_t spin = 0;
+            for (; spin < ((QUAD_TSKIP & 1) ? 0u : QUAD_SPIN_MAX); spin++) {
+                const uint32_t v = lane < R ? __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
+                if (__all(v >= (uint32_t)(i + 1))) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (spin == QUAD_SPIN_MAX && lane == 0 && a.quad_fail)
+                __hip_atomic_store(a.quad_fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (!QUAD_PPOLL && t == 0) {
             __hip_atomic_store(flags + q * (Cfg::FLAG_BYTES / 4), (uint32_t)(i + 1), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
             for (int p = 0; p < ((QUAD_TSKIP & 1) ? 0 : R); p++) {
