@@ -132,8 +132,8 @@ def _split_params():
         out[f"mb3_3g{g}"] = (name, f"shortint apply_lookup_table (keyswitch -> multi-bit PBS, grouping {g}) at {name} "
                                    f"(shortint/parameters/multi_bit.rs:{line}), N={p.polynomial_size}, batch per GPU; "
                                    "the reference publishes no number for this set",
-                             (f"large_mb_pair2_kernel<{p.polynomial_size},{g}> (+ large_mb_inv_fwd per group, "
-                              "ks_mfma_kernel)" if os.environ.get("TFHE_MI355_MB_PAIR2", "1") != "0" else
+                             (f"large_mb_pair2_kernel<{p.polynomial_size},{g}> (+ large_mb_inv_fwd per group: packed "
+                              "digits in, twist + top DIF in the pair kernel; ks_mfma_kernel)" if os.environ.get("TFHE_MI355_MB_PAIR2", "1") != "0" else
                               f"large_pair_sub_kernel<{p.polynomial_size},1,{p.pbs_level},{g},1> (+ large_top_fwd/top_inv "
                               "per group, ks_mfma_kernel)"))
     return out
@@ -288,6 +288,11 @@ def split_dsub_flops(p) -> float:
     return k1 * L * (6 * M + 5 * M * math.log2(R)) + split_sub_flops(p)
 
 
+def mb_digits_on() -> bool:
+    """The multi-bit pair kernel reads packed digits (pbs_large.hip mb_dig) unless switched off."""
+    return all(os.environ.get(v, "1") != "0" for v in ("TFHE_MI355_MB_DIGITS", "TFHE_MI355_MB_FUSED", "TFHE_MI355_MB_PAIR2"))
+
+
 def split_chunk(p, units: int) -> int:
     """Ciphertexts per pass of the split CMUX (capi.cpp large_chunk)."""
     if p.polynomial_size >= 32768:
@@ -328,7 +333,9 @@ def roofline(tag, p, units_per_launch: int, step_ms: float, kname: str, with_ks:
     else:  # one launch per step (or a replayed graph): the step's own events
         kernel_ms, timed = step_ms, None
         kernel_src = "HIP events around the whole step on the launch stream (no per-kernel timer)"
-    dsub = large and fam == "large_dsub_kernel"
+    # digits-fed kernels (the twist + top radix-R share inside): large_dsub, and the multi-bit pair kernel
+    # unless TFHE_MI355_MB_DIGITS=0 / TFHE_MI355_MB_FUSED=0
+    dsub = large and (fam == "large_dsub_kernel" or (fam == "large_mb_pair2_kernel" and mb_digits_on()))
     flop_launch = ((large_group_flops(p) if grouped else split_dsub_flops(p) if dsub else split_sub_flops(p)) * chunk
                    if large else steps_flop)
     fp64 = flop_launch / (kernel_ms * 1e-3) / 1e12

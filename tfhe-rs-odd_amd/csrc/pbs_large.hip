@@ -822,6 +822,66 @@ __global__ void __launch_bounds__((PairSubCfg<K, L>::THREADS), 2) large_pair_sub
 #define MB2_TSKIP 0  // timing-only builds (wrong outputs): 1 no GGSW loads, 2 no forward sub-FFTs, 4 no
                      // inverse sub-FFTs, 8 no keybundle sums (PBS_MB_TSKIP_MONO=1: conflict-free monomials)
 #endif
+// top DIF output Q of butterfly a0 for both rows and levels -> spectra buffers p = (lvl - 1) 2 + r
+// (tv[h][b] = twist[a0 + 1024 b], wq[h] = W[a0 Q], loaded by the caller ahead of the barrier)
+template <int N, int Q, int H>
+__device__ __forceinline__ void quad_top(double2 *lds, const uint64_t (&pk)[2][H][Split<N>::R],
+                                         const cx (&tvh)[H][Split<N>::R], const cx (&wqh)[H], int t) {
+    constexpr int R = Split<N>::R, BUF = SubFft::XL;
+#pragma unroll
+    for (int h = 0; h < H; h++) {
+        const int a0 = t + 512 * h;
+        const cx *tv = tvh[h];
+        const cx wq = wqh[h];
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int li = 0; li < 2; li++) {  // li = 0: level L, 1: level L-1
+                cx u[R];
+#pragma unroll
+                for (int b = 0; b < R; b++) {
+                    const uint64_t w = pk[r][h][b] >> (32 * li);
+                    const int32_t d0 = (int32_t)(int16_t)(w & 0xffffu), d1 = (int32_t)(int16_t)((w >> 16) & 0xffffu);
+                    u[b] = cmulw(cx{(double)d0, (double)d1}, tv[b].re, tv[b].im);
+                }
+                dftR_fwd<R>(u);
+                const cx y = Q ? cmulw(u[Q], wq.re, wq.im) : u[0];
+                const int p = (1 - li) * 2 + r;  // level L -> 2, 3; level L-1 -> 0, 1
+                lds[p * BUF + a0] = make_double2(y.re, y.im);
+            }
+    }
+}
+
+// MB2_DIGITS: the multi-bit step's input as packed int16 digits (the quad / on-chip word: level L at
+// j, j + M in the low dword, level L-1 in the high dword), row r at [r M + j], in the level-2
+// spectra slots of the ciphertext (the pair kernel's outputs go to the level-1 slots)
+template <int N>
+__device__ __forceinline__ uint64_t *mb_digits(const LargePbsLaunch &a, int cl) {
+    constexpr int M = Split<N>::M;
+    return reinterpret_cast<uint64_t *>(a.spectra + ((size_t)cl * 4 + 2) * M);
+}
+
+// digits of group 0 (the initial accumulator; multi-bit: no rotation), thread per (ct, row, t < 1024)
+template <int N>
+__global__ void __launch_bounds__(256) mb_digits_init_kernel(LargePbsLaunch a, int ct0) {
+    constexpr int M = Split<N>::M, R = Split<N>::R;
+    (void)ct0;
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    const int cl = e / 2048, r = (e >> 10) & 1, t = e & 1023;
+    if (cl >= a.chunk_count) return;
+    const Digit2 dg2(a.base_log);
+    const uint64_t *acc = a.acc + ((size_t)cl * 2 + r) * N;
+    uint64_t *dg = mb_digits<N>(a, cl) + (size_t)r * M;
+#pragma unroll
+    for (int b = 0; b < R; b++) {
+        const int j = t + 1024 * b;
+        const acc_pair self = *reinterpret_cast<const acc_pair *>(acc + 2 * j);
+        uint32_t lv0, lv1;
+        dg2.pair((uint32_t)(self.x >> 32), (uint32_t)(self.y >> 32), lv0, lv1);
+        dg[j] = (uint64_t)lv0 | ((uint64_t)lv1 << 32);
+    }
+}
+
 template <int N, int G>
 struct MbPair2Cfg {
     static constexpr int K = 1, L = 2, CPW = 2, PW = (K + 1) * L, WAVES = CPW * PW, THREADS = 64 * WAVES;
@@ -835,7 +895,7 @@ struct MbPair2Cfg {
     static_assert(LDS <= 160 * 1024, "LDS per workgroup exceeds a CU");
 };
 
-template <int N, int G>
+template <int N, int G, bool DIG>
 __global__ void __launch_bounds__((MbPair2Cfg<N, G>::THREADS), 2) large_mb_pair2_kernel(LargePbsLaunch a, int ct0, int i) {
     using Cfg = MbPair2Cfg<N, G>;
     using S = Split<N>;
@@ -864,7 +924,46 @@ __global__ void __launch_bounds__((MbPair2Cfg<N, G>::THREADS), 2) large_mb_pair2
     // ---- phase 1: forward sub-FFT of polynomial p of ciphertext c (spectrum stays in registers) ----
     const int c1 = wave / PW, p1 = wave % PW;
     cx v[16];
-    {
+    if constexpr (DIG) {
+        // the top DIF output q of both ciphertexts' four polynomials, from their packed digits
+        // (quad_top: twist, dftR_fwd, times W[a0 q] -- top_fwd_body's operations), thread t serving
+        // butterflies a0 = t + 512 h -> the waves' exchange blocks in the natural layout
+        const int t = threadIdx.x;
+        cx tvh[2][R], wqh[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+#pragma unroll
+            for (int b = 0; b < R; b++) tvh[h][b] = gld(a.twist + t + 512 * h + 1024 * b);
+            wqh[h] = q ? gld(a.wtop + (q - 1) * 1024 + t + 512 * h) : cx{1.0, 0.0};
+        }
+#pragma unroll
+        for (int c = 0; c < CPW; c++) {
+            const uint64_t *dg = mb_digits<N>(a, ct_of(c));
+            uint64_t pk[2][2][R];
+#pragma unroll
+            for (int r = 0; r < 2; r++)
+#pragma unroll
+                for (int h = 0; h < 2; h++)
+#pragma unroll
+                    for (int b = 0; b < R; b++) pk[r][h][b] = dg[r * M + t + 512 * h + 1024 * b];
+            double2 *blk = lds + c * PW * SubFft::XL;
+            switch (q) {
+                case 0: quad_top<N, 0, 2>(blk, pk, tvh, wqh, t); break;
+                case 1: quad_top<N, 1, 2>(blk, pk, tvh, wqh, t); break;
+                case 2: quad_top<N, 2, 2>(blk, pk, tvh, wqh, t); break;
+                default: quad_top<N, 3, 2>(blk, pk, tvh, wqh, t); break;
+            }
+        }
+        __syncthreads();  // twiddle table, every exchange block filled
+        cx *xb = reinterpret_cast<cx *>(lds) + wave * SubFft::XL;
+#pragma unroll
+        for (int b = 0; b < 16; b++) {
+            const double2 y = reinterpret_cast<const double2 *>(xb)[lane + 64 * b];
+            v[b] = cx{y.x, y.y};
+        }
+        wsync();
+        if (!(MB2_TSKIP & 2)) SubFft::forward(v, xb, tw, lane, wsync);
+    } else {
         const double2 *src = spectra(c1) + (size_t)p1 * M + 1024 * q + lane;
 #pragma unroll
         for (int b = 0; b < 16; b++) v[b] = gld(src + 64 * b);
@@ -1036,6 +1135,16 @@ __global__ void __launch_bounds__((MbPair2Cfg<N, G>::THREADS), 2) large_mb_pair2
     if (2 * cp + c >= cnt) return;
     double2 *dst = spectra(c) + (size_t)col * M + 1024 * q + lane;  // (lvl 1, row col) slot: this WG only
     store_sub_out<LARGE_SUB_AUX>(dst, v, lane);
+}
+
+// TFHE_MI355_MB_DIGITS=0: the multi-bit pair kernel reads f64 spectra from large_top_fwd /
+// large_mb_inv_fwd instead of packed digits (A/B)
+static bool mb_digits_enabled() {
+    static const bool v = [] {
+        const char *e = std::getenv("TFHE_MI355_MB_DIGITS");
+        return !(e && e[0] == '0');
+    }();
+    return v;
 }
 
 static bool mb_pair2_enabled() {
@@ -1496,7 +1605,7 @@ __device__ __forceinline__ void top_inv_body(const LargePbsLaunch &a, int cl, in
 // extraction).  Per ciphertext and group: 384 KiB (U in, spectra out) instead of 640 KiB (top_inv's
 // accumulator write and top_fwd's read), and one launch fewer.  Same operations on the same values
 // as the two kernels, so bit-identical.  TFHE_MI355_MB_FUSED=0: the separate launches (A/B).
-template <int N, int K, int L, int G>
+template <int N, int K, int L, int G, bool DIG>
 __global__ void __launch_bounds__(TOPT, (top_fwd_wpe<N, L>())) large_mb_inv_fwd_kernel(LargePbsLaunch a, int ct0, int i) {
     static_assert(G > 0, "multi-bit only (the classic CMUX rotates between the two)");
     using S = Split<N>;
@@ -1524,6 +1633,19 @@ __global__ void __launch_bounds__(TOPT, (top_fwd_wpe<N, L>())) large_mb_inv_fwd_
     uint64_t lo[R], hi[R];
 #pragma unroll
     for (int b = 0; b < R; b++) backward_convert(u[b], tw[b], lo[b], hi[b], k32);
+    if constexpr (DIG) {
+        // MB2_DIGITS: group i + 1's packed digits; the pair kernel does the twist + top DIF
+        static_assert(N == 8192 && K == 1 && L == 2, "pair kernel shape");
+        const Digit2 dg2(a.base_log);
+        uint64_t *dg = mb_digits<N>(a, cl) + (size_t)r * M;
+#pragma unroll
+        for (int b = 0; b < R; b++) {
+            uint32_t lv0, lv1;
+            dg2.pair((uint32_t)(lo[b] >> 32), (uint32_t)(hi[b] >> 32), lv0, lv1);
+            dg[t + 1024 * b] = (uint64_t)lv0 | ((uint64_t)lv1 << 32);
+        }
+        return;
+    }
     // ---- large_top_fwd of group i + 1, row r, butterfly t (top_fwd_body, G > 0) ----
     const int beta = a.base_log;
     uint64_t pk[L > 1 ? R : 1];
@@ -2160,36 +2282,6 @@ __device__ __forceinline__ double2 *quad_u(const LargePbsLaunch &a, int cnt, int
     using Cfg = QuadCfg<N>;
     char *base = reinterpret_cast<char *>(a.scratch) + (size_t)cnt * Cfg::R * Cfg::FLAG_BYTES;
     return reinterpret_cast<double2 *>(base + (size_t)ct * Cfg::U_BYTES) + ((size_t)(par * Cfg::R + q) * 2 + c) * 1024;
-}
-
-// top DIF output Q of butterfly a0 for both rows and levels -> spectra buffers p = (lvl - 1) 2 + r
-// (tv[h][b] = twist[a0 + 1024 b], wq[h] = W[a0 Q], loaded by the caller ahead of the barrier)
-template <int N, int Q, int H>
-__device__ __forceinline__ void quad_top(double2 *lds, const uint64_t (&pk)[2][H][Split<N>::R],
-                                         const cx (&tvh)[H][Split<N>::R], const cx (&wqh)[H], int t) {
-    constexpr int R = Split<N>::R, BUF = SubFft::XL;
-#pragma unroll
-    for (int h = 0; h < H; h++) {
-        const int a0 = t + 512 * h;
-        const cx *tv = tvh[h];
-        const cx wq = wqh[h];
-#pragma unroll
-        for (int r = 0; r < 2; r++)
-#pragma unroll
-            for (int li = 0; li < 2; li++) {  // li = 0: level L, 1: level L-1
-                cx u[R];
-#pragma unroll
-                for (int b = 0; b < R; b++) {
-                    const uint64_t w = pk[r][h][b] >> (32 * li);
-                    const int32_t d0 = (int32_t)(int16_t)(w & 0xffffu), d1 = (int32_t)(int16_t)((w >> 16) & 0xffffu);
-                    u[b] = cmulw(cx{(double)d0, (double)d1}, tv[b].re, tv[b].im);
-                }
-                dftR_fwd<R>(u);
-                const cx y = Q ? cmulw(u[Q], wq.re, wq.im) : u[0];
-                const int p = (1 - li) * 2 + r;  // level L -> 2, 3; level L-1 -> 0, 1
-                lds[p * BUF + a0] = make_double2(y.re, y.im);
-            }
-    }
 }
 
 template <int N, bool D32>
@@ -2904,8 +2996,14 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
         const unsigned sub_blocks = (unsigned)cnt * S::R;
         const int steps = G ? a.n / G : a.n;  // CMUXes, or multi-bit groups
         const bool mb_fused = G > 0 && mb_fused_enabled();  // top_inv of group i + top_fwd of i + 1
+        // packed digits between the fused inverse and the pair kernel (MB2_DIGITS)
+        const bool mb_dig = N == 8192 && K == 1 && L == 2 && mb_fused && mb_pair2_enabled() && mb_digits_enabled() &&
+                            a.base_log * 2 <= 30;
         for (int i = 0; i < steps; i++) {
-            if (i == 0 || !mb_fused) {
+            if (i == 0 && mb_dig) {
+                TimedLaunch tl(a.timer, "mb_digits_init_kernel", s);
+                hipLaunchKernelGGL((mb_digits_init_kernel<N>), dim3((unsigned)cnt * 8), dim3(256), 0, s, a, ct0);
+            } else if (i == 0 || !mb_fused) {
                 TimedLaunch tl(a.timer, "large_top_fwd_kernel", s);
                 hipLaunchKernelGGL((large_top_fwd_kernel<N, K, L, G>), dim3(fwd_blocks), dim3(TOPT), 0, s, a, ct0, i);
             }
@@ -2919,8 +3017,12 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
                     if (mb_pair2_enabled()) {
                         using P2 = MbPair2Cfg<N, G>;
                         TimedLaunch tl(a.timer, "large_mb_pair2_kernel", s);
-                        hipLaunchKernelGGL((large_mb_pair2_kernel<N, G>), dim3(pair_sub_blocks<S::R>((cnt + 1) / 2)),
-                                           dim3(P2::THREADS), P2::LDS, s, a, ct0, i);
+                        if (mb_dig)
+                            hipLaunchKernelGGL((large_mb_pair2_kernel<N, G, true>), dim3(pair_sub_blocks<S::R>((cnt + 1) / 2)),
+                                               dim3(P2::THREADS), P2::LDS, s, a, ct0, i);
+                        else
+                            hipLaunchKernelGGL((large_mb_pair2_kernel<N, G, false>), dim3(pair_sub_blocks<S::R>((cnt + 1) / 2)),
+                                               dim3(P2::THREADS), P2::LDS, s, a, ct0, i);
                         pair2 = true;
                     }
                 }
@@ -2950,8 +3052,17 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
             if constexpr (G > 0) {
                 if (mb_fused && i + 1 < steps) {
                     TimedLaunch tl(a.timer, "large_mb_inv_fwd_kernel", s);
-                    hipLaunchKernelGGL((large_mb_inv_fwd_kernel<N, K, L, G>), dim3(fwd_blocks), dim3(TOPT), 0, s, a,
-                                       ct0, i);
+                    bool dig_done = false;
+                    if constexpr (N == 8192 && K == 1 && L == 2) {
+                        if (mb_dig) {
+                            hipLaunchKernelGGL((large_mb_inv_fwd_kernel<N, K, L, G, true>), dim3(fwd_blocks), dim3(TOPT), 0,
+                                               s, a, ct0, i);
+                            dig_done = true;
+                        }
+                    }
+                    if (!dig_done)
+                        hipLaunchKernelGGL((large_mb_inv_fwd_kernel<N, K, L, G, false>), dim3(fwd_blocks), dim3(TOPT), 0,
+                                           s, a, ct0, i);
                     continue;
                 }
             }
