@@ -195,7 +195,7 @@ def pbs_flops(p) -> float:
 
 
 PMC_ALIAS = {"mul32": "2_2ks"}  # the multiply DAG runs the 2_2 KS+PBS kernels: per-PBS traffic of that workload
-PMC_ROUNDS = ("r06", "r05", "r04", "r03")  # newest committed PMC summary first (kernels unchanged since are still described by it)
+PMC_ROUNDS = ("r06b", "r06", "r05", "r04", "r03")  # newest committed PMC summary first (kernels unchanged since are still described by it)
 
 # dominant kernel of each workload: (kernel-timer family, rocprofv3 name normalised as
 # scripts/pmc_workload.py does).  Its average duration comes from the engine's HIP-event timer
