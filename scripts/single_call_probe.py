@@ -23,8 +23,13 @@ def main():
     P = ALL[os.environ.get("PROBE_PARAMS", "PARAM_MESSAGE_2_CARRY_2_KS_PBS")]
     lwe_sk = client.gen_binary_key(3, 1, P.lwe_dimension)
     glwe_sk = client.gen_binary_key(3, 2, P.big_lwe_dimension)
-    bsk = client.gen_bootstrap_key(4, lwe_sk, glwe_sk, P.glwe_dimension, P.polynomial_size, P.pbs_base_log,
-                                   P.pbs_level, P.glwe_modular_std_dev)
+    if P.grouping_factor:
+        bsk = client.gen_multi_bit_bootstrap_key(4, lwe_sk, glwe_sk, P.glwe_dimension, P.polynomial_size,
+                                                 P.pbs_base_log, P.pbs_level, P.grouping_factor,
+                                                 P.glwe_modular_std_dev)
+    else:
+        bsk = client.gen_bootstrap_key(4, lwe_sk, glwe_sk, P.glwe_dimension, P.polynomial_size, P.pbs_base_log,
+                                       P.pbs_level, P.glwe_modular_std_dev)
     ksk = client.gen_keyswitch_key(6, glwe_sk, lwe_sk, P.ks_base_log, P.ks_level, P.lwe_modular_std_dev)
     eng = Engine(P, 0)
     eng.upload_bootstrap_key(bsk)

@@ -809,6 +809,9 @@ __global__ void __launch_bounds__((PairSubCfg<K, L>::THREADS), 2) large_pair_sub
 // 0..k) are those of the kernel above, so the outputs are bit-identical.  TFHE_MI355_MB_PAIR2=0
 // selects the kernel above (A/B).
 // ---------------------------------------------------------------------------------------
+#ifndef MB_DIGITS_MIN
+#define MB_DIGITS_MIN 128  // smallest chunk fed packed digits (TFHE_MI355_MB_DIGITS_MIN overrides; profiles/r06_mb_digits_min.txt)
+#endif
 #ifndef MB2_PIPE
 #define MB2_PIPE 1  // phase 2's GGSW operand batches software pipelined (0: one (level, column) batch at a time)
 #endif
@@ -1139,12 +1142,16 @@ __global__ void __launch_bounds__((MbPair2Cfg<N, G>::THREADS), 2) large_mb_pair2
 
 // TFHE_MI355_MB_DIGITS=0: the multi-bit pair kernel reads f64 spectra from large_top_fwd /
 // large_mb_inv_fwd instead of packed digits (A/B)
-static bool mb_digits_enabled() {
-    static const bool v = [] {
+// Chunks below TFHE_MI355_MB_DIGITS_MIN ciphertexts keep the spectra path: there the inverse kernel is
+// not bandwidth-bound and the pair kernel's top DIF sits on the critical path of every group
+static bool mb_digits_enabled(int cnt) {
+    static const int v = [] {
         const char *e = std::getenv("TFHE_MI355_MB_DIGITS");
-        return !(e && e[0] == '0');
+        if (e && e[0] == '0') return -1;
+        const char *m = std::getenv("TFHE_MI355_MB_DIGITS_MIN");
+        return m ? std::atoi(m) : MB_DIGITS_MIN;
     }();
-    return v;
+    return v >= 0 && cnt >= v;
 }
 
 static bool mb_pair2_enabled() {
@@ -2997,7 +3004,7 @@ static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
         const int steps = G ? a.n / G : a.n;  // CMUXes, or multi-bit groups
         const bool mb_fused = G > 0 && mb_fused_enabled();  // top_inv of group i + top_fwd of i + 1
         // packed digits between the fused inverse and the pair kernel (MB2_DIGITS)
-        const bool mb_dig = N == 8192 && K == 1 && L == 2 && mb_fused && mb_pair2_enabled() && mb_digits_enabled() &&
+        const bool mb_dig = N == 8192 && K == 1 && L == 2 && mb_fused && mb_pair2_enabled() && mb_digits_enabled(cnt) &&
                             a.base_log * 2 <= 30;
         for (int i = 0; i < steps; i++) {
             if (i == 0 && mb_dig) {
