@@ -56,20 +56,20 @@ for s in ${STAGES:-tests smoke bench}; do
     kt) for t in ${KT_TAGS:-2_2}; do
           if [ "$t" = quad ]; then  # the quad CMUX: single 3_3 KS+PBS calls of 1 and 64 rows
             step ${TAGR:-r06}_kt_quad 300 env PROBE_PARAMS=PARAM_MESSAGE_3_CARRY_3_KS_PBS rocprofv3 --kernel-trace --stats \
-              -d gpurun_out/kt_quad -o run --output-format csv -- python3 scripts/single_call_probe.py 5 1,64
+              -d gpurun_out/${TAGR:-r06}_kt_quad -o run --output-format csv -- python3 scripts/single_call_probe.py 5 1,64
           elif [ "$t" = lat ]; then
-            step ${TAGR:-r06}_kt_lat 300 rocprofv3 --kernel-trace --stats -d gpurun_out/kt_lat -o run --output-format csv -- \
+            step ${TAGR:-r06}_kt_lat 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAGR:-r06}_kt_lat -o run --output-format csv -- \
               python3 scripts/latency_probe.py 1,64,256
           else
-            step ${TAGR:-r06}_kt_$t 400 rocprofv3 --kernel-trace --stats -d gpurun_out/kt_$t -o run --output-format csv -- \
+            step ${TAGR:-r06}_kt_$t 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAGR:-r06}_kt_$t -o run --output-format csv -- \
               python3 bench.py --params $t --steps 3 --warmup 1 --no-cpu-baseline --no-host-abi --no-single-call --no-other-workloads
           fi
-          find gpurun_out/kt_$t -name '*kernel_trace.csv' -delete
+          find gpurun_out/${TAGR:-r06}_kt_$t -name '*kernel_trace.csv' -delete
         done ;;
     pmc) for t in ${PMC_TAGS:-2_2}; do
            export ROUND=${TAGR:-r06}
            step ${TAGR:-r06}_pmc_$t 700 bash scripts/pmc_workload.sh $t
-           find gpurun_out/pmc_$t -name '*.csv' -delete
+           find gpurun_out/${TAGR:-r06}_pmcraw_$t -name '*.csv' -delete
          done ;;
   esac
 done

@@ -5,7 +5,8 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 tag=$1
-mkdir -p gpurun_out/pmc_$tag
+D=gpurun_out/${ROUND:-r04}_pmcraw_$tag
+mkdir -p $D
 case $tag in
   2_2)   K='pbs_classic_kernel'; U='pbs_classic_kernel'; UPD=4096; M='pbs_classic_kernel'; ARGS="--params 2_2" ;;
   2_2ks) K='pbs_classic_kernel|ks_digits|ks_mfma'; U='pbs_classic_kernel'; UPD=4096; M='pbs_classic_kernel'; ARGS="--params 2_2ks" ;;
@@ -21,17 +22,23 @@ case $tag in
   mb3_3g2|mb3_3g3) K='large_|split_|ks_digits|ks_mfma'; U='large_extract_kernel'; UPD=1024; M='large_mb_pair2_kernel|large_pair_sub_kernel|large_sub_kernel'; ARGS="--params $tag --batch 1024" ;;
   *) echo "unknown tag $tag"; exit 2 ;;
 esac
-B="$ARGS --steps 2 --warmup 1 --no-cpu-baseline --no-host-abi --no-single-call"
+B="$ARGS ${PMC_EXTRA:-} --steps 2 --warmup 1 --no-cpu-baseline --no-host-abi --no-single-call"
 run() {  # run NAME COUNTERS...
   local n=$1; shift
   # counters only for the workload's own kernels (copy / fill kernels of the runtime excluded)
-  timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-include-regex "$K" -d gpurun_out/pmc_$tag/$n -o run --output-format csv -- python3 bench.py $B \
-    > gpurun_out/pmc_$tag/$n.log 2>&1
-  local rc=$?; echo "pmc $tag $n rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/pmc_$tag/$n.log; exit $rc; }
+  timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-include-regex "$K" -d $D/$n -o run --output-format csv -- python3 bench.py $B \
+    > $D/$n.log 2>&1
+  local rc=$?; echo "pmc $tag $n rc=$rc"; [ $rc -eq 0 ] || { tail -5 $D/$n.log; exit $rc; }
 }
+if [ "${PMC_TRAFFIC_ONLY:-0}" = 1 ]; then  # L2<->fabric bytes only (the SQ pass crashed under CU-masked lanes)
+  run fetch FETCH_SIZE && run write WRITE_SIZE && \
+  python3 scripts/pmc_workload.py --fetch $D/fetch --write $D/write --tag $tag --kernels "$K" --unit-kernel "$U" \
+    --units-per-dispatch $UPD --main-kernel "$M" --note "${PMC_NOTE:-}" --out gpurun_out/${ROUND:-r04}_pmc_$tag.json
+  exit $?
+fi
 run fetch FETCH_SIZE && run write WRITE_SIZE && \
 run sq SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE && \
 run lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS TCC_HIT_sum TCC_MISS_sum && \
-python3 scripts/pmc_workload.py --fetch gpurun_out/pmc_$tag/fetch --write gpurun_out/pmc_$tag/write \
-  --sq gpurun_out/pmc_$tag/sq --extra gpurun_out/pmc_$tag/lds --tag $tag --kernels "$K" --unit-kernel "$U" \
+python3 scripts/pmc_workload.py --fetch $D/fetch --write $D/write \
+  --sq $D/sq --extra $D/lds --tag $tag --kernels "$K" --unit-kernel "$U" \
   --units-per-dispatch $UPD --main-kernel "$M" --out gpurun_out/${ROUND:-r04}_pmc_$tag.json
