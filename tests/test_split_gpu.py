@@ -170,7 +170,8 @@ def test_onchip_and_split_cmux_agree(orc, name):
     """N = 8192 and 4096, L = 2 and 1: one call of C ciphertexts runs the on-chip CMUX (onchip_cmux_kernel;
     capi.cpp onchip_min: >= 96 rows at N = 8192, >= 160 at N = 4096 on 256 CUs; at N = 4096 two
     ciphertexts per workgroup, the odd count leaving a padding slot), the same ciphertexts in two calls
-    below the threshold the split CMUX (digits-fed at L = 2, three launches at L = 1); every row
+    below the threshold the split CMUX (digits-fed at L = 2, three launches at L = 1) or, at L = 2 and
+    at most CUs / R rows, the quad / duo CMUX; every row
     identical, a sample bit-exact against the oracle, edge masks and per-ciphertext LUTs included."""
     from tfhe_mi355.parameters import SHORTINT_ALL
 
@@ -182,7 +183,7 @@ def test_onchip_and_split_cmux_agree(orc, name):
     on_min = cus * 3 // 8 if p.polynomial_size == 8192 else cus * 5 // 8  # capi.cpp onchip_min
     C = on_min + 35
     h = C // 2
-    quad = p.polynomial_size == 8192 and p.pbs_level == 2 and h <= cus // 4
+    quad = p.pbs_level == 2 and h <= cus // (p.polynomial_size // 2048)  # capi.cpp quad_max (quad / duo)
     msgs = np.random.default_rng(5).integers(0, space, C)
     cts = orc.lwe_encrypt(78, lwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta), p.lwe_modular_std_dev)
     cts[0, :-1] = 0                                   # every a~ = 0
@@ -206,14 +207,15 @@ def test_onchip_and_split_cmux_agree(orc, name):
     assert np.array_equal(dec, [fs[i](m) for i, m in zip(idx[3:], msgs[3:])])
 
 
-@pytest.mark.parametrize("name", ["PARAM_MESSAGE_3_CARRY_3_KS_PBS", "PARAM_MESSAGE_2_CARRY_4_KS_PBS"])
+@pytest.mark.parametrize("name", ["PARAM_MESSAGE_3_CARRY_3_KS_PBS", "PARAM_MESSAGE_2_CARRY_4_KS_PBS",
+                                  "PARAM_MESSAGE_1_CARRY_4_KS_PBS"])
 def test_quad_onchip_and_split_cmux_agree(orc, name):
-    """N = 8192, L = 2: the same ciphertexts through the three CMUX forms -- one call of 3/8 of the CU
-    count + 35 (on-chip CMUX, one ciphertext per CU), calls of 1, 7 and CUs/4 - 12 (quad CMUX: four
-    workgroups per ciphertext exchanging their sub-blocks every CMUX; capi.cpp quad_max = CUs / 4) and
-    one call of the rest (split CMUX, between the quad and the on-chip ranges), the kernel of each call
-    checked by the engine's kernel timer -- every row identical, a sample bit-exact against the oracle,
-    edge masks and per-ciphertext LUTs included."""
+    """N = 8192 and 4096, L = 2: the same ciphertexts through the three CMUX forms -- one call above
+    the on-chip threshold (on-chip CMUX, one ciphertext per CU), calls of 1, 7 and CUs/R - 12 (quad /
+    duo CMUX: R = N / 2048 workgroups per ciphertext exchanging their sub-blocks every CMUX; capi.cpp
+    quad_max = CUs / R) and one call of the rest (split CMUX, between the quad and the on-chip ranges),
+    the kernel of each call checked by the engine's kernel timer -- every row identical, a sample
+    bit-exact against the oracle, edge masks and per-ciphertext LUTs included."""
     from tfhe_mi355.parameters import SHORTINT_ALL
 
     p = SHORTINT_ALL[name].with_(lwe_dimension=6)
@@ -221,8 +223,9 @@ def test_quad_onchip_and_split_cmux_agree(orc, name):
     lwe_sk, glwe_sk, bsk, fbsk = _keys(orc, p, 79)
     eng = _engine(p, bsk)
     cus = _cus()
-    Q, O = cus // 4, cus * 3 // 8  # capi.cpp quad_max, onchip_min
-    C = O + 35
+    R = p.polynomial_size // 2048
+    Q, O = cus // R, cus * (5 if R == 2 else 3) // 8  # capi.cpp quad_max, onchip_min
+    C = max(O + 35, Q - 4 + (Q + O) // 2)  # the last call (Q - 4 .. C) lands between Q and O
     msgs = np.random.default_rng(8).integers(0, space, C)
     cts = orc.lwe_encrypt(80, lwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta), p.lwe_modular_std_dev)
     cts[0, :-1] = 0                                   # every a~ = 0

@@ -498,15 +498,17 @@ size_t onchip_min(const TfheMi355Context *c) {
     return c->N() == 4096 ? (size_t)c->cus * 5 / 8 : (size_t)c->cus * 3 / 8;
 }
 
-// The quad CMUX (N = 8192, L = 2 classic, four CUs per ciphertext, pbs_large.hip) for batches of at
-// most this many ciphertexts: one pass of CUs / 4 by default; TFHE_MI355_QUAD_MAX overrides (0 = never)
+// The quad CMUX (N = 8192, L = 2 classic, four CUs per ciphertext, pbs_large.hip; N = 4096: two CUs,
+// the "duo") for batches of at most this many ciphertexts: one pass of CUs / R by default (R = N / 2048
+// sub-blocks); TFHE_MI355_QUAD_MAX overrides (0 = never)
+size_t quad_sub_blocks(const TfheMi355Context *c) { return c->N() / 2048; }
 size_t quad_max(const TfheMi355Context *c) {
-    if (c->N() != 8192 || c->p.pbs_level != 2 || c->p.grouping_factor || c->k() != 1) return 0;
+    if ((c->N() != 8192 && c->N() != 4096) || c->p.pbs_level != 2 || c->p.grouping_factor || c->k() != 1) return 0;
     static const long env = [] {
         const char *e = std::getenv("TFHE_MI355_QUAD_MAX");
         return e && *e ? std::strtol(e, nullptr, 10) : -1L;
     }();
-    return env >= 0 ? (size_t)env : (size_t)c->cus / 4;
+    return env >= 0 ? (size_t)env : (size_t)c->cus / quad_sub_blocks(c);
 }
 
 // Batches of at most this many ciphertexts run the latency kernels (one ciphertext per CU) at the
@@ -626,7 +628,7 @@ void launch_pbs_dev(TfheMi355Context *c, const uint64_t *d_in, uint64_t *d_out, 
         a.timer = c->timer_or_null();
         a.grouping = (int)c->p.grouping_factor;
         a.onchip_min_count = (int)onchip_min(c);
-        a.quad_pass = (int)(c->cus / 4);
+        a.quad_pass = (int)(c->cus / quad_sub_blocks(c));
         a.quad_max_count = (int)quad_max(c);
         if (a.quad_max_count > 0 && count <= (size_t)a.quad_max_count) {
             if (!c->quad_fail.ptr) {  // created zeroed at the first quad launch of the context

@@ -2273,8 +2273,8 @@ struct QuadCfg {
     static constexpr int M = N / 2, R = M / 1024;
     static constexpr int THREADS = 512, TPC = THREADS, H = 1024 / THREADS;
     static constexpr int BUF = SubFft::XL;
-    static constexpr int REGION = 2 * R * BUF;  // the rotation's 2 x M pairs; then 4 spectra + 2 columns
-    static_assert(REGION >= 6 * BUF, "spectra and column buffers fit the pair region");
+    // the rotation's 2 x M pairs; then 4 spectra + 2 columns (N = 4096: the six buffers are the larger)
+    static constexpr int REGION = (2 * R > 6 ? 2 * R : 6) * BUF;
     static constexpr int S1 = REGION;
     static constexpr size_t LDS = sizeof(double2) * (S1 + SubFft::Lds::s1_len);
     static_assert(LDS > 80 * 1024 && LDS <= 160 * 1024, "one workgroup per CU");
@@ -2296,7 +2296,7 @@ __global__ void __launch_bounds__(512, 1) quad_cmux_kernel(LargePbsLaunch a, int
     using S = Split<N>;
     using Cfg = QuadCfg<N>;
     constexpr int K = 1, L = 2, M = S::M, R = S::R, H = Cfg::H, BUF = Cfg::BUF, TPC = Cfg::TPC;
-    static_assert(R == 4, "N = 8192");
+    static_assert(R == 4 || R == 2, "N = 8192 (quad) or 4096 (duo)");
     constexpr size_t ggsw_len = (size_t)L * (K + 1) * (K + 1) * M;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double2 *lds = reinterpret_cast<double2 *>(smem);
@@ -2410,11 +2410,16 @@ __global__ void __launch_bounds__(512, 1) quad_cmux_kernel(LargePbsLaunch a, int
         stamp(i, 3);
         // ---- top DIF output q of both rows and levels ----
         if (!QUAD_TPF) top_tables();
-        switch (q) {
-            case 0: quad_top<N, 0, H>(lds, pk, tvh, wqh, t); break;
-            case 1: quad_top<N, 1, H>(lds, pk, tvh, wqh, t); break;
-            case 2: quad_top<N, 2, H>(lds, pk, tvh, wqh, t); break;
-            default: quad_top<N, 3, H>(lds, pk, tvh, wqh, t); break;
+        if constexpr (R == 4) {
+            switch (q) {
+                case 0: quad_top<N, 0, H>(lds, pk, tvh, wqh, t); break;
+                case 1: quad_top<N, 1, H>(lds, pk, tvh, wqh, t); break;
+                case 2: quad_top<N, 2, H>(lds, pk, tvh, wqh, t); break;
+                default: quad_top<N, 3, H>(lds, pk, tvh, wqh, t); break;
+            }
+        } else {
+            if (q == 0) quad_top<N, 0, H>(lds, pk, tvh, wqh, t);
+            else quad_top<N, 1, H>(lds, pk, tvh, wqh, t);
         }
         stamp(i, 4);
         __syncthreads();
@@ -2909,7 +2914,7 @@ template <int N, int K, int L, int G = 0>
 static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
     using S = Split<N>;
     if (a0.count == 0) return hipSuccess;
-    if constexpr (G == 0 && K == 1 && L == 2 && S::R == 4) {
+    if constexpr (G == 0 && K == 1 && L == 2 && (S::R == 4 || S::R == 2)) {  // quad (N = 8192) / duo (4096)
         if (quad_enabled() && a0.count <= a0.quad_max_count) return launch_quad<N>(a0, s);
     }
     if constexpr (G == 0 && K == 1 && (L == 2 || L == 1) && (S::R == 4 || S::R == 2)) {
