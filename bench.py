@@ -98,6 +98,11 @@ PARAMS = {  # --params choice -> (parameter set name, workload text, kernel name
 
 
 
+def mb_digits_on() -> bool:
+    """The multi-bit pair kernel reads packed digits (pbs_large.hip mb_dig) unless switched off."""
+    return all(os.environ.get(v, "1") != "0" for v in ("TFHE_MI355_MB_DIGITS", "TFHE_MI355_MB_FUSED", "TFHE_MI355_MB_PAIR2"))
+
+
 def _split_params():
     """`--params m_c`: every shortint KS_PBS set at N = 4096 ... 32768 (the split CMUX, pbs_large.hip)
     as a shortint apply_lookup_table (KS -> PBS) batch; 4_4 keeps its grouped-CMUX entry above."""
@@ -132,7 +137,8 @@ def _split_params():
         out[f"mb3_3g{g}"] = (name, f"shortint apply_lookup_table (keyswitch -> multi-bit PBS, grouping {g}) at {name} "
                                    f"(shortint/parameters/multi_bit.rs:{line}), N={p.polynomial_size}, batch per GPU; "
                                    "the reference publishes no number for this set",
-                             (f"large_mb_pair2_kernel<{p.polynomial_size},{g}> (+ large_mb_inv_fwd per group: packed "
+                             (f"large_mb_pair2_kernel<{p.polynomial_size},{g},{'true' if mb_digits_on() else 'false'}> "
+                              "(+ large_mb_inv_fwd per group: packed "
                               "digits in, twist + top DIF in the pair kernel; ks_mfma_kernel)" if os.environ.get("TFHE_MI355_MB_PAIR2", "1") != "0" else
                               f"large_pair_sub_kernel<{p.polynomial_size},1,{p.pbs_level},{g},1> (+ large_top_fwd/top_inv "
                               "per group, ks_mfma_kernel)"))
@@ -286,11 +292,6 @@ def split_dsub_flops(p) -> float:
     R = M // 1024
     k1, L = p.glwe_dimension + 1, p.pbs_level
     return k1 * L * (6 * M + 5 * M * math.log2(R)) + split_sub_flops(p)
-
-
-def mb_digits_on() -> bool:
-    """The multi-bit pair kernel reads packed digits (pbs_large.hip mb_dig) unless switched off."""
-    return all(os.environ.get(v, "1") != "0" for v in ("TFHE_MI355_MB_DIGITS", "TFHE_MI355_MB_FUSED", "TFHE_MI355_MB_PAIR2"))
 
 
 def split_chunk(p, units: int) -> int:
