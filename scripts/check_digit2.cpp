@@ -1,6 +1,7 @@
 // Exhaustive check of Digit2 (tfhe-rs-odd_amd/csrc/pbs_common.h): for every 32-bit hi word and
 // beta = 1..15 the two int16 digits of the short form equal decomp_state32<2> + two decomp_digit32
-// (the SignedDecomposer's digits, decomposer.rs:99-119 / iter.rs:134-141).
+// (the SignedDecomposer's digits, decomposer.rs:99-119 / iter.rs:134-141); and DigitL1, the one-level
+// 3-op digit, against decomp_state32<1> + decomp_digit32 for beta = 1..30.
 //   g++ -O3 -fopenmp scripts/check_digit2.cpp -o /tmp/check_digit2 && /tmp/check_digit2   (~30 s on 8 cores)
 //   /tmp/check_digit2 24   : 2^24 evenly spread hi words per beta instead (tests/test_digit2.py)
 #include <cstdint>
@@ -31,6 +32,22 @@ int main(int argc, char **argv) {
             if ((uint16_t)d0 != (uint16_t)r0 || (uint16_t)d1 != (uint16_t)r1) bb++;
         }
         printf("beta %d mismatches %ld\n", beta, bb); fflush(stdout);
+        bad += bb;
+    }
+    // DigitL1 (one level, beta = 1..30): ((x_hi + ((2^beta - 1) << (31 - beta))) >> (32 - beta)) - (2^(beta-1) - 1)
+    for (int beta = 1; beta <= 30; beta++) {
+        const uint32_t mask = (1u << beta) - 1, ck = ((1u << beta) - 1) << (31 - beta);
+        const int sh = 32 - beta;
+        const int32_t h = (int32_t)(1u << (beta - 1)) - 1;
+        long bb = 0;
+        #pragma omp parallel for reduction(+:bb)
+        for (long xl = 0; xl < (1l << lg); xl++) {
+            const uint32_t xh = (uint32_t)((xl << (32 - lg)) | (xl & ((1l << (32 - lg)) - 1)));
+            uint32_t st = ((xh >> (31 - beta)) + 1) >> 1;
+            const int32_t r0 = dig(st, beta, mask);
+            if ((int32_t)((xh + ck) >> sh) - h != r0) bb++;
+        }
+        printf("L1 beta %d mismatches %ld\n", beta, bb); fflush(stdout);
         bad += bb;
     }
     return bad != 0;

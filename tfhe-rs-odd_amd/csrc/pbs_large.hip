@@ -2046,6 +2046,7 @@ __global__ void __launch_bounds__(OnchipCfg<N>::THREADS, OnchipCfg<N>::MIN_WPS /
     const double k32 = torus_k32();
     const int beta = a.base_log;
     const Digit2 dg2(D32 ? beta : 2);  // (unused unless D32)
+    const DigitL1 dl1(D32 ? beta : 2);
     // accumulator pair (row r, j) <-> LDS slot (2 (j >> 10) + r) BUF + (j & 1023): the slots thread t
     // owns, (2 b + r) BUF + t + 512 h, are exactly the top-stage / top-inverse slots of its butterflies,
     // so the top inverse writes the updated pairs in place (no barrier between its reads and them)
@@ -2082,8 +2083,15 @@ __global__ void __launch_bounds__(OnchipCfg<N>::THREADS, OnchipCfg<N>::MIN_WPS /
                         pk[r][h][b] = onchip_pack2<D32>((neg0 ? 0 - x0 : x0) - lo[r][h][b], (neg1 ? 0 - x1 : x1) - hi[r][h][b],
                                                         beta, dg2);
                     } else {  // one level: |digit| <= 2^(beta - 1) (2^21 at base 2^22) -- two int32 fields
-                        const int32_t e0 = onchip_decompose1<D32>((neg0 ? 0 - x0 : x0) - lo[r][h][b], beta);
-                        const int32_t e1 = onchip_decompose1<D32>((neg1 ? 0 - x1 : x1) - hi[r][h][b], beta);
+                        const uint64_t v0 = (neg0 ? 0 - x0 : x0) - lo[r][h][b], v1 = (neg1 ? 0 - x1 : x1) - hi[r][h][b];
+                        int32_t e0, e1;
+                        if constexpr (D32 && ONCHIP_DIGIT2) {  // the classic kernel's 3-op digit (DigitL1)
+                            e0 = dl1((uint32_t)(v0 >> 32));
+                            e1 = dl1((uint32_t)(v1 >> 32));
+                        } else {
+                            e0 = onchip_decompose1<D32>(v0, beta);
+                            e1 = onchip_decompose1<D32>(v1, beta);
+                        }
                         pk[r][h][b] = (uint64_t)(uint32_t)e0 | ((uint64_t)(uint32_t)e1 << 32);
                     }
                 }
