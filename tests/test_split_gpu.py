@@ -170,8 +170,8 @@ def test_onchip_and_split_cmux_agree(orc, name):
     """N = 8192 and 4096, L = 2 and 1: one call of C ciphertexts runs the on-chip CMUX (onchip_cmux_kernel;
     capi.cpp onchip_min: >= 96 rows at N = 8192, >= 160 at N = 4096 on 256 CUs; at N = 4096 two
     ciphertexts per workgroup, the odd count leaving a padding slot), the same ciphertexts in two calls
-    below the threshold the split CMUX (digits-fed at L = 2, three launches at L = 1) or, at L = 2 and
-    at most CUs / R rows, the quad / duo CMUX; every row
+    below the threshold the split CMUX (digits-fed at L = 2, three launches at L = 1) or, at most
+    CUs / R rows, the quad / duo CMUX; every row
     identical, a sample bit-exact against the oracle, edge masks and per-ciphertext LUTs included."""
     from tfhe_mi355.parameters import SHORTINT_ALL
 
@@ -183,7 +183,7 @@ def test_onchip_and_split_cmux_agree(orc, name):
     on_min = cus * 3 // 8 if p.polynomial_size == 8192 else cus * 5 // 8  # capi.cpp onchip_min
     C = on_min + 35
     h = C // 2
-    quad = p.pbs_level == 2 and h <= cus // (p.polynomial_size // 2048)  # capi.cpp quad_max (quad / duo)
+    quad = h <= cus // (p.polynomial_size // 2048)  # capi.cpp quad_max (quad / duo, L = 1 and 2)
     msgs = np.random.default_rng(5).integers(0, space, C)
     cts = orc.lwe_encrypt(78, lwe_sk, msgs.astype(np.uint64) * np.uint64(p.delta), p.lwe_modular_std_dev)
     cts[0, :-1] = 0                                   # every a~ = 0
@@ -208,9 +208,10 @@ def test_onchip_and_split_cmux_agree(orc, name):
 
 
 @pytest.mark.parametrize("name", ["PARAM_MESSAGE_3_CARRY_3_KS_PBS", "PARAM_MESSAGE_2_CARRY_4_KS_PBS",
-                                  "PARAM_MESSAGE_1_CARRY_4_KS_PBS"])
+                                  "PARAM_MESSAGE_1_CARRY_4_KS_PBS", "PARAM_MESSAGE_6_CARRY_0_KS_PBS",
+                                  "PARAM_MESSAGE_2_CARRY_3_KS_PBS"])
 def test_quad_onchip_and_split_cmux_agree(orc, name):
-    """N = 8192 and 4096, L = 2: the same ciphertexts through the three CMUX forms -- one call above
+    """N = 8192 and 4096, L = 2 and 1: the same ciphertexts through the three CMUX forms -- one call above
     the on-chip threshold (on-chip CMUX, one ciphertext per CU), calls of 1, 7 and CUs/R - 12 (quad /
     duo CMUX: R = N / 2048 workgroups per ciphertext exchanging their sub-blocks every CMUX; capi.cpp
     quad_max = CUs / R) and one call of the rest (split CMUX, between the quad and the on-chip ranges),
@@ -238,8 +239,9 @@ def test_quad_onchip_and_split_cmux_agree(orc, name):
     whole, ran = _ran(eng, lambda: eng.programmable_bootstrap(cts, luts, lut_indexes=idx))
     assert "onchip_cmux_kernel" in ran, ran
     parts = []
+    split = "large_dsub_kernel" if p.pbs_level == 2 else "large_sub_kernel"  # digits-fed at L = 2
     for a, b, kern in ((0, 1, "quad_cmux_kernel"), (1, 8, "quad_cmux_kernel"), (8, Q - 4, "quad_cmux_kernel"),
-                       (Q - 4, C, "large_dsub_kernel")):
+                       (Q - 4, C, split)):
         assert 0 < b - a <= Q if kern.startswith("quad") else Q < b - a < O
         out, ran = _ran(eng, lambda: eng.programmable_bootstrap(cts[a:b], luts, lut_indexes=idx[a:b]))
         assert kern in ran and "onchip_cmux_kernel" not in ran, (a, b, ran)
@@ -250,6 +252,24 @@ def test_quad_onchip_and_split_cmux_agree(orc, name):
     assert np.array_equal(whole[sample], fbsk.pbs(cts[sample], luts, lut_idx=idx[sample], threads=9))
     dec = decode(orc.lwe_decrypt(glwe_sk, whole[4:]), p.delta) % space
     assert np.array_equal(dec, [fs[i](m) for i, m in zip(idx[4:], msgs[4:])])
+    # the async entry with scratch for 5 ciphertexts: quad passes of 5, 5, 2 (pbs_large.hip launch_quad)
+    import torch
+
+    dev = torch.device("cuda", 0)
+    n = 12
+    ref = eng.programmable_bootstrap(cts[:n], luts[0])
+    d_in = torch.from_numpy(cts[:n].view(np.int64)).to(dev)
+    d_out = torch.zeros((n, p.big_lwe_dimension + 1), dtype=torch.int64, device=dev)
+    d_lut = torch.from_numpy(luts[0].view(np.int64)).to(dev)
+    scratch = torch.empty(eng.pbs_scratch_bytes(1) * 5, dtype=torch.uint8, device=dev)
+
+    def run_async():
+        eng.programmable_bootstrap_async(d_in, d_out, d_lut, 1, n, d_scratch=scratch)
+        torch.cuda.synchronize()
+
+    _, ran = _ran(eng, run_async)
+    assert "quad_cmux_kernel" in ran, ran
+    assert np.array_equal(d_out.cpu().numpy().view(np.uint64), ref)
 
 
 @pytest.mark.timeout(900)

@@ -498,12 +498,14 @@ size_t onchip_min(const TfheMi355Context *c) {
     return c->N() == 4096 ? (size_t)c->cus * 5 / 8 : (size_t)c->cus * 3 / 8;
 }
 
-// The quad CMUX (N = 8192, L = 2 classic, four CUs per ciphertext, pbs_large.hip; N = 4096: two CUs,
+// The quad CMUX (N = 8192, L = 1 or 2 classic, four CUs per ciphertext, pbs_large.hip; N = 4096: two CUs,
 // the "duo") for batches of at most this many ciphertexts: one pass of CUs / R by default (R = N / 2048
 // sub-blocks); TFHE_MI355_QUAD_MAX overrides (0 = never)
 size_t quad_sub_blocks(const TfheMi355Context *c) { return c->N() / 2048; }
 size_t quad_max(const TfheMi355Context *c) {
-    if ((c->N() != 8192 && c->N() != 4096) || c->p.pbs_level != 2 || c->p.grouping_factor || c->k() != 1) return 0;
+    if ((c->N() != 8192 && c->N() != 4096) || (c->p.pbs_level != 2 && c->p.pbs_level != 1) || c->p.grouping_factor ||
+        c->k() != 1)
+        return 0;
     static const long env = [] {
         const char *e = std::getenv("TFHE_MI355_QUAD_MAX");
         return e && *e ? std::strtol(e, nullptr, 10) : -1L;

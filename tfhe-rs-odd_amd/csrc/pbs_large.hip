@@ -827,10 +827,12 @@ __global__ void __launch_bounds__((PairSubCfg<K, L>::THREADS), 2) large_pair_sub
 #endif
 // top DIF output Q of butterfly a0 for both rows and levels -> spectra buffers p = (lvl - 1) 2 + r
 // (tv[h][b] = twist[a0 + 1024 b], wq[h] = W[a0 Q], loaded by the caller ahead of the barrier)
-template <int N, int Q, int H>
+// (L = 1: one level, the digits of j and j + M as two int32 fields -> buffers p = r)
+template <int N, int Q, int H, int L = 2>
 __device__ __forceinline__ void quad_top(double2 *lds, const uint64_t (&pk)[2][H][Split<N>::R],
                                          const cx (&tvh)[H][Split<N>::R], const cx (&wqh)[H], int t) {
     constexpr int R = Split<N>::R, BUF = SubFft::XL;
+    static_assert(L == 1 || L == 2, "one or two levels");
 #pragma unroll
     for (int h = 0; h < H; h++) {
         const int a0 = t + 512 * h;
@@ -839,17 +841,24 @@ __device__ __forceinline__ void quad_top(double2 *lds, const uint64_t (&pk)[2][H
 #pragma unroll
         for (int r = 0; r < 2; r++)
 #pragma unroll
-            for (int li = 0; li < 2; li++) {  // li = 0: level L, 1: level L-1
+            for (int li = 0; li < L; li++) {  // li = 0: level L, 1: level L-1
                 cx u[R];
 #pragma unroll
                 for (int b = 0; b < R; b++) {
-                    const uint64_t w = pk[r][h][b] >> (32 * li);
-                    const int32_t d0 = (int32_t)(int16_t)(w & 0xffffu), d1 = (int32_t)(int16_t)((w >> 16) & 0xffffu);
+                    int32_t d0, d1;
+                    if constexpr (L == 2) {
+                        const uint64_t w = pk[r][h][b] >> (32 * li);
+                        d0 = (int32_t)(int16_t)(w & 0xffffu);
+                        d1 = (int32_t)(int16_t)((w >> 16) & 0xffffu);
+                    } else {
+                        d0 = (int32_t)(uint32_t)pk[r][h][b];
+                        d1 = (int32_t)(uint32_t)(pk[r][h][b] >> 32);
+                    }
                     u[b] = cmulw(cx{(double)d0, (double)d1}, tv[b].re, tv[b].im);
                 }
                 dftR_fwd<R>(u);
                 const cx y = Q ? cmulw(u[Q], wq.re, wq.im) : u[0];
-                const int p = (1 - li) * 2 + r;  // level L -> 2, 3; level L-1 -> 0, 1
+                const int p = (L - 1 - li) * 2 + r;  // level L -> 2, 3 (L = 2) or 0, 1 (L = 1); level L-1 -> 0, 1
                 lds[p * BUF + a0] = make_double2(y.re, y.im);
             }
     }
@@ -2299,11 +2308,12 @@ __device__ __forceinline__ double2 *quad_u(const LargePbsLaunch &a, int cnt, int
     return reinterpret_cast<double2 *>(base + (size_t)ct * Cfg::U_BYTES) + ((size_t)(par * Cfg::R + q) * 2 + c) * 1024;
 }
 
-template <int N, bool D32>
+template <int N, bool D32, int L>
 __global__ void __launch_bounds__(512, 1) quad_cmux_kernel(LargePbsLaunch a, int ct0, int cnt) {
     using S = Split<N>;
     using Cfg = QuadCfg<N>;
-    constexpr int K = 1, L = 2, M = S::M, R = S::R, H = Cfg::H, BUF = Cfg::BUF, TPC = Cfg::TPC;
+    constexpr int K = 1, M = S::M, R = S::R, H = Cfg::H, BUF = Cfg::BUF, TPC = Cfg::TPC, P = 2 * L;
+    static_assert(L == 1 || L == 2, "one or two levels (2 L spectra per sub-block)");
     static_assert(R == 4 || R == 2, "N = 8192 (quad) or 4096 (duo)");
     constexpr size_t ggsw_len = (size_t)L * (K + 1) * (K + 1) * M;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2349,6 +2359,7 @@ __global__ void __launch_bounds__(512, 1) quad_cmux_kernel(LargePbsLaunch a, int
     const double k32 = torus_k32();
     const int beta = a.base_log;
     const Digit2 dg2(D32 ? beta : 2);  // (unused unless D32)
+    const DigitL1 dl1(D32 ? beta : 2);
     auto pslot = [&](int r, int j) { return (2 * (j >> 10) + r) * BUF + (j & 1023); };
     auto store_pairs = [&]() {
 #pragma unroll
@@ -2408,8 +2419,20 @@ __global__ void __launch_bounds__(512, 1) quad_cmux_kernel(LargePbsLaunch a, int
                     const bool swap = jj0 < 0 && jj0 >= -M;
                     const uint64_t x0 = swap ? rot.y : rot.x, x1 = swap ? rot.x : rot.y;
                     const bool neg0 = (jj0 < 0) != full_odd, neg1 = (jj0 + M < 0) != full_odd;
-                    pk[r][h][b] = onchip_pack2<D32>((neg0 ? 0 - x0 : x0) - lo[r][h][b], (neg1 ? 0 - x1 : x1) - hi[r][h][b],
-                                                    beta, dg2);
+                    const uint64_t v0 = (neg0 ? 0 - x0 : x0) - lo[r][h][b], v1 = (neg1 ? 0 - x1 : x1) - hi[r][h][b];
+                    if constexpr (L == 2) {
+                        pk[r][h][b] = onchip_pack2<D32>(v0, v1, beta, dg2);
+                    } else {  // |digit| <= 2^(beta - 1): two int32 fields
+                        int32_t e0, e1;
+                        if constexpr (D32) {
+                            e0 = dl1((uint32_t)(v0 >> 32));
+                            e1 = dl1((uint32_t)(v1 >> 32));
+                        } else {
+                            e0 = onchip_decompose1<D32>(v0, beta);
+                            e1 = onchip_decompose1<D32>(v1, beta);
+                        }
+                        pk[r][h][b] = (uint64_t)(uint32_t)e0 | ((uint64_t)(uint32_t)e1 << 32);
+                    }
                     if (QUAD_PKFENCE) asm volatile("" : "+v"(pk[r][h][b]));  // digits before the barrier: 32
                                                                             // registers live across it, not 64
                 }
@@ -2420,32 +2443,34 @@ __global__ void __launch_bounds__(512, 1) quad_cmux_kernel(LargePbsLaunch a, int
         if (!QUAD_TPF) top_tables();
         if constexpr (R == 4) {
             switch (q) {
-                case 0: quad_top<N, 0, H>(lds, pk, tvh, wqh, t); break;
-                case 1: quad_top<N, 1, H>(lds, pk, tvh, wqh, t); break;
-                case 2: quad_top<N, 2, H>(lds, pk, tvh, wqh, t); break;
-                default: quad_top<N, 3, H>(lds, pk, tvh, wqh, t); break;
+                case 0: quad_top<N, 0, H, L>(lds, pk, tvh, wqh, t); break;
+                case 1: quad_top<N, 1, H, L>(lds, pk, tvh, wqh, t); break;
+                case 2: quad_top<N, 2, H, L>(lds, pk, tvh, wqh, t); break;
+                default: quad_top<N, 3, H, L>(lds, pk, tvh, wqh, t); break;
             }
         } else {
-            if (q == 0) quad_top<N, 0, H>(lds, pk, tvh, wqh, t);
-            else quad_top<N, 1, H>(lds, pk, tvh, wqh, t);
+            if (q == 0) quad_top<N, 0, H, L>(lds, pk, tvh, wqh, t);
+            else quad_top<N, 1, H, L>(lds, pk, tvh, wqh, t);
         }
         stamp(i, 4);
         __syncthreads();
         stamp(i, 5);
         const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.fbsk + (size_t)i * ggsw_len + 1024 * q);
         if (wave < 4) {
-            // ---- sub-block forward FFT of polynomial p = wave, published in place ----
-            double2 *own = lds + wave * BUF;
             cx v[16];
+            if (wave < P) {
+                // ---- sub-block forward FFT of polynomial p = wave, published in place ----
+                double2 *own = lds + wave * BUF;
 #pragma unroll
-            for (int b = 0; b < 16; b++) {
-                const double2 y = own[lane + 64 * b];
-                v[b] = cx{y.x, y.y};
+                for (int b = 0; b < 16; b++) {
+                    const double2 y = own[lane + 64 * b];
+                    v[b] = cx{y.x, y.y};
+                }
+                if (!(QUAD_TSKIP & 2)) SubFft::forward(v, reinterpret_cast<cx *>(own), tw, lane, wsync);
+                wsync();
+#pragma unroll
+                for (int sl = 0; sl < 16; sl++) own[sl * 64 + lane] = make_double2(v[sl].re, v[sl].im);
             }
-            if (!(QUAD_TSKIP & 2)) SubFft::forward(v, reinterpret_cast<cx *>(own), tw, lane, wsync);
-            wsync();
-#pragma unroll
-            for (int sl = 0; sl < 16; sl++) own[sl * 64 + lane] = make_double2(v[sl].re, v[sl].im);
             __syncthreads();  // spectra published
             stamp(i, 6);
             __syncthreads();  // MAC outputs in the column buffers
@@ -2476,36 +2501,37 @@ __global__ void __launch_bounds__(512, 1) quad_cmux_kernel(LargePbsLaunch a, int
         } else {
             // ---- GGSW operands of slots 4 w' .. 4 w' + 3, both columns (in flight during the FFTs) ----
             const int w4 = wave - 4;
-            double2 g[4][2][4];  // [slot][column][polynomial p]
+            double2 g[4][2][P];  // [slot][column][polynomial p]
 #pragma unroll
             for (int k = 0; k < 4; k++)
 #pragma unroll
                 for (int c = 0; c < 2; c++)
 #pragma unroll
-                    for (int p = 0; p < 4; p++)
+                    for (int p = 0; p < P; p++)
                         g[k][c][p] = (QUAD_TSKIP & 8) ? make_double2(p + c, k)
                                                       : buffer_ld_d2(rg, 16u * lane, 16u * (uint32_t)((p * 2 + c) * M + (4 * w4 + k) * 64));
             __syncthreads();  // spectra published
             stamp(i, 6);
-            // ---- MAC: levels L..1, rows 0..k (p = 2, 3, 0, 1), the oracle's forms ----
+            // ---- MAC: levels L..1, rows 0..k (p = 2, 3, 0, 1 at L = 2; 0, 1 at L = 1), the oracle's forms ----
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const int sl = 4 * w4 + k;
-                double2 f[4];
+                double2 f[P];
 #pragma unroll
-                for (int p = 0; p < 4; p++) f[p] = lds[p * BUF + sl * 64 + lane];
+                for (int p = 0; p < P; p++) f[p] = lds[p * BUF + sl * 64 + lane];
+                constexpr int first = 2 * (L - 1);  // level L, row 0; then row 1, then level L-1 (L = 2)
 #pragma unroll
                 for (int c = 0; c < 2; c++) {
                     cx o;
                     {
-                        const double2 gg = g[k][c][2], ff = f[2];
+                        const double2 gg = g[k][c][first], ff = f[first];
                         o.re = fma(gg.x, ff.x, -(gg.y * ff.y));
                         o.im = fma(gg.x, ff.y, gg.y * ff.x);
                     }
-                    constexpr int order[3] = {3, 0, 1};
 #pragma unroll
-                    for (int u = 0; u < 3; u++) {
-                        const double2 gg = g[k][c][order[u]], ff = f[order[u]];
+                    for (int u = 1; u < P; u++) {
+                        const int pp = (first + u) % P;
+                        const double2 gg = g[k][c][pp], ff = f[pp];
                         o.re = fma(gg.x, ff.x, fma(-gg.y, ff.y, o.re));
                         o.im = fma(gg.x, ff.y, fma(gg.y, ff.x, o.im));
                     }
@@ -2747,7 +2773,13 @@ bool large_pbs_supported(int N, int k, int L) {
 }
 
 size_t large_pbs_scratch_per_ct(int N, int k, int L) {
-    return (size_t)(k + 1) * N * sizeof(uint64_t) + (size_t)L * (k + 1) * (N / 2) * sizeof(double2);
+    const size_t split = (size_t)(k + 1) * N * sizeof(uint64_t) + (size_t)L * (k + 1) * (N / 2) * sizeof(double2);
+    // the quad / duo CMUX's flags + exchange buffers per ciphertext (more than the split CMUX's
+    // accumulator + spectra at L = 1)
+    size_t quad = 0;
+    if (k == 1 && L <= 2 && N == 8192) quad = QuadCfg<8192>::R * QuadCfg<8192>::FLAG_BYTES + QuadCfg<8192>::U_BYTES;
+    if (k == 1 && L <= 2 && N == 4096) quad = QuadCfg<4096>::R * QuadCfg<4096>::FLAG_BYTES + QuadCfg<4096>::U_BYTES;
+    return std::max(split, quad);
 }
 
 // TFHE_MI355_LARGE_SPLIT=1: the N = 32768, L = 2 CMUX through the split path (top_fwd / sub /
@@ -2885,7 +2917,7 @@ static hipError_t launch_grouped_lanes(const LargePbsLaunch &a0, hipStream_t s, 
 // The quad CMUX over the batch in passes of quad_pass ciphertexts.  Its workgroups wait on each
 // other, so two quad launches must never share the device's CUs: every launch of a device waits
 // for the previous one (an event chained across streams under a process-wide lock).
-template <int N>
+template <int N, int L>
 static hipError_t launch_quad(const LargePbsLaunch &a0, hipStream_t s) {
     using Cfg = QuadCfg<N>;
     static std::mutex mu;
@@ -2895,9 +2927,9 @@ static hipError_t launch_quad(const LargePbsLaunch &a0, hipStream_t s) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(s, &cs);
     const bool capturing = cs != hipStreamCaptureStatusNone;
-    const int pass = a0.quad_pass;
-    if (pass <= 0 || (size_t)std::min(pass, a0.count) * (Cfg::R * Cfg::FLAG_BYTES + Cfg::U_BYTES) > a0.scratch_bytes)
-        return hipErrorInvalidValue;
+    // passes of at most quad_pass ciphertexts (one per R CUs) and of what the caller's scratch holds
+    const int pass = (int)std::min<size_t>((size_t)a0.quad_pass, a0.scratch_bytes / (Cfg::R * Cfg::FLAG_BYTES + Cfg::U_BYTES));
+    if (pass <= 0) return hipErrorInvalidValue;
     std::lock_guard<std::mutex> g(mu);
     if (!capturing && last[dev]) (void)hipStreamWaitEvent(s, last[dev], 0);
     for (int c0 = 0; c0 < a0.count; c0 += pass) {
@@ -2906,10 +2938,10 @@ static hipError_t launch_quad(const LargePbsLaunch &a0, hipStream_t s) {
         if (e != hipSuccess) return e;
         TimedLaunch tl(a0.timer, "quad_cmux_kernel", s);
         const dim3 grid((unsigned)((cnt + 7) / 8) * 8 * Cfg::R), block(Cfg::THREADS);
-        if (a0.base_log * 2 <= 30)
-            hipLaunchKernelGGL((quad_cmux_kernel<N, true>), grid, block, Cfg::LDS, s, a0, c0, cnt);
+        if (a0.base_log * L <= 30)
+            hipLaunchKernelGGL((quad_cmux_kernel<N, true, L>), grid, block, Cfg::LDS, s, a0, c0, cnt);
         else
-            hipLaunchKernelGGL((quad_cmux_kernel<N, false>), grid, block, Cfg::LDS, s, a0, c0, cnt);
+            hipLaunchKernelGGL((quad_cmux_kernel<N, false, L>), grid, block, Cfg::LDS, s, a0, c0, cnt);
     }
     if (!capturing) {
         if (!last[dev]) (void)hipEventCreateWithFlags(&last[dev], hipEventDisableTiming);
@@ -2922,8 +2954,8 @@ template <int N, int K, int L, int G = 0>
 static hipError_t launch_large_t(const LargePbsLaunch &a0, hipStream_t s) {
     using S = Split<N>;
     if (a0.count == 0) return hipSuccess;
-    if constexpr (G == 0 && K == 1 && L == 2 && (S::R == 4 || S::R == 2)) {  // quad (N = 8192) / duo (4096)
-        if (quad_enabled() && a0.count <= a0.quad_max_count) return launch_quad<N>(a0, s);
+    if constexpr (G == 0 && K == 1 && (L == 2 || L == 1) && (S::R == 4 || S::R == 2)) {  // quad (8192) / duo (4096)
+        if (quad_enabled() && a0.count <= a0.quad_max_count) return launch_quad<N, L>(a0, s);
     }
     if constexpr (G == 0 && K == 1 && (L == 2 || L == 1) && (S::R == 4 || S::R == 2)) {
         if (onchip_enabled() && a0.count >= a0.onchip_min_count) {  // the whole blind rotation on chip, no scratch
