@@ -42,7 +42,7 @@
  *     3/8 / 5/8 of the CU count (96 / 160 rows on 256 CUs) run the on-chip CMUX (the whole blind
  *     rotation in one workgroup per ciphertext, two per CU at N = 4096, no scratch used), smaller
  *     ones the split CMUX (same outputs; TFHE_MI355_ONCHIP_MIN = rows overrides,
- *     TFHE_MI355_ONCHIP=0 = never); at N = 8192 / 4096, L = 2 batches of at most CUs / 4 / CUs / 2
+ *     TFHE_MI355_ONCHIP=0 = never); at N = 8192 / 4096 (L = 1 or 2) batches of at most CUs / 4 / CUs / 2
  *     rows run the quad CMUX instead (four / two CUs per ciphertext exchanging sub-blocks every CMUX
  *     through the scratch; same outputs; TFHE_MI355_QUAD_MAX = rows overrides, TFHE_MI355_QUAD=0 =
  *     never).  The quad
