@@ -253,6 +253,9 @@ __device__ __forceinline__ void decompose64(uint64_t x, int beta, int32_t (&d)[L
 #endif
 constexpr int TOPT = LARGE_TOPT;  // threads per top-stage workgroup
 
+#ifndef LARGE_DIGIT2
+#define LARGE_DIGIT2 1  // split / grouped digit kernels: Digit2 (pbs_common.h) when 2 base_log <= 30 (0: A/B)
+#endif
 // rotate, decompose, twist and top DIF radix-R of butterfly t of row r, CMUX i -> T.
 // G > 0 (multi-bit, step i = group i): the external product's input is the accumulator itself
 // (acc <- ExtProd(KB_i, acc), lwe_multi_bit_programmable_bootstrapping.rs:548-828): no rotation.
@@ -281,8 +284,21 @@ __device__ __forceinline__ void top_fwd_body(const LargePbsLaunch &a, int ct0, i
             ct1_pair_m<M>(acc, j, rem, full_odd, dd[0], dd[1]);
         }
         int32_t d0[L], d1[L];
-        decompose64<L>(dd[0], beta, d0);
-        decompose64<L>(dd[1], beta, d1);
+        if (LARGE_DIGIT2 && L == 2 && N <= 16384 && beta * 2 <= 30) {  // Digit2 (at N = 32768 it spilled)
+            uint32_t lv0, lv1;
+            Digit2(beta).pair((uint32_t)(dd[0] >> 32), (uint32_t)(dd[1] >> 32), lv0, lv1);
+            d0[0] = (int32_t)(int16_t)(lv0 & 0xffffu);
+            d1[0] = (int32_t)(int16_t)(lv0 >> 16);
+            d0[L - 1] = (int32_t)(int16_t)(lv1 & 0xffffu);
+            d1[L - 1] = (int32_t)(int16_t)(lv1 >> 16);
+        } else if (LARGE_DIGIT2 && L == 1 && beta <= 30) {  // DigitL1
+            const DigitL1 dl1(beta);
+            d0[0] = dl1((uint32_t)(dd[0] >> 32));
+            d1[0] = dl1((uint32_t)(dd[1] >> 32));
+        } else {
+            decompose64<L>(dd[0], beta, d0);
+            decompose64<L>(dd[1], beta, d1);
+        }
         if constexpr (L > 1) {
             uint64_t w = 0;
 #pragma unroll
@@ -515,6 +531,12 @@ __global__ void __launch_bounds__(256) split_digits_kernel(LargePbsLaunch a, int
     for (int r = 0; r < 2; r++) {
         uint64_t dd[2];
         ct1_pair_m<M>(a.acc + ((size_t)cl * 2 + r) * N, j, rem, full_odd, dd[0], dd[1]);
+        if (LARGE_DIGIT2 && a.base_log * 2 <= 30) {  // Digit2: the same words, 32-bit
+            uint32_t lv0, lv1;
+            Digit2(a.base_log).pair((uint32_t)(dd[0] >> 32), (uint32_t)(dd[1] >> 32), lv0, lv1);
+            w[r] = (uint64_t)lv0 | ((uint64_t)lv1 << 32);
+            continue;
+        }
         int32_t d0[2], d1[2];
         decompose64<2>(dd[0], a.base_log, d0);
         decompose64<2>(dd[1], a.base_log, d1);
@@ -1516,6 +1538,11 @@ __device__ __forceinline__ uint64_t group_digit_word(const LargePbsLaunch &a, in
     const uint64_t *acc = a.acc + ((size_t)cl * 2 + r) * LN;
     uint64_t w = 0, dd[2];
     ct1_pair(acc, j, rem, full_odd, dd[0], dd[1]);  // ct1 = X^{a~} acc - acc
+    if (LARGE_DIGIT2) {  // Digit2 (pbs_common.h): the same int16 words in 9 VALU per value
+        uint32_t lv0, lv1;
+        Digit2(beta).pair((uint32_t)(dd[0] >> 32), (uint32_t)(dd[1] >> 32), lv0, lv1);
+        return (uint64_t)lv0 | ((uint64_t)lv1 << 32);
+    }
 #pragma unroll
     for (int half = 0; half < 2; half++) {
         const uint64_t d = dd[half];
@@ -1784,6 +1811,12 @@ __global__ void __launch_bounds__(1024) split_inv_digits_kernel(LargePbsLaunch a
         const bool neg0 = (jj0 < 0) != full_odd, neg1 = (jj0 + M < 0) != full_odd;
         const uint64_t d0 = (neg0 ? 0 - x0 : x0) - lo[b];
         const uint64_t d1 = (neg1 ? 0 - x1 : x1) - hi[b];
+        if (LARGE_DIGIT2 && a.base_log * 2 <= 30) {  // Digit2: the same words, 32-bit
+            uint32_t lv0, lv1;
+            Digit2(a.base_log).pair((uint32_t)(d0 >> 32), (uint32_t)(d1 >> 32), lv0, lv1);
+            dig[2 * j + row] = (uint64_t)lv0 | ((uint64_t)lv1 << 32);
+            continue;
+        }
         int32_t e0[2], e1[2];
         decompose64<2>(d0, a.base_log, e0);
         decompose64<2>(d1, a.base_log, e1);
@@ -2278,6 +2311,9 @@ static bool onchip_enabled() {
 #ifndef QUAD_PPOLL
 #define QUAD_PPOLL 1  // the R exchange flags polled by R lanes at once (0: lane 0 polls them in turn)
 #endif
+#ifndef QUAD_WPOLL
+#define QUAD_WPOLL 0  // 1: every wave polls the flags itself instead of wave 0 + a workgroup barrier
+#endif
 #ifndef QUAD_PKFENCE
 #define QUAD_PKFENCE 1  // the digits computed before the barrier that ends the rotation
 #endif
@@ -2564,9 +2600,10 @@ __global__ void __launch_bounds__(512, 1) quad_cmux_kernel(LargePbsLaunch a, int
         __syncthreads();  // U_q stored and drained by both storing waves
         stamp(i, 9);
         // ---- exchange: the R workgroups' U of CMUX i ----
-        if (QUAD_PPOLL && wave == 0) {
+        if (QUAD_PPOLL && (QUAD_WPOLL || wave == 0)) {
             // lanes 0..R-1 poll the R flags together: one L2 round trip per poll instead of R in turn
-            if (lane == 0)
+            // (QUAD_WPOLL: every wave polls for itself, so no workgroup barrier follows the wait)
+            if (wave == 0 && lane == 0)
                 __hip_atomic_store(flags + q * (Cfg::FLAG_BYTES / 4), (uint32_t)(i + 1), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             const uint32_t *f = flags + (lane < R ? lane : 0) * (Cfg::FLAG_BYTES / 4);
@@ -2594,7 +2631,7 @@ __global__ void __launch_bounds__(512, 1) quad_cmux_kernel(LargePbsLaunch a, int
                     __hip_atomic_store(a.quad_fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
-        __syncthreads();
+        if (!(QUAD_PPOLL && QUAD_WPOLL)) __syncthreads();
         stamp(i, 10);
         // ---- top DIT radix-4 of both columns, backward_add (large_top_inv), full width ----
         if (!QUAD_TPF) dit_tables();
