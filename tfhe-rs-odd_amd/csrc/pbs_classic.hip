@@ -31,6 +31,10 @@
 #include "engine.h"
 #include "pbs_common.h"
 
+#ifndef CLASSIC_DIGIT2
+#define CLASSIC_DIGIT2 1  // L = 2 shapes: Digit2 (pbs_common.h) instead of the per-level digit loop (0: A/B)
+#endif
+
 namespace tfhe_mi355 {
 
 #ifndef PBS_CPW
@@ -116,6 +120,7 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
     const int beta = a.base_log;
     const uint32_t dmask = (1u << beta) - 1;
     const DigitL1 digit_l1(beta);                      // L = 1 digits
+    const Digit2 digit2(L == 2 ? beta : 2);             // L = 2: both levels of a pair at once (2 beta <= 30)
     BlockSync sync;       // cross-wave: spectrum exchange
 #if PBS_WAVE_LOCAL
     WaveLocalSync wsync;  // wave-private buffer reuse
@@ -264,7 +269,11 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
             return (uint32_t)((r - c0[h]) >> 32);
         };
         uint32_t st[L > 1 ? 2 * V : 1];
-        if constexpr (L > 1) {
+        if constexpr (L == 2 && CLASSIC_DIGIT2) {
+            // st[b] = level-L int16 pair of positions (b, V + b), st[V + b] = level L-1 (Digit2)
+#pragma unroll
+            for (int b = 0; b < V; b++) digit2.pair(ct1_hi(b), ct1_hi(V + b), st[b], st[V + b]);
+        } else if constexpr (L > 1) {
 #pragma unroll
             for (int h = 0; h < 2 * V; h++) st[h] = decomp_state32_hi<L>(ct1_hi(h), beta);
         }
@@ -281,6 +290,10 @@ __global__ void __launch_bounds__((64 * (K + 1) * PbsConfig<N, K, L>::CPW), (Pbs
                 if constexpr (L == 1) {
                     d0 = digit_l1(ct1_hi(b));
                     d1 = digit_l1(ct1_hi(V + b));
+                } else if constexpr (L == 2 && CLASSIC_DIGIT2) {
+                    const uint32_t w = lvl == L ? st[b] : st[V + b];
+                    d0 = (int32_t)(int16_t)(w & 0xffffu);
+                    d1 = (int32_t)(int16_t)(w >> 16);
                 } else {
                     d0 = decomp_digit32(st[b], beta, dmask);
                     d1 = decomp_digit32(st[V + b], beta, dmask);
