@@ -66,6 +66,13 @@ for s in ${STAGES:-tests smoke bench}; do
           fi
           find gpurun_out/${TAGR:-r06}_kt_$t -name '*kernel_trace.csv' -delete
         done ;;
+    ktq) # kernel traces of single KS+PBS calls (1 and 64 rows) at each KTQ_PARAMS entry "PARAM_NAME:tag"
+        for v in ${KTQ_PARAMS:-PARAM_MESSAGE_3_CARRY_3_KS_PBS:quad}; do
+          n=${v#*:}
+          step ${TAGR:-r06}_kt_$n 300 env PROBE_PARAMS=${v%%:*} rocprofv3 --kernel-trace --stats \
+            -d gpurun_out/${TAGR:-r06}_kt_$n -o run --output-format csv -- python3 scripts/single_call_probe.py 5 1,64
+          find gpurun_out/${TAGR:-r06}_kt_$n -name '*kernel_trace.csv' -delete
+        done ;;
     pmc) for t in ${PMC_TAGS:-2_2}; do
            export ROUND=${TAGR:-r06}
            step ${TAGR:-r06}_pmc_$t 700 bash scripts/pmc_workload.sh $t
